@@ -1,0 +1,129 @@
+"""ctypes binding of ``librbc_gpu.so`` (include/rbc_gpu.h).
+
+The product path is the HIP library; there is no CPU fallback.  Importing
+this module without the built library raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librbc_gpu.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "rbc_gpu.h")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+        "(the RBC data path has no CPU fallback)")
+
+lib = ctypes.CDLL(LIB_PATH)
+
+u8p = POINTER(c_uint8)
+u32p = POINTER(c_uint32)
+i32p = POINTER(c_int32)
+szp = POINTER(c_size_t)
+u8pp = POINTER(u8p)
+
+_SIGS = {
+    "rbc_strerror": (c_char_p, [c_int]),
+    "rbc_abi_version": (c_int, []),
+    "rbc_device_count": (c_int, [POINTER(c_int)]),
+    "rbc_ctx_create": (c_int, [c_int, c_int, c_int, POINTER(c_void_p)]),
+    "rbc_ctx_destroy": (None, [c_void_p]),
+    "rbc_ctx_params": (c_int, [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_int)]),
+    "rbc_ctx_encode_matrix": (c_int, [c_void_p, c_void_p]),
+    "rbc_dev_malloc": (c_int, [c_int, c_size_t, POINTER(c_void_p)]),
+    "rbc_dev_free": (c_int, [c_void_p]),
+    "rbc_dev_memset": (c_int, [c_void_p, c_int, c_size_t]),
+    "rbc_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_size_t]),
+    "rbc_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_size_t]),
+    "rbc_host_alloc": (c_int, [c_size_t, POINTER(c_void_p)]),
+    "rbc_host_free": (c_int, [c_void_p]),
+    "rbc_stream_create": (c_int, [c_int, POINTER(c_void_p)]),
+    "rbc_stream_destroy": (c_int, [c_void_p]),
+    "rbc_stream_sync": (c_int, [c_void_p]),
+    "rbc_event_create": (c_int, [POINTER(c_void_p)]),
+    "rbc_event_destroy": (c_int, [c_void_p]),
+    "rbc_event_record": (c_int, [c_void_p, c_void_p]),
+    "rbc_event_elapsed_ms": (c_int, [c_void_p, c_void_p, POINTER(c_float)]),
+    "rbc_device_sync": (c_int, [c_int]),
+    "rbc_dev_encode": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_uint64, c_void_p, c_uint32, c_void_p,
+                               c_uint32]),
+    "rbc_dev_leaves": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_uint32, c_void_p, c_uint32, c_void_p]),
+    "rbc_dev_merkle_build": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "rbc_dev_shard_commit": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_uint64, c_void_p, c_uint32, c_void_p,
+                                     c_uint32, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rbc_dev_verify": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_uint32, c_void_p, c_uint32, c_void_p,
+                               c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rbc_dev_interpolate": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_uint32, c_void_p, c_uint32, c_void_p,
+                                    c_void_p, c_int, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p]),
+    "rbc_dev_inject_faults": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_uint32, c_void_p]),
+    "rbc_shard_commit": (c_int, [c_void_p, c_int, c_void_p, szp, c_void_p, c_size_t, u32p, c_void_p, c_void_p,
+                                 POINTER(c_uint64)]),
+    "rbc_validate_batch": (c_int, [c_void_p, c_int, c_void_p, szp, u32p, c_void_p, szp, c_void_p, c_void_p,
+                                   POINTER(c_uint64)]),
+    "rbc_interpolate_batch": (c_int, [c_void_p, c_int, c_void_p, c_size_t, szp, c_void_p, c_void_p, c_void_p,
+                                      c_size_t, c_void_p, i32p, POINTER(c_uint64)]),
+    "rbc_wait": (c_int, [c_void_p, c_uint64]),
+    "rbc_poll": (c_int, [c_void_p, c_uint64, POINTER(c_int)]),
+    "rbc_shard": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, szp, c_void_p, c_void_p]),
+    "rbc_validate_message": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_uint32,
+                                     POINTER(c_int)]),
+    "rbc_interpolate": (c_int, [c_void_p, c_void_p, c_void_p, szp, c_void_p, c_size_t, szp, c_void_p]),
+    "rbc_rs_new": (c_int, [c_int, c_int, c_int, POINTER(c_void_p)]),
+    "rbc_rs_free": (None, [c_void_p]),
+    "rbc_rs_encode": (c_int, [c_void_p, c_void_p, szp, c_int]),
+    "rbc_rs_verify": (c_int, [c_void_p, c_void_p, szp, c_int, POINTER(c_int)]),
+    "rbc_rs_reconstruct": (c_int, [c_void_p, c_void_p, szp, c_int]),
+    "rbc_rs_reconstruct_data": (c_int, [c_void_p, c_void_p, szp, c_int]),
+    "rbc_rs_split": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, szp]),
+    "rbc_rs_join": (c_int, [c_void_p, c_void_p, szp, c_int, c_size_t, c_void_p]),
+    "rbc_comm_unique_id": (c_int, [c_void_p]),
+    "rbc_comm_init": (c_int, [c_void_p, c_int, c_int, c_void_p]),
+    "rbc_comm_destroy": (c_int, [c_void_p]),
+    "rbc_dev_allgather_roots": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+}
+
+for _name, (_res, _args) in _SIGS.items():
+    _fn = getattr(lib, _name)
+    _fn.restype = _res
+    _fn.argtypes = _args
+
+
+def header_functions(path: str = HEADER_PATH):
+    """Every function the C-ABI header declares (for the export test)."""
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"\b(rbc_[a-z0-9_]+)\s*\(", text)
+    return sorted(set(names))
+
+
+# status codes (include/rbc_gpu.h)
+RBC_OK = 0
+RBC_ERR_INV_SHARD_NUM = -1
+RBC_ERR_MAX_SHARD_NUM = -2
+RBC_ERR_TOO_FEW_SHARDS = -3
+RBC_ERR_SHARD_NO_DATA = -4
+RBC_ERR_SHARD_SIZE = -5
+RBC_ERR_SHORT_DATA = -6
+RBC_ERR_RECONSTRUCT_REQUIRED = -7
+RBC_ERR_ROOT_MISMATCH = -8
+RBC_ERR_DEVICE = -9
+RBC_ERR_INVALID_ARG = -10
+RBC_ERR_SINGULAR = -11
+RBC_ERR_NO_COMM = -12
+
+
+class RBCError(Exception):
+    def __init__(self, code: int, where: str = ""):
+        self.code = code
+        msg = lib.rbc_strerror(code).decode()
+        super().__init__(f"{where}: {msg} ({code})" if where else f"{msg} ({code})")
+
+
+def check(code: int, where: str = "") -> None:
+    if code != RBC_OK:
+        raise RBCError(code, where)

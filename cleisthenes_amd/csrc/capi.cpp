@@ -1,0 +1,1046 @@
+// capi.cpp -- C++ host runtime behind include/rbc_gpu.h.
+//
+// Mirrors, on the host side, the interfaces the reference's rbc package
+// binds (rbc/rbc.go:20 `enc reedsolomon.Encoder`, shard/validateMessage/
+// interpolate at rbc/rbc.go:86-100) and drives the batched HIP kernels in
+// kernels.hip.  Argument checks and error values follow klauspost/reedsolomon
+// v1.9.1 (reedsolomon.go: New, Split, Encode, Verify, Reconstruct, Join).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+#include "../../include/rbc_gpu.h"
+#include "gf_host.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr size_t kAlign = 64;
+inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+int tree_width(int n) {
+    int w = 1;
+    while (w < n) w <<= 1;
+    return w;
+}
+int tree_depth(int n) {
+    int w = tree_width(n), d = 0;
+    while ((1 << d) < w) ++d;
+    return d;
+}
+
+#define RBC_HIP(expr)                                  \
+    do {                                               \
+        hipError_t e_ = (expr);                        \
+        if (e_ != hipSuccess) return RBC_ERR_DEVICE;   \
+    } while (0)
+
+// growable device / pinned buffer
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    bool pinned = false;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap && p) return hipSuccess;
+        release();
+        size_t want = std::max(bytes, (size_t)256);
+        hipError_t e = pinned ? hipHostMalloc(&p, want, hipHostMallocDefault) : hipMalloc(&p, want);
+        if (e != hipSuccess) { p = nullptr; cap = 0; return e; }
+        cap = want;
+        return hipSuccess;
+    }
+    void release() {
+        if (p) {
+            if (pinned) (void)hipHostFree(p);
+            else (void)hipFree(p);
+        }
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T> T *as() const { return reinterpret_cast<T *>(p); }
+};
+
+}  // namespace
+
+struct rbc_ctx {
+    int n = 0, f = 0, k = 0, p = 0, depth = 0, width = 0, device = 0;
+    std::vector<uint8_t> h_M;      // n x k encode matrix
+    uint8_t *d_M = nullptr;        // device copy; parity rows at d_M + k*k
+    std::mutex mu;
+    hipStream_t stream = nullptr;  // host-API stream
+    // interpolate workspace (device API)
+    DevBuf ws_used, ws_regen, ws_dmat;
+    // host-API staging
+    DevBuf d_values, d_shards, d_leaves, d_roots, d_branches, d_valid, d_status, d_digests, d_lens, d_slens,
+        d_idx, d_present;
+    DevBuf h_stage{nullptr, 0, true}, h_small{nullptr, 0, true};
+    uint64_t next_ticket = 1;
+    // RCCL
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+    DevBuf d_pack;
+};
+
+struct rbc_rs {
+    rbc_ctx *ctx = nullptr;
+};
+
+namespace {
+
+int ctx_create_kn(int n, int k, int device, rbc_ctx **out) {
+    if (!out) return RBC_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (k <= 0 || n - k < 0) return RBC_ERR_INV_SHARD_NUM;
+    if (n > 256) return RBC_ERR_MAX_SHARD_NUM;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return RBC_ERR_DEVICE;
+    rbc_ctx *c = new rbc_ctx();
+    c->n = n;
+    c->k = k;
+    c->p = n - k;
+    c->f = (n - k) / 2;
+    c->width = tree_width(n);
+    c->depth = tree_depth(n);
+    c->device = device;
+    if (!rbchost::build_matrix(k, n, c->h_M)) { delete c; return RBC_ERR_SINGULAR; }
+    if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->d_M, c->h_M.size()) != hipSuccess ||
+        hipMemcpy(c->d_M, c->h_M.data(), c->h_M.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        if (c->d_M) (void)hipFree(c->d_M);
+        delete c;
+        return RBC_ERR_DEVICE;
+    }
+    *out = c;
+    return RBC_OK;
+}
+
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ------------------------------------------------------------ stage bodies
+int stage_encode(rbc_ctx *c, hipStream_t st, int count, const uint8_t *values, uint64_t value_pitch,
+                 const uint32_t *value_lens, uint32_t uniform_value_len, uint8_t *shards, uint32_t shard_pitch) {
+    if (count < 0 || (count > 0 && (!values || !shards))) return RBC_ERR_INVALID_ARG;
+    if (shard_pitch == 0 || shard_pitch % kAlign) return RBC_ERR_INVALID_ARG;
+    if (!value_lens) {
+        if (uniform_value_len == 0) return RBC_ERR_SHORT_DATA;
+        const size_t S = (uniform_value_len + c->k - 1) / c->k;
+        if (S > shard_pitch || value_pitch < round_up((size_t)c->k * S, 16) + 16) return RBC_ERR_INVALID_ARG;
+    }
+    if (value_pitch > 0x7fffffffULL || (uint64_t)c->n * shard_pitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
+    if (count == 0) return RBC_OK;
+    GfArgs g{};
+    g.count = count;
+    g.tiles = (int)((shard_pitch + 4095) / 4096);
+    g.R = c->p;
+    g.K = c->k;
+    g.rc = rbc_gf_pick_rc(c->p > 0 ? c->p : 1);
+    g.mode = GF_MODE_ENCODE;
+    g.in = values;
+    g.in_inst_pitch = value_pitch;
+    g.in_inst_bytes = (uint32_t)value_pitch;
+    g.out = shards;
+    g.out_inst_pitch = (uint64_t)c->n * shard_pitch;
+    g.out_row_pitch = shard_pitch;
+    g.copy = shards;
+    g.lens = value_lens;
+    g.uniform_len = uniform_value_len;
+    g.coef = c->d_M + (size_t)c->k * c->k;
+    g.coef_inst_stride = 0;
+    RBC_HIP(rbc_launch_gf_rows(g, st));
+    return RBC_OK;
+}
+
+int stage_leaves(rbc_ctx *c, hipStream_t st, int count, const uint8_t *shards, uint32_t shard_pitch,
+                 const uint32_t *shard_lens, uint32_t uniform_shard_len, uint8_t *leaves) {
+    if (count < 0 || (count > 0 && (!shards || !leaves))) return RBC_ERR_INVALID_ARG;
+    if (shard_pitch % kAlign || (!shard_lens && (uniform_shard_len == 0 || uniform_shard_len > shard_pitch)))
+        return RBC_ERR_INVALID_ARG;
+    if (count == 0) return RBC_OK;
+    ShaArgs a{};
+    a.count = count;
+    a.rows_per_inst = c->n;
+    a.rows = shards;
+    a.inst_pitch = (uint64_t)c->n * shard_pitch;
+    a.row_pitch = shard_pitch;
+    a.lens = shard_lens;
+    a.uniform_len = uniform_shard_len;
+    a.leaves = leaves;
+    a.leaves_inst_pitch = (uint64_t)c->n * 32;
+    a.n = c->n;
+    a.depth = c->depth;
+    RBC_HIP(rbc_launch_sha_rows(a, false, st));
+    return RBC_OK;
+}
+
+int stage_merkle_build(rbc_ctx *c, hipStream_t st, int count, const uint8_t *leaves, uint8_t *roots,
+                       uint8_t *branches) {
+    if (count < 0 || (count > 0 && (!leaves || !roots))) return RBC_ERR_INVALID_ARG;
+    if (count == 0) return RBC_OK;
+    MerkleArgs m{};
+    m.count = count;
+    m.n = c->n;
+    m.width = c->width;
+    m.depth = c->depth;
+    m.k = c->k;
+    m.leaves = leaves;
+    m.leaves_inst_pitch = (uint64_t)c->n * 32;
+    m.roots = roots;
+    m.branches = c->depth > 0 ? branches : nullptr;
+    m.br_inst_pitch = (uint64_t)c->n * c->depth * 32;
+    RBC_HIP(rbc_launch_merkle(m, false, st));
+    return RBC_OK;
+}
+
+int stage_verify(rbc_ctx *c, hipStream_t st, int count, const uint8_t *shards, uint32_t shard_pitch,
+                 const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *branches,
+                 const uint8_t *roots, const uint8_t *present, uint8_t *valid, uint8_t *leaves) {
+    if (count < 0 || (count > 0 && (!shards || !roots || !valid || (c->depth > 0 && !branches))))
+        return RBC_ERR_INVALID_ARG;
+    if (shard_pitch % kAlign || (!shard_lens && (uniform_shard_len == 0 || uniform_shard_len > shard_pitch)))
+        return RBC_ERR_INVALID_ARG;
+    if (count == 0) return RBC_OK;
+    ShaArgs a{};
+    a.count = count;
+    a.rows_per_inst = c->n;
+    a.rows = shards;
+    a.inst_pitch = (uint64_t)c->n * shard_pitch;
+    a.row_pitch = shard_pitch;
+    a.lens = shard_lens;
+    a.uniform_len = uniform_shard_len;
+    a.leaves = leaves;
+    a.leaves_inst_pitch = (uint64_t)c->n * 32;
+    a.n = c->n;
+    a.depth = c->depth;
+    a.branches = branches;
+    a.br_inst_pitch = (uint64_t)c->n * c->depth * 32;
+    a.roots = roots;
+    a.present = present;
+    a.valid = valid;
+    RBC_HIP(rbc_launch_sha_rows(a, true, st));
+    return RBC_OK;
+}
+
+int ensure_ws(rbc_ctx *c, int count) {
+    const size_t nr = (size_t)std::max(c->n - c->k, 1);
+    RBC_HIP(c->ws_used.ensure((size_t)count * c->k));
+    RBC_HIP(c->ws_regen.ensure((size_t)count * nr));
+    RBC_HIP(c->ws_dmat.ensure((size_t)count * nr * c->k));
+    return RBC_OK;
+}
+
+// decode_prepare + GF regeneration (in place), no hashing
+int stage_regenerate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, uint32_t shard_pitch,
+                     const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *valid,
+                     int32_t *status) {
+    int rc = ensure_ws(c, count);
+    if (rc) return rc;
+    const int nr = c->n - c->k;
+    PrepArgs pa{};
+    pa.count = count;
+    pa.n = c->n;
+    pa.k = c->k;
+    pa.valid = valid;
+    pa.valid_stride = (uint32_t)c->n;
+    pa.M = c->d_M;
+    pa.used = c->ws_used.as<uint8_t>();
+    pa.used_stride = (uint32_t)c->k;
+    pa.regen = c->ws_regen.as<uint8_t>();
+    pa.regen_stride = (uint32_t)std::max(nr, 1);
+    pa.dmat = c->ws_dmat.as<uint8_t>();
+    pa.dmat_stride = (uint64_t)std::max(nr, 1) * c->k;
+    pa.status = status;
+    RBC_HIP(rbc_launch_decode_prepare(pa, st));
+    if (nr > 0) {
+        GfArgs g{};
+        g.count = count;
+        g.tiles = (int)((shard_pitch + 4095) / 4096);
+        g.R = nr;
+        g.K = c->k;
+        g.rc = rbc_gf_pick_rc(nr);
+        g.mode = GF_MODE_DECODE;
+        g.in = shards;
+        g.in_inst_pitch = (uint64_t)c->n * shard_pitch;
+        g.in_row_pitch = shard_pitch;
+        g.in_inst_bytes = (uint32_t)((uint64_t)c->n * shard_pitch);
+        g.out = shards;
+        g.out_inst_pitch = (uint64_t)c->n * shard_pitch;
+        g.out_row_pitch = shard_pitch;
+        g.copy = nullptr;
+        g.lens = shard_lens;
+        g.uniform_len = uniform_shard_len;
+        g.coef = pa.dmat;
+        g.coef_inst_stride = pa.dmat_stride;
+        g.in_idx = pa.used;
+        g.out_idx = pa.regen;
+        g.idx_stride = pa.used_stride;
+        g.idx_stride2 = pa.regen_stride;
+        g.status = status;
+        RBC_HIP(rbc_launch_gf_rows(g, st));
+    }
+    return RBC_OK;
+}
+
+int stage_interpolate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, uint32_t shard_pitch,
+                      const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *valid, uint8_t *leaves,
+                      int leaves_verified, const uint8_t *roots, uint8_t *values_out, uint32_t value_pitch,
+                      uint8_t *digests, int32_t *status) {
+    if (count < 0 || (count > 0 && (!shards || !valid || !leaves || !roots || !values_out || !status)))
+        return RBC_ERR_INVALID_ARG;
+    if (shard_pitch % kAlign || value_pitch % 16) return RBC_ERR_INVALID_ARG;
+    if (!shard_lens && (uniform_shard_len == 0 || uniform_shard_len > shard_pitch ||
+                        value_pitch < (uint64_t)uniform_shard_len * c->k))
+        return RBC_ERR_INVALID_ARG;
+    if ((uint64_t)c->n * shard_pitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
+    if (count == 0) return RBC_OK;
+    int rc = stage_regenerate(c, st, count, shards, shard_pitch, shard_lens, uniform_shard_len, valid, status);
+    if (rc) return rc;
+    const int nr = c->n - c->k;
+    ShaArgs a{};
+    a.count = count;
+    a.rows = shards;
+    a.inst_pitch = (uint64_t)c->n * shard_pitch;
+    a.row_pitch = shard_pitch;
+    a.lens = shard_lens;
+    a.uniform_len = uniform_shard_len;
+    a.status = status;
+    a.leaves = leaves;
+    a.leaves_inst_pitch = (uint64_t)c->n * 32;
+    a.n = c->n;
+    a.depth = c->depth;
+    if (leaves_verified) {
+        a.rows_per_inst = nr;
+        a.idx = c->ws_regen.as<uint8_t>();
+        a.idx_stride = (uint32_t)std::max(nr, 1);
+    } else {
+        a.rows_per_inst = c->n;
+    }
+    if (a.rows_per_inst > 0) RBC_HIP(rbc_launch_sha_rows(a, false, st));
+    MerkleArgs m{};
+    m.count = count;
+    m.n = c->n;
+    m.width = c->width;
+    m.depth = c->depth;
+    m.k = c->k;
+    m.leaves = leaves;
+    m.leaves_inst_pitch = (uint64_t)c->n * 32;
+    m.expect_roots = roots;
+    m.status = status;
+    m.digests = digests;
+    RBC_HIP(rbc_launch_merkle(m, true, st));
+    JoinArgs j{};
+    j.count = count;
+    j.k = c->k;
+    j.chunks = value_pitch / 16;
+    j.shards = shards;
+    j.inst_pitch = (uint64_t)c->n * shard_pitch;
+    j.row_pitch = shard_pitch;
+    j.inst_bytes = (uint32_t)((uint64_t)c->n * shard_pitch);
+    j.lens = shard_lens;
+    j.uniform_len = uniform_shard_len;
+    j.values = values_out;
+    j.value_pitch = value_pitch;
+    j.status = status;
+    RBC_HIP(rbc_launch_join(j, st));
+    return RBC_OK;
+}
+
+// klauspost checkShards / shardSize (reedsolomon.go)
+int check_shards(const size_t *lens, int n, bool nilok, size_t *size_out) {
+    size_t size = 0;
+    for (int i = 0; i < n; ++i)
+        if (lens[i]) { size = lens[i]; break; }
+    if (size == 0) return RBC_ERR_SHARD_NO_DATA;
+    for (int i = 0; i < n; ++i)
+        if (lens[i] != size && (lens[i] != 0 || !nilok)) return RBC_ERR_SHARD_SIZE;
+    *size_out = size;
+    return RBC_OK;
+}
+
+// Regenerate on the GPU every non-used position of one codeword held in host
+// buffers; copy back only the rows the caller asks for.
+int host_reconstruct(rbc_ctx *c, uint8_t *const *shards, size_t *lens, int n_shards, bool data_only) {
+    if (!shards || !lens) return RBC_ERR_INVALID_ARG;
+    if (n_shards != c->n) return RBC_ERR_TOO_FEW_SHARDS;
+    size_t S = 0;
+    int rc = check_shards(lens, n_shards, true, &S);
+    if (rc) return rc;
+    int present = 0;
+    for (int i = 0; i < c->n; ++i) present += lens[i] != 0;
+    if (present == c->n) return RBC_OK;
+    if (present < c->k) return RBC_ERR_TOO_FEW_SHARDS;
+    if (S > 0x7fffffffULL / (size_t)c->n) return RBC_ERR_INVALID_ARG;
+    const size_t pitch = round_up(S, kAlign);
+    std::lock_guard<std::mutex> lk(c->mu);
+    RBC_HIP(hipSetDevice(c->device));
+    RBC_HIP(c->d_shards.ensure((size_t)c->n * pitch));
+    RBC_HIP(c->d_valid.ensure((size_t)c->n));
+    RBC_HIP(c->d_status.ensure(sizeof(int32_t)));
+    RBC_HIP(c->h_stage.ensure((size_t)c->n * pitch + c->n));
+    uint8_t *stage = c->h_stage.as<uint8_t>();
+    memset(stage, 0, (size_t)c->n * pitch + c->n);
+    for (int i = 0; i < c->n; ++i) {
+        if (lens[i]) memcpy(stage + (size_t)i * pitch, shards[i], S);
+        stage[(size_t)c->n * pitch + i] = lens[i] ? 1 : 0;
+    }
+    hipStream_t st = c->stream;
+    RBC_HIP(hipMemcpyAsync(c->d_shards.p, stage, (size_t)c->n * pitch, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(c->d_valid.p, stage + (size_t)c->n * pitch, c->n, hipMemcpyHostToDevice, st));
+    rc = stage_regenerate(c, st, 1, c->d_shards.as<uint8_t>(), (uint32_t)pitch, nullptr, (uint32_t)S,
+                          c->d_valid.as<uint8_t>(), c->d_status.as<int32_t>());
+    if (rc) return rc;
+    RBC_HIP(hipMemcpyAsync(stage, c->d_shards.p, (size_t)c->n * pitch, hipMemcpyDeviceToHost, st));
+    int32_t status = 0;
+    RBC_HIP(hipMemcpyAsync(&status, c->d_status.p, sizeof status, hipMemcpyDeviceToHost, st));
+    RBC_HIP(hipStreamSynchronize(st));
+    if (status) return status;
+    const int last = data_only ? c->k : c->n;
+    for (int i = 0; i < last; ++i) {
+        if (lens[i]) continue;
+        if (!shards[i]) return RBC_ERR_INVALID_ARG;
+        memcpy(shards[i], stage + (size_t)i * pitch, S);
+        lens[i] = S;
+    }
+    return RBC_OK;
+}
+
+}  // namespace
+
+// =========================================================================
+extern "C" {
+
+const char *rbc_strerror(int s) {
+    switch (s) {
+        case RBC_OK: return "ok";
+        case RBC_ERR_INV_SHARD_NUM: return "cannot create Encoder with zero or less data/parity shards";
+        case RBC_ERR_MAX_SHARD_NUM: return "cannot create Encoder with more than 256 data+parity shards";
+        case RBC_ERR_TOO_FEW_SHARDS: return "too few shards given";
+        case RBC_ERR_SHARD_NO_DATA: return "no shard data";
+        case RBC_ERR_SHARD_SIZE: return "shard sizes do not match";
+        case RBC_ERR_SHORT_DATA: return "not enough data to fill the number of requested shards";
+        case RBC_ERR_RECONSTRUCT_REQUIRED:
+            return "reconstruction required as one or more required data shards are nil";
+        case RBC_ERR_ROOT_MISMATCH: return "interpolated merkle root does not match the committed root";
+        case RBC_ERR_DEVICE: return "HIP/RCCL device error";
+        case RBC_ERR_INVALID_ARG: return "invalid argument";
+        case RBC_ERR_SINGULAR: return "matrix is singular";
+        case RBC_ERR_NO_COMM: return "multi-GPU communicator not initialised";
+        default: return "unknown rbc status";
+    }
+}
+
+int rbc_abi_version(void) { return RBC_ABI_VERSION; }
+
+int rbc_device_count(int *count) {
+    if (!count) return RBC_ERR_INVALID_ARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return RBC_OK;
+}
+
+int rbc_ctx_create(int n, int f, int device, rbc_ctx **out) {
+    if (f < 0 || n - 2 * f <= 0) return RBC_ERR_INV_SHARD_NUM;
+    return ctx_create_kn(n, n - 2 * f, device, out);
+}
+
+void rbc_ctx_destroy(rbc_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    for (DevBuf *b : {&c->ws_used, &c->ws_regen, &c->ws_dmat, &c->d_values, &c->d_shards, &c->d_leaves,
+                      &c->d_roots, &c->d_branches, &c->d_valid, &c->d_status, &c->d_digests, &c->d_lens,
+                      &c->d_slens, &c->d_idx, &c->d_present, &c->h_stage, &c->h_small, &c->d_pack})
+        b->release();
+    if (c->d_M) (void)hipFree(c->d_M);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int rbc_ctx_params(const rbc_ctx *c, int *k, int *p, int *depth) {
+    if (!c) return RBC_ERR_INVALID_ARG;
+    if (k) *k = c->k;
+    if (p) *p = c->p;
+    if (depth) *depth = c->depth;
+    return RBC_OK;
+}
+
+int rbc_ctx_encode_matrix(const rbc_ctx *c, uint8_t *out) {
+    if (!c || !out) return RBC_ERR_INVALID_ARG;
+    memcpy(out, c->h_M.data(), c->h_M.size());
+    return RBC_OK;
+}
+
+// ---- memory / streams / events
+int rbc_dev_malloc(int device, size_t bytes, void **ptr) {
+    if (!ptr) return RBC_ERR_INVALID_ARG;
+    RBC_HIP(hipSetDevice(device));
+    RBC_HIP(hipMalloc(ptr, bytes ? bytes : 1));
+    return RBC_OK;
+}
+int rbc_dev_free(void *ptr) { RBC_HIP(hipFree(ptr)); return RBC_OK; }
+int rbc_dev_memset(void *ptr, int value, size_t bytes) { RBC_HIP(hipMemset(ptr, value, bytes)); return RBC_OK; }
+int rbc_memcpy_h2d(void *dst, const void *src, size_t bytes) {
+    RBC_HIP(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return RBC_OK;
+}
+int rbc_memcpy_d2h(void *dst, const void *src, size_t bytes) {
+    RBC_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return RBC_OK;
+}
+int rbc_host_alloc(size_t bytes, void **ptr) {
+    if (!ptr) return RBC_ERR_INVALID_ARG;
+    RBC_HIP(hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocDefault));
+    return RBC_OK;
+}
+int rbc_host_free(void *ptr) { RBC_HIP(hipHostFree(ptr)); return RBC_OK; }
+int rbc_stream_create(int device, void **stream) {
+    if (!stream) return RBC_ERR_INVALID_ARG;
+    RBC_HIP(hipSetDevice(device));
+    hipStream_t s;
+    RBC_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *stream = s;
+    return RBC_OK;
+}
+int rbc_stream_destroy(void *stream) { RBC_HIP(hipStreamDestroy(as_stream(stream))); return RBC_OK; }
+int rbc_stream_sync(void *stream) { RBC_HIP(hipStreamSynchronize(as_stream(stream))); return RBC_OK; }
+int rbc_event_create(void **event) {
+    if (!event) return RBC_ERR_INVALID_ARG;
+    hipEvent_t e;
+    RBC_HIP(hipEventCreate(&e));
+    *event = e;
+    return RBC_OK;
+}
+int rbc_event_destroy(void *event) { RBC_HIP(hipEventDestroy((hipEvent_t)event)); return RBC_OK; }
+int rbc_event_record(void *event, void *stream) {
+    RBC_HIP(hipEventRecord((hipEvent_t)event, as_stream(stream)));
+    return RBC_OK;
+}
+int rbc_event_elapsed_ms(void *start, void *stop, float *ms) {
+    if (!ms) return RBC_ERR_INVALID_ARG;
+    RBC_HIP(hipEventSynchronize((hipEvent_t)stop));
+    RBC_HIP(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
+    return RBC_OK;
+}
+int rbc_device_sync(int device) {
+    RBC_HIP(hipSetDevice(device));
+    RBC_HIP(hipDeviceSynchronize());
+    return RBC_OK;
+}
+
+// ---- device-resident stages
+int rbc_dev_encode(rbc_ctx *c, void *stream, int count, const uint8_t *values, uint64_t value_pitch,
+                   const uint32_t *value_lens, uint32_t uniform_value_len, uint8_t *shards, uint32_t shard_pitch) {
+    if (!c) return RBC_ERR_INVALID_ARG;
+    RBC_HIP(hipSetDevice(c->device));
+    return stage_encode(c, as_stream(stream), count, values, value_pitch, value_lens, uniform_value_len, shards,
+                        shard_pitch);
+}
+
+int rbc_dev_leaves(rbc_ctx *c, void *stream, int count, const uint8_t *shards, uint32_t shard_pitch,
+                   const uint32_t *shard_lens, uint32_t uniform_shard_len, uint8_t *leaves) {
+    if (!c) return RBC_ERR_INVALID_ARG;
+    RBC_HIP(hipSetDevice(c->device));
+    return stage_leaves(c, as_stream(stream), count, shards, shard_pitch, shard_lens, uniform_shard_len, leaves);
+}
+
+int rbc_dev_merkle_build(rbc_ctx *c, void *stream, int count, const uint8_t *leaves, uint8_t *roots,
+                         uint8_t *branches) {
+    if (!c) return RBC_ERR_INVALID_ARG;
+    RBC_HIP(hipSetDevice(c->device));
+    return stage_merkle_build(c, as_stream(stream), count, leaves, roots, branches);
+}
+
+int rbc_dev_shard_commit(rbc_ctx *c, void *stream, int count, const uint8_t *values, uint64_t value_pitch,
+                         const uint32_t *value_lens, uint32_t uniform_value_len, uint8_t *shards,
+                         uint32_t shard_pitch, const uint32_t *shard_lens, uint8_t *leaves, uint8_t *roots,
+                         uint8_t *branches) {
+    if (!c) return RBC_ERR_INVALID_ARG;
+    if (value_lens && !shard_lens) return RBC_ERR_INVALID_ARG;
+    RBC_HIP(hipSetDevice(c->device));
+    hipStream_t st = as_stream(stream);
+    int rc = stage_encode(c, st, count, values, value_pitch, value_lens, uniform_value_len, shards, shard_pitch);
+    if (rc) return rc;
+    const uint32_t uS = value_lens ? 0u : (uniform_value_len + c->k - 1) / c->k;
+    rc = stage_leaves(c, st, count, shards, shard_pitch, shard_lens, uS, leaves);
+    if (rc) return rc;
+    return stage_merkle_build(c, st, count, leaves, roots, branches);
+}
+
+int rbc_dev_verify(rbc_ctx *c, void *stream, int count, const uint8_t *shards, uint32_t shard_pitch,
+                   const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *branches,
+                   const uint8_t *roots, const uint8_t *present, uint8_t *valid, uint8_t *leaves) {
+    if (!c) return RBC_ERR_INVALID_ARG;
+    RBC_HIP(hipSetDevice(c->device));
+    return stage_verify(c, as_stream(stream), count, shards, shard_pitch, shard_lens, uniform_shard_len, branches,
+                        roots, present, valid, leaves);
+}
+
+int rbc_dev_interpolate(rbc_ctx *c, void *stream, int count, uint8_t *shards, uint32_t shard_pitch,
+                        const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *valid,
+                        uint8_t *leaves, int leaves_verified, const uint8_t *roots, uint8_t *values_out,
+                        uint32_t value_pitch, uint8_t *digests, int32_t *status) {
+    if (!c) return RBC_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);  // shared decode workspace
+    RBC_HIP(hipSetDevice(c->device));
+    return stage_interpolate(c, as_stream(stream), count, shards, shard_pitch, shard_lens, uniform_shard_len, valid,
+                             leaves, leaves_verified, roots, values_out, value_pitch, digests, status);
+}
+
+int rbc_dev_inject_faults(rbc_ctx *c, void *stream, int count, uint8_t *shards, uint32_t shard_pitch,
+                          const int32_t *corrupt) {
+    if (!c || count < 0 || (count > 0 && (!shards || !corrupt))) return RBC_ERR_INVALID_ARG;
+    RBC_HIP(hipSetDevice(c->device));
+    RBC_HIP(rbc_launch_inject_faults(shards, (uint64_t)c->n * shard_pitch, shard_pitch, corrupt, count,
+                                     as_stream(stream)));
+    return RBC_OK;
+}
+
+// ---- host-memory batch API
+int rbc_shard_commit(rbc_ctx *c, int count, const uint8_t *const *values, const size_t *value_lens,
+                     uint8_t *shards_out, size_t shard_pitch, uint32_t *shard_lens_out, uint8_t *roots_out,
+                     uint8_t *branches_out, uint64_t *ticket) {
+    if (!c || count < 0 || (count > 0 && (!values || !value_lens || !shards_out || !roots_out)))
+        return RBC_ERR_INVALID_ARG;
+    if (count == 0) { if (ticket) *ticket = 0; return RBC_OK; }
+    size_t Smax = 0;
+    for (int i = 0; i < count; ++i) {
+        if (value_lens[i] == 0) return RBC_ERR_SHORT_DATA;  // Split: len(data) == 0
+        if (!values[i]) return RBC_ERR_INVALID_ARG;
+        Smax = std::max(Smax, (value_lens[i] + c->k - 1) / c->k);
+    }
+    if (shard_pitch < Smax) return RBC_ERR_INVALID_ARG;
+    const size_t dpitch = round_up(Smax, kAlign);
+    const size_t vpitch = round_up((size_t)c->k * Smax + 32, kAlign);
+    if (vpitch > 0x7fffffffULL || (size_t)c->n * dpitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    RBC_HIP(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    RBC_HIP(c->d_values.ensure((size_t)count * vpitch));
+    RBC_HIP(c->d_shards.ensure((size_t)count * c->n * dpitch));
+    RBC_HIP(c->d_leaves.ensure((size_t)count * c->n * 32));
+    RBC_HIP(c->d_roots.ensure((size_t)count * 32));
+    RBC_HIP(c->d_branches.ensure((size_t)count * c->n * std::max(c->depth, 1) * 32));
+    RBC_HIP(c->d_lens.ensure((size_t)count * 4));
+    RBC_HIP(c->d_slens.ensure((size_t)count * 4));
+    RBC_HIP(c->h_stage.ensure((size_t)count * vpitch));
+    RBC_HIP(c->h_small.ensure((size_t)count * 8));
+    uint8_t *stage = c->h_stage.as<uint8_t>();
+    uint32_t *lens = c->h_small.as<uint32_t>();
+    for (int i = 0; i < count; ++i) {
+        memcpy(stage + (size_t)i * vpitch, values[i], value_lens[i]);
+        memset(stage + (size_t)i * vpitch + value_lens[i], 0, vpitch - value_lens[i]);
+        lens[i] = (uint32_t)value_lens[i];
+        lens[count + i] = (uint32_t)((value_lens[i] + c->k - 1) / c->k);
+    }
+    RBC_HIP(hipMemcpyAsync(c->d_values.p, stage, (size_t)count * vpitch, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(c->d_lens.p, lens, (size_t)count * 4, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(c->d_slens.p, lens + count, (size_t)count * 4, hipMemcpyHostToDevice, st));
+    int rc = stage_encode(c, st, count, c->d_values.as<uint8_t>(), vpitch, c->d_lens.as<uint32_t>(), 0,
+                          c->d_shards.as<uint8_t>(), (uint32_t)dpitch);
+    if (!rc) rc = stage_leaves(c, st, count, c->d_shards.as<uint8_t>(), (uint32_t)dpitch, c->d_slens.as<uint32_t>(),
+                               0, c->d_leaves.as<uint8_t>());
+    if (!rc) rc = stage_merkle_build(c, st, count, c->d_leaves.as<uint8_t>(), c->d_roots.as<uint8_t>(),
+                                     c->d_branches.as<uint8_t>());
+    if (rc) return rc;
+    RBC_HIP(hipMemcpy2DAsync(shards_out, shard_pitch, c->d_shards.p, dpitch, Smax, (size_t)count * c->n,
+                             hipMemcpyDeviceToHost, st));
+    RBC_HIP(hipMemcpyAsync(roots_out, c->d_roots.p, (size_t)count * 32, hipMemcpyDeviceToHost, st));
+    if (branches_out && c->depth > 0)
+        RBC_HIP(hipMemcpyAsync(branches_out, c->d_branches.p, (size_t)count * c->n * c->depth * 32,
+                               hipMemcpyDeviceToHost, st));
+    RBC_HIP(hipStreamSynchronize(st));
+    if (shard_lens_out)
+        for (int i = 0; i < count; ++i) shard_lens_out[i] = lens[count + i];
+    if (ticket) *ticket = c->next_ticket++;
+    return RBC_OK;
+}
+
+int rbc_validate_batch(rbc_ctx *c, int count, const uint8_t *const *shards, const size_t *shard_lens,
+                       const uint32_t *indices, const uint8_t *const *branches, const size_t *branch_lens,
+                       const uint8_t *const *roots, uint8_t *ok_out, uint64_t *ticket) {
+    if (!c || count < 0 ||
+        (count > 0 && (!shards || !shard_lens || !indices || !branches || !branch_lens || !roots || !ok_out)))
+        return RBC_ERR_INVALID_ARG;
+    if (count == 0) { if (ticket) *ticket = 0; return RBC_OK; }
+    const int d = c->depth;
+    size_t Smax = 1;
+    for (int i = 0; i < count; ++i) Smax = std::max(Smax, shard_lens[i]);
+    const size_t pitch = round_up(Smax, kAlign);
+    const size_t bslot = (size_t)std::max(d, 1) * 32;
+    std::lock_guard<std::mutex> lk(c->mu);
+    RBC_HIP(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    const size_t stage_bytes = (size_t)count * (pitch + bslot + 32 + 4 + 1);
+    RBC_HIP(c->h_stage.ensure(stage_bytes));
+    RBC_HIP(c->d_shards.ensure((size_t)count * pitch));
+    RBC_HIP(c->d_branches.ensure((size_t)count * bslot));
+    RBC_HIP(c->d_roots.ensure((size_t)count * 32));
+    RBC_HIP(c->d_slens.ensure((size_t)count * 4));
+    RBC_HIP(c->d_idx.ensure((size_t)count));
+    RBC_HIP(c->d_valid.ensure((size_t)count));
+    uint8_t *sh = c->h_stage.as<uint8_t>();
+    uint8_t *br = sh + (size_t)count * pitch;
+    uint8_t *rt = br + (size_t)count * bslot;
+    uint32_t *ln = reinterpret_cast<uint32_t *>(rt + (size_t)count * 32);
+    uint8_t *ix = reinterpret_cast<uint8_t *>(ln + count);
+    std::vector<uint8_t> shape_ok(count, 1);
+    memset(sh, 0, stage_bytes);
+    for (int i = 0; i < count; ++i) {
+        const uint32_t j = indices[i];
+        // unflatten the Go-form branch (the empty level-0 sibling is omitted)
+        const bool empty0 = d > 0 && (int)(j ^ 1u) >= c->n;
+        const size_t want = (size_t)32 * (d - (empty0 ? 1 : 0));
+        if ((int)j >= c->n || branch_lens[i] != want || shard_lens[i] == 0 || !shards[i] || !roots[i] ||
+            (want && !branches[i])) {
+            shape_ok[i] = 0;
+            ln[i] = 1;
+            ix[i] = 0;
+            continue;
+        }
+        memcpy(sh + (size_t)i * pitch, shards[i], shard_lens[i]);
+        size_t off = 0;
+        for (int l = 0; l < d; ++l) {
+            if (l == 0 && empty0) continue;
+            memcpy(br + (size_t)i * bslot + 32 * l, branches[i] + off, 32);
+            off += 32;
+        }
+        memcpy(rt + 32 * i, roots[i], 32);
+        ln[i] = (uint32_t)shard_lens[i];
+        ix[i] = (uint8_t)j;
+    }
+    RBC_HIP(hipMemcpyAsync(c->d_shards.p, sh, (size_t)count * pitch, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(c->d_branches.p, br, (size_t)count * bslot, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(c->d_roots.p, rt, (size_t)count * 32, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(c->d_slens.p, ln, (size_t)count * 4, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(c->d_idx.p, ix, (size_t)count, hipMemcpyHostToDevice, st));
+    ShaArgs a{};
+    a.count = count;
+    a.rows_per_inst = 1;
+    a.rows = c->d_shards.as<uint8_t>();
+    a.inst_pitch = pitch;
+    a.row_pitch = 0;
+    a.lens = c->d_slens.as<uint32_t>();
+    a.idx = c->d_idx.as<uint8_t>();
+    a.idx_stride = 1;
+    a.per_message = 1;
+    a.n = c->n;
+    a.depth = d;
+    a.branches = c->d_branches.as<uint8_t>();
+    a.br_inst_pitch = bslot;
+    a.roots = c->d_roots.as<uint8_t>();
+    a.valid = c->d_valid.as<uint8_t>();
+    RBC_HIP(rbc_launch_sha_rows(a, true, st));
+    RBC_HIP(hipMemcpyAsync(ok_out, c->d_valid.p, (size_t)count, hipMemcpyDeviceToHost, st));
+    RBC_HIP(hipStreamSynchronize(st));
+    for (int i = 0; i < count; ++i)
+        if (!shape_ok[i]) ok_out[i] = 0;
+    if (ticket) *ticket = c->next_ticket++;
+    return RBC_OK;
+}
+
+int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t shard_pitch,
+                          const size_t *shard_lens, const uint8_t *present, const uint8_t *roots,
+                          uint8_t *values_out, size_t value_pitch, uint8_t *digests_out, int32_t *status_out,
+                          uint64_t *ticket) {
+    if (!c || count < 0 ||
+        (count > 0 && (!shards || !shard_lens || !present || !roots || !values_out || !status_out)))
+        return RBC_ERR_INVALID_ARG;
+    if (count == 0) { if (ticket) *ticket = 0; return RBC_OK; }
+    size_t Smax = 1;
+    for (int i = 0; i < count; ++i) {
+        if (shard_lens[i] > shard_pitch) return RBC_ERR_INVALID_ARG;
+        Smax = std::max(Smax, shard_lens[i]);
+    }
+    if (value_pitch < (size_t)c->k * Smax) return RBC_ERR_INVALID_ARG;
+    const size_t dpitch = round_up(Smax, kAlign);
+    const size_t vpitch = round_up((size_t)c->k * Smax, 16);
+    if ((size_t)c->n * dpitch > 0x7fffffffULL || vpitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    RBC_HIP(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    RBC_HIP(c->d_shards.ensure((size_t)count * c->n * dpitch));
+    RBC_HIP(c->d_valid.ensure((size_t)count * c->n));
+    RBC_HIP(c->d_leaves.ensure((size_t)count * c->n * 32));
+    RBC_HIP(c->d_roots.ensure((size_t)count * 32));
+    RBC_HIP(c->d_values.ensure((size_t)count * vpitch));
+    RBC_HIP(c->d_digests.ensure((size_t)count * 32));
+    RBC_HIP(c->d_status.ensure((size_t)count * 4));
+    RBC_HIP(c->d_slens.ensure((size_t)count * 4));
+    RBC_HIP(c->h_small.ensure((size_t)count * 4));
+    uint32_t *ln = c->h_small.as<uint32_t>();
+    for (int i = 0; i < count; ++i) ln[i] = (uint32_t)shard_lens[i];
+    RBC_HIP(hipMemcpy2DAsync(c->d_shards.p, dpitch, shards, shard_pitch, Smax, (size_t)count * c->n,
+                             hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(c->d_valid.p, present, (size_t)count * c->n, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(c->d_roots.p, roots, (size_t)count * 32, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(c->d_slens.p, ln, (size_t)count * 4, hipMemcpyHostToDevice, st));
+    int rc = stage_interpolate(c, st, count, c->d_shards.as<uint8_t>(), (uint32_t)dpitch, c->d_slens.as<uint32_t>(),
+                               0, c->d_valid.as<uint8_t>(), c->d_leaves.as<uint8_t>(), 0, c->d_roots.as<uint8_t>(),
+                               c->d_values.as<uint8_t>(), (uint32_t)vpitch, c->d_digests.as<uint8_t>(),
+                               c->d_status.as<int32_t>());
+    if (rc) return rc;
+    RBC_HIP(hipMemcpyAsync(status_out, c->d_status.p, (size_t)count * 4, hipMemcpyDeviceToHost, st));
+    RBC_HIP(hipMemcpy2DAsync(values_out, value_pitch, c->d_values.p, vpitch, (size_t)c->k * Smax, count,
+                             hipMemcpyDeviceToHost, st));
+    if (digests_out)
+        RBC_HIP(hipMemcpyAsync(digests_out, c->d_digests.p, (size_t)count * 32, hipMemcpyDeviceToHost, st));
+    RBC_HIP(hipStreamSynchronize(st));
+    if (ticket) *ticket = c->next_ticket++;
+    return RBC_OK;
+}
+
+// Round 1: host-API submissions complete before returning (tickets are
+// already done); rbc_wait/rbc_poll keep the Go batcher's contract stable.
+int rbc_wait(rbc_ctx *c, uint64_t ticket) {
+    if (!c || ticket >= c->next_ticket) return RBC_ERR_INVALID_ARG;
+    return RBC_OK;
+}
+int rbc_poll(rbc_ctx *c, uint64_t ticket, int *done) {
+    if (!c || !done || ticket >= c->next_ticket) return RBC_ERR_INVALID_ARG;
+    *done = 1;
+    return RBC_OK;
+}
+
+// ---- single-call drop-ins
+int rbc_shard(rbc_ctx *c, const uint8_t *data, size_t len, uint8_t *shards_out, size_t shards_cap,
+              size_t *shard_len_out, uint8_t *root_out, uint8_t *branches_out) {
+    if (!c || !shards_out || !root_out) return RBC_ERR_INVALID_ARG;
+    if (len == 0) return RBC_ERR_SHORT_DATA;
+    if (!data) return RBC_ERR_INVALID_ARG;
+    const size_t S = (len + c->k - 1) / c->k;
+    if (shards_cap < (size_t)c->n * S) return RBC_ERR_INVALID_ARG;
+    uint32_t slen = 0;
+    uint64_t t = 0;
+    int rc = rbc_shard_commit(c, 1, &data, &len, shards_out, S, &slen, root_out, branches_out, &t);
+    if (rc) return rc;
+    if (shard_len_out) *shard_len_out = slen;
+    return RBC_OK;
+}
+
+int rbc_validate_message(rbc_ctx *c, const uint8_t *root, const uint8_t *branch, size_t branch_len,
+                         const uint8_t *shard, size_t shard_len, uint32_t index, int *ok) {
+    if (!c || !ok || !root) return RBC_ERR_INVALID_ARG;
+    *ok = 0;
+    if (!shard || shard_len == 0) return RBC_OK;
+    uint8_t r = 0;
+    uint64_t t = 0;
+    int rc = rbc_validate_batch(c, 1, &shard, &shard_len, &index, &branch, &branch_len, &root, &r, &t);
+    if (rc) return rc;
+    *ok = r;
+    return RBC_OK;
+}
+
+int rbc_interpolate(rbc_ctx *c, const uint8_t *root, const uint8_t *const *shards, const size_t *lens,
+                    uint8_t *value_out, size_t value_cap, size_t *value_len, uint8_t *digest_out) {
+    if (!c || !root || !shards || !lens || !value_out) return RBC_ERR_INVALID_ARG;
+    size_t S = 0;
+    int rc = check_shards(lens, c->n, true, &S);
+    if (rc) return rc;
+    int present = 0;
+    for (int i = 0; i < c->n; ++i) present += lens[i] != 0;
+    if (present < c->k) return RBC_ERR_TOO_FEW_SHARDS;  // rbc/rbc.go:87
+    if (value_cap < (size_t)c->k * S) return RBC_ERR_INVALID_ARG;
+    std::vector<uint8_t> buf((size_t)c->n * S, 0), pres(c->n, 0);
+    for (int i = 0; i < c->n; ++i)
+        if (lens[i]) {
+            if (!shards[i]) return RBC_ERR_INVALID_ARG;
+            memcpy(buf.data() + (size_t)i * S, shards[i], S);
+            pres[i] = 1;
+        }
+    int32_t status = 0;
+    uint64_t t = 0;
+    rc = rbc_interpolate_batch(c, 1, buf.data(), S, &S, pres.data(), root, value_out, value_cap, digest_out, &status,
+                               &t);
+    if (rc) return rc;
+    if (status) return status;
+    if (value_len) *value_len = (size_t)c->k * S;
+    return RBC_OK;
+}
+
+// ---- reedsolomon.Encoder mirror
+int rbc_rs_new(int data_shards, int parity_shards, int device, rbc_rs **out) {
+    if (!out) return RBC_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (data_shards <= 0 || parity_shards < 0) return RBC_ERR_INV_SHARD_NUM;
+    if (data_shards + parity_shards > 256) return RBC_ERR_MAX_SHARD_NUM;
+    rbc_ctx *c = nullptr;
+    int rc = ctx_create_kn(data_shards + parity_shards, data_shards, device, &c);
+    if (rc) return rc;
+    *out = new rbc_rs{c};
+    return RBC_OK;
+}
+
+void rbc_rs_free(rbc_rs *rs) {
+    if (!rs) return;
+    rbc_ctx_destroy(rs->ctx);
+    delete rs;
+}
+
+static int rs_parity(rbc_ctx *c, const uint8_t *const *shards, size_t S, std::vector<uint8_t> &parity) {
+    // parity of the data shards, computed by the GPU encode kernel
+    const size_t dpitch = round_up(S, kAlign);
+    const size_t vpitch = round_up((size_t)c->k * S + 32, kAlign);
+    if (vpitch > 0x7fffffffULL || (size_t)c->n * dpitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
+    RBC_HIP(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    RBC_HIP(c->h_stage.ensure(std::max(vpitch, (size_t)c->n * dpitch)));
+    RBC_HIP(c->d_values.ensure(vpitch));
+    RBC_HIP(c->d_shards.ensure((size_t)c->n * dpitch));
+    uint8_t *stage = c->h_stage.as<uint8_t>();
+    memset(stage, 0, vpitch);
+    for (int j = 0; j < c->k; ++j) memcpy(stage + (size_t)j * S, shards[j], S);
+    RBC_HIP(hipMemcpyAsync(c->d_values.p, stage, vpitch, hipMemcpyHostToDevice, st));
+    int rc = stage_encode(c, st, 1, c->d_values.as<uint8_t>(), vpitch, nullptr, (uint32_t)((size_t)c->k * S),
+                          c->d_shards.as<uint8_t>(), (uint32_t)dpitch);
+    if (rc) return rc;
+    parity.assign((size_t)c->p * S, 0);
+    if (c->p > 0)
+        RBC_HIP(hipMemcpy2DAsync(parity.data(), S, c->d_shards.as<uint8_t>() + (size_t)c->k * dpitch, dpitch, S,
+                                 c->p, hipMemcpyDeviceToHost, st));
+    RBC_HIP(hipStreamSynchronize(st));
+    return RBC_OK;
+}
+
+int rbc_rs_encode(rbc_rs *rs, uint8_t *const *shards, const size_t *lens, int n_shards) {
+    if (!rs || !shards || !lens) return RBC_ERR_INVALID_ARG;
+    rbc_ctx *c = rs->ctx;
+    if (n_shards != c->n) return RBC_ERR_TOO_FEW_SHARDS;
+    size_t S = 0;
+    int rc = check_shards(lens, n_shards, false, &S);
+    if (rc) return rc;
+    for (int i = 0; i < c->n; ++i)
+        if (!shards[i]) return RBC_ERR_INVALID_ARG;
+    std::vector<uint8_t> parity;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        rc = rs_parity(c, shards, S, parity);
+    }
+    if (rc) return rc;
+    for (int r = 0; r < c->p; ++r) memcpy(shards[c->k + r], parity.data() + (size_t)r * S, S);
+    return RBC_OK;
+}
+
+int rbc_rs_verify(rbc_rs *rs, const uint8_t *const *shards, const size_t *lens, int n_shards, int *ok) {
+    if (!rs || !shards || !lens || !ok) return RBC_ERR_INVALID_ARG;
+    rbc_ctx *c = rs->ctx;
+    *ok = 0;
+    if (n_shards != c->n) return RBC_ERR_TOO_FEW_SHARDS;
+    size_t S = 0;
+    int rc = check_shards(lens, n_shards, false, &S);
+    if (rc) return rc;
+    for (int i = 0; i < c->n; ++i)
+        if (!shards[i]) return RBC_ERR_INVALID_ARG;
+    std::vector<uint8_t> parity;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        rc = rs_parity(c, shards, S, parity);
+    }
+    if (rc) return rc;
+    int good = 1;
+    for (int r = 0; r < c->p && good; ++r) good = memcmp(shards[c->k + r], parity.data() + (size_t)r * S, S) == 0;
+    *ok = good;
+    return RBC_OK;
+}
+
+int rbc_rs_reconstruct(rbc_rs *rs, uint8_t *const *shards, size_t *lens, int n_shards) {
+    if (!rs) return RBC_ERR_INVALID_ARG;
+    return host_reconstruct(rs->ctx, shards, lens, n_shards, false);
+}
+
+int rbc_rs_reconstruct_data(rbc_rs *rs, uint8_t *const *shards, size_t *lens, int n_shards) {
+    if (!rs) return RBC_ERR_INVALID_ARG;
+    return host_reconstruct(rs->ctx, shards, lens, n_shards, true);
+}
+
+int rbc_rs_split(rbc_rs *rs, const uint8_t *data, size_t len, uint8_t *out, size_t out_cap, size_t *per_shard) {
+    if (!rs || !out || !per_shard) return RBC_ERR_INVALID_ARG;
+    rbc_ctx *c = rs->ctx;
+    if (len == 0) return RBC_ERR_SHORT_DATA;
+    if (!data) return RBC_ERR_INVALID_ARG;
+    const size_t per = (len + c->k - 1) / c->k;
+    if (out_cap < (size_t)c->n * per) return RBC_ERR_INVALID_ARG;
+    memcpy(out, data, len);
+    memset(out + len, 0, (size_t)c->n * per - len);
+    *per_shard = per;
+    return RBC_OK;
+}
+
+int rbc_rs_join(rbc_rs *rs, const uint8_t *const *shards, const size_t *lens, int n_shards, size_t out_size,
+                uint8_t *dst) {
+    if (!rs || !shards || !lens || (!dst && out_size)) return RBC_ERR_INVALID_ARG;
+    rbc_ctx *c = rs->ctx;
+    if (n_shards < c->k) return RBC_ERR_TOO_FEW_SHARDS;
+    size_t size = 0;
+    for (int i = 0; i < c->k; ++i) {
+        if (!shards[i]) return RBC_ERR_RECONSTRUCT_REQUIRED;
+        size += lens[i];
+        if (size >= out_size) break;
+    }
+    if (size < out_size) return RBC_ERR_SHORT_DATA;
+    size_t write = out_size, off = 0;
+    for (int i = 0; i < c->k && write; ++i) {
+        const size_t w = std::min(write, lens[i]);
+        memcpy(dst + off, shards[i], w);
+        off += w;
+        write -= w;
+    }
+    return RBC_OK;
+}
+
+// ---- multi-GPU
+int rbc_comm_unique_id(uint8_t id_out[128]) {
+    if (!id_out) return RBC_ERR_INVALID_ARG;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return RBC_ERR_DEVICE;
+    memcpy(id_out, id.internal, 128);
+    return RBC_OK;
+}
+
+int rbc_comm_init(rbc_ctx *c, int nranks, int rank, const uint8_t id[128]) {
+    if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return RBC_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    RBC_HIP(hipSetDevice(c->device));
+    if (c->comm) { (void)ncclCommDestroy(c->comm); c->comm = nullptr; }
+    ncclUniqueId uid;
+    memcpy(uid.internal, id, 128);
+    if (ncclCommInitRank(&c->comm, nranks, uid, rank) != ncclSuccess) { c->comm = nullptr; return RBC_ERR_DEVICE; }
+    c->nranks = nranks;
+    c->rank = rank;
+    return RBC_OK;
+}
+
+int rbc_comm_destroy(rbc_ctx *c) {
+    if (!c) return RBC_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    c->comm = nullptr;
+    c->nranks = 1;
+    c->rank = 0;
+    return RBC_OK;
+}
+
+int rbc_dev_allgather_roots(rbc_ctx *c, void *stream, int count, const uint8_t *roots, const uint8_t *digests,
+                            uint8_t *gathered) {
+    if (!c || count < 0 || (count > 0 && (!roots || !gathered))) return RBC_ERR_INVALID_ARG;
+    if (!c->comm) return RBC_ERR_NO_COMM;
+    if (count == 0) return RBC_OK;
+    std::lock_guard<std::mutex> lk(c->mu);
+    RBC_HIP(hipSetDevice(c->device));
+    hipStream_t st = as_stream(stream);
+    RBC_HIP(c->d_pack.ensure((size_t)count * 64));
+    RBC_HIP(hipMemcpy2DAsync(c->d_pack.p, 64, roots, 32, 32, count, hipMemcpyDeviceToDevice, st));
+    if (digests)
+        RBC_HIP(hipMemcpy2DAsync(c->d_pack.as<uint8_t>() + 32, 64, digests, 32, 32, count, hipMemcpyDeviceToDevice,
+                                 st));
+    else
+        RBC_HIP(hipMemset2DAsync(c->d_pack.as<uint8_t>() + 32, 64, 0, 32, count, st));
+    if (ncclAllGather(c->d_pack.p, gathered, (size_t)count * 64, ncclUint8, c->comm, st) != ncclSuccess)
+        return RBC_ERR_DEVICE;
+    return RBC_OK;
+}
+
+}  // extern "C"

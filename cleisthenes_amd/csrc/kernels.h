@@ -1,0 +1,105 @@
+// kernels.h -- argument blocks and launchers of the batched RBC kernels
+// (host side of kernels.hip).  Plain structs passed by value to the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rbc_gpu.h"
+
+enum { GF_MODE_ENCODE = 0, GF_MODE_DECODE = 1 };
+
+struct GfArgs {
+    int count;                 // instances
+    int tiles;                 // 4 KiB column tiles per instance (ceil(out_row_pitch / 4096))
+    int rc;                    // rows per chunk (template)
+    int R, K;                  // output rows, input rows per instance
+    int mode;                  // GF_MODE_*
+    const uint8_t *in;         // encode: values [I][value_pitch]; decode: shards [I][N][pitch]
+    uint64_t in_inst_pitch;
+    uint32_t in_row_pitch;     // decode only
+    uint32_t in_inst_bytes;    // readable bytes per instance (buffer bound)
+    uint8_t *out;              // shards [I][N][pitch]
+    uint64_t out_inst_pitch;
+    uint32_t out_row_pitch;
+    uint8_t *copy;             // encode: data rows written through; decode: used rows copied (out != in)
+    const uint32_t *lens;      // encode: B_i; decode: S_i (nullptr -> uniform_len)
+    uint32_t uniform_len;
+    const uint8_t *coef;       // R x K bytes (+ inst * coef_inst_stride)
+    uint64_t coef_inst_stride;
+    const uint8_t *in_idx;     // decode: [I][idx_stride] input row positions (K used)
+    const uint8_t *out_idx;    // decode: [I][idx_stride2] output row positions (R regen)
+    uint32_t idx_stride, idx_stride2;
+    const int32_t *status;     // skip instances with status != 0 (nullable)
+};
+
+struct ShaArgs {
+    int count;
+    int rows_per_inst;         // row slots per instance
+    const uint8_t *rows;       // [I][N][row_pitch]
+    uint64_t inst_pitch;
+    uint32_t row_pitch;
+    const uint32_t *lens;      // S_i (nullable)
+    uint32_t uniform_len;
+    const uint8_t *idx;        // optional row positions [I][idx_stride]
+    uint32_t idx_stride;
+    const int32_t *status;     // nullable
+    uint8_t *leaves;           // [I][N][32] (nullable)
+    uint64_t leaves_inst_pitch;
+    int per_message;           // 1: each instance is one ECHO message (leaf index = idx[inst])
+    // verify
+    int n, depth;
+    const uint8_t *branches;   // [I][N][d][32]
+    uint64_t br_inst_pitch;
+    const uint8_t *roots;      // [I][32]
+    const uint8_t *present;    // [I][N] (nullable -> all present)
+    uint8_t *valid;            // [I][N]
+};
+
+struct MerkleArgs {
+    int count, n, width, depth, k;
+    const uint8_t *leaves;     // [I][N][32]
+    uint64_t leaves_inst_pitch;
+    uint8_t *roots;            // build: out; check: recomputed root out (nullable)
+    uint8_t *branches;         // build: [I][N][d][32] (nullable)
+    uint64_t br_inst_pitch;
+    const uint8_t *expect_roots;  // check
+    int32_t *status;           // check: in/out
+    uint8_t *digests;          // check: [I][32] (nullable)
+};
+
+struct PrepArgs {
+    int count, n, k;
+    const uint8_t *valid;      // [I][valid_stride]
+    uint32_t valid_stride;
+    const uint8_t *M;          // encode matrix [n][k]
+    uint8_t *used;             // [I][used_stride]   first k valid positions
+    uint32_t used_stride;
+    uint8_t *regen;            // [I][regen_stride]  the other n-k positions
+    uint32_t regen_stride;
+    uint8_t *dmat;             // [I][dmat_stride] = (n-k) x k decode matrix
+    uint64_t dmat_stride;
+    int32_t *status;           // out
+};
+
+struct JoinArgs {
+    int count, k;
+    uint32_t chunks;           // 16-byte chunks per instance (= value_pitch / 16)
+    const uint8_t *shards;     // full codeword rows
+    uint64_t inst_pitch;
+    uint32_t row_pitch;
+    uint32_t inst_bytes;       // readable bytes per instance
+    const uint32_t *lens;      // S_i (nullable)
+    uint32_t uniform_len;
+    uint8_t *values;           // [I][value_pitch]
+    uint32_t value_pitch;
+    const int32_t *status;
+};
+
+int rbc_gf_pick_rc(int R);
+hipError_t rbc_launch_gf_rows(const GfArgs &a, hipStream_t st);
+hipError_t rbc_launch_sha_rows(const ShaArgs &a, bool verify, hipStream_t st);
+hipError_t rbc_launch_merkle(const MerkleArgs &a, bool check, hipStream_t st);
+hipError_t rbc_launch_decode_prepare(const PrepArgs &a, hipStream_t st);
+hipError_t rbc_launch_join(const JoinArgs &a, hipStream_t st);
+hipError_t rbc_launch_inject_faults(uint8_t *shards, uint64_t inst_pitch, uint32_t row_pitch,
+                                    const int32_t *corrupt, int count, hipStream_t st);

@@ -1,0 +1,594 @@
+// kernels.hip -- batched RBC data-path kernels for MI355X (gfx950).
+//
+// Replaces, for thousands of RBC instances per launch, the work behind
+//   shard()           rbc/rbc.go:97-100  (klauspost Split + Encode)
+//   Merkle build      (VAL construction, rbc/rbc.go:42; docs/RBC-EN.md:31)
+//   validateMessage() rbc/rbc.go:92-95   (ECHO branch verify)
+//   interpolate()     rbc/rbc.go:86-90   (Reconstruct + re-encode + root recheck)
+//
+// HBM layout:
+//   values   [I][value_pitch]            proposer input, B_i bytes used
+//   shards   [I][N][shard_pitch]         shard_pitch % 64 == 0, >= S_i; bytes in
+//                                        [S_i, pitch) are written as zero
+//   leaves   [I][N][32]                  SHA-256(shard)
+//   roots    [I][32]
+//   branches [I][N][d][32]               level-0 slot zero when sibling empty
+//   valid    [I][N] u8 ; status [I] i32 ; digests [I][32]
+// No MFMA: GF(2^8) and SHA-256 are not dense contractions (north_star).
+#include "device_common.h"
+#include "kernels.h"
+
+using namespace rbcdev;
+
+namespace {
+
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+constexpr int RBC_RSRC_DW3 = 0x00020000;  // gfx9 raw buffer, bounds-checked
+
+RBC_DEV rsrc_t make_rsrc(const void *p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, RBC_RSRC_DW3);
+}
+RBC_DEV uint4 bload16(rsrc_t r, uint32_t off) {
+    auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+RBC_DEV uint32_t inst_len(const uint32_t *lens, uint32_t uniform, int i) { return lens ? lens[i] : uniform; }
+
+// byte mask keeping the first `nv` bytes (little-endian) of a word
+RBC_DEV uint32_t keep_bytes(int nv) {
+    return nv >= 4 ? 0xffffffffu : (nv <= 0 ? 0u : ((1u << (8 * nv)) - 1u));
+}
+RBC_DEV uint4 mask16(uint4 v, int nvalid) {
+    v.x &= keep_bytes(nvalid);
+    v.y &= keep_bytes(nvalid - 4);
+    v.z &= keep_bytes(nvalid - 8);
+    v.w &= keep_bytes(nvalid - 12);
+    return v;
+}
+// gfx950 runs with unaligned global/buffer access enabled (hipcc itself
+// emits dwordx4 for byte-aligned pointers), so a 16-byte row read at any
+// byte offset is a single buffer_load_dwordx4; bounds are still checked by
+// the buffer descriptor (out of range -> 0).
+
+}  // namespace
+
+// ============================================================================
+// gf_rows: out[r] = XOR_j coef[r][j] * in[j]   (klauspost codeSomeShards)
+// One block = one instance x one 4 KiB column tile; each thread owns 16
+// consecutive bytes (4 packed words) of every row.  Output rows are done in
+// chunks of RC so the RC x 4 accumulators stay in VGPRs; the chunk's perm
+// tables (RC x K x 20 B) live in LDS and are read by wave-uniform broadcast.
+// Encode mode reads data row j straight out of the value bytes at j*S
+// (Split), funnel-shifting unaligned rows, masks the zero pad, and writes the
+// data rows through to shards[0..k) on the first chunk.
+// ============================================================================
+template <int RC>
+__global__ __launch_bounds__(256) void gf_rows_kernel(GfArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int KP = (a.K + 1) & ~1;
+    uint4 *s_t01 = reinterpret_cast<uint4 *>(smem);
+    uint32_t *s_t2 = reinterpret_cast<uint32_t *>(smem + (size_t)16 * RC * KP);
+    uint8_t *s_in = reinterpret_cast<uint8_t *>(smem + (size_t)20 * RC * KP);
+    uint8_t *s_out = s_in + 256;
+
+    const int inst = blockIdx.x / a.tiles;
+    const int tile = blockIdx.x - inst * a.tiles;
+    const int tid = threadIdx.x;
+    if (a.status && a.status[inst] != 0) return;
+
+    // shard length of this instance
+    uint32_t S;
+    uint32_t B = 0;
+    if (a.mode == GF_MODE_ENCODE) {
+        B = inst_len(a.lens, a.uniform_len, inst);
+        S = (B + a.K - 1) / a.K;
+    } else {
+        S = inst_len(a.lens, a.uniform_len, inst);
+    }
+    const uint32_t tile_byte0 = (uint32_t)tile * 4096u;
+    if (tile_byte0 >= a.out_row_pitch) return;
+    const uint32_t my_off = tile_byte0 + 16u * tid;      // byte offset inside a row
+    const bool my_store = my_off < a.out_row_pitch;
+
+    const uint8_t *in_inst = a.in + (size_t)inst * a.in_inst_pitch;
+    uint8_t *out_inst = a.out + (size_t)inst * a.out_inst_pitch;
+    const rsrc_t rin = make_rsrc(in_inst, a.in_inst_bytes);
+
+    if (a.mode == GF_MODE_DECODE) {
+        for (int t = tid; t < a.K; t += 256) s_in[t] = a.in_idx[(size_t)inst * a.idx_stride + t];
+        for (int t = tid; t < a.R; t += 256) s_out[t] = a.out_idx[(size_t)inst * a.idx_stride2 + t];
+    }
+
+    // load 16 bytes of input row j for this thread (masked to the row)
+    auto load_row = [&](int j) -> uint4 {
+        if (j >= a.K) return make_uint4(0, 0, 0, 0);
+        if (a.mode == GF_MODE_ENCODE) {
+            const uint32_t row0 = (uint32_t)j * S;                   // Split: data[j*S : (j+1)*S]
+            const int lim = (int)min(S, B > row0 ? B - row0 : 0u);  // bytes of this row that are data
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if ((int)my_off < lim) {
+                v = bload16(rin, row0 + my_off);  // unaligned when S % 16 != 0
+                if ((int)my_off + 16 > lim) v = mask16(v, lim - (int)my_off);
+            }
+            return v;
+        } else {
+            const uint32_t pos = s_in[j];
+            uint4 v = bload16(rin, pos * a.in_row_pitch + my_off);
+            return v;
+        }
+    };
+
+    // R == 0 (no parity, f = 0) still runs one chunk so Split's copy happens
+    const int chunks = a.R > 0 ? (a.R + RC - 1) / RC : 1;
+    for (int c = 0; c < chunks; ++c) {
+        const int r0 = c * RC;
+        const int rows = min(RC, a.R - r0);
+        __syncthreads();  // previous chunk's tables no longer read; idx lists visible
+        for (int e = tid; e < RC * KP; e += 256) {
+            const int r = e / KP, j = e - r * KP;
+            uint32_t cf = 0;
+            if (r < rows && j < a.K)
+                cf = a.coef[(size_t)inst * a.coef_inst_stride + (size_t)(r0 + r) * a.K + j];
+            uint4 t01;
+            uint32_t t2;
+            gf_tables(cf, t01, t2);
+            s_t01[e] = t01;
+            s_t2[e] = t2;
+        }
+        __syncthreads();
+
+        uint32_t acc[RC][4];
+#pragma unroll
+        for (int r = 0; r < RC; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0;
+
+        const bool do_copy = (c == 0) && a.copy && my_store;
+        uint4 xa = load_row(0), xb = load_row(1);
+        for (int j = 0; j < KP; j += 2) {
+            const uint4 na = load_row(j + 2), nb = load_row(j + 3);  // prefetch next pair
+            if (do_copy) {
+                const uint32_t pa = (a.mode == GF_MODE_ENCODE) ? (uint32_t)j : s_in[j];
+                *reinterpret_cast<uint4 *>(a.copy + (size_t)inst * a.out_inst_pitch +
+                                           (size_t)pa * a.out_row_pitch + my_off) = xa;
+                if (j + 1 < a.K) {
+                    const uint32_t pb = (a.mode == GF_MODE_ENCODE) ? (uint32_t)(j + 1) : s_in[j + 1];
+                    *reinterpret_cast<uint4 *>(a.copy + (size_t)inst * a.out_inst_pitch +
+                                               (size_t)pb * a.out_row_pitch + my_off) = xb;
+                }
+            }
+            const GfSel sa0 = gf_sel(xa.x), sa1 = gf_sel(xa.y), sa2 = gf_sel(xa.z), sa3 = gf_sel(xa.w);
+            const GfSel sb0 = gf_sel(xb.x), sb1 = gf_sel(xb.y), sb2 = gf_sel(xb.z), sb3 = gf_sel(xb.w);
+#pragma unroll
+            for (int r = 0; r < RC; ++r) {
+                const uint4 ta = s_t01[r * KP + j];
+                const uint4 tb = s_t01[r * KP + j + 1];
+                const uint2 t2 = *reinterpret_cast<const uint2 *>(&s_t2[r * KP + j]);
+                acc[r][0] = xor3(acc[r][0], gf_mul4(ta, t2.x, sa0), gf_mul4(tb, t2.y, sb0));
+                acc[r][1] = xor3(acc[r][1], gf_mul4(ta, t2.x, sa1), gf_mul4(tb, t2.y, sb1));
+                acc[r][2] = xor3(acc[r][2], gf_mul4(ta, t2.x, sa2), gf_mul4(tb, t2.y, sb2));
+                acc[r][3] = xor3(acc[r][3], gf_mul4(ta, t2.x, sa3), gf_mul4(tb, t2.y, sb3));
+            }
+            xa = na;
+            xb = nb;
+        }
+        if (my_store) {
+            const int nvalid = (int)S - (int)my_off;  // zero the bytes past S
+#pragma unroll
+            for (int r = 0; r < RC; ++r) {
+                if (r < rows) {
+                    const uint32_t pos = (a.mode == GF_MODE_ENCODE) ? (uint32_t)(a.K + r0 + r) : s_out[r0 + r];
+                    uint4 v = make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+                    if (nvalid < 16) v = mask16(v, nvalid);
+                    *reinterpret_cast<uint4 *>(out_inst + (size_t)pos * a.out_row_pitch + my_off) = v;
+                }
+            }
+        }
+    }
+}
+
+// ============================================================================
+// sha_rows: leaf_j = SHA-256(shard_j) for a list of rows, one lane per row;
+// VERIFY additionally walks the Merkle branch (validateMessage,
+// rbc/rbc.go:92-95) and writes valid = present && (root' == root).
+// ============================================================================
+template <bool VERIFY>
+__global__ __launch_bounds__(256) void sha_rows_kernel(ShaArgs a) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= a.count * a.rows_per_inst) return;
+    const int inst = t / a.rows_per_inst;
+    const int slot = t - inst * a.rows_per_inst;
+    if (a.status && a.status[inst] != 0) return;
+    // per_message: every "instance" is one independent ECHO message whose
+    // leaf index is idx[inst]; otherwise slot -> row position (idx optional)
+    const int pos = a.idx ? (int)a.idx[(size_t)inst * a.idx_stride + slot] : slot;
+    const int rowsel = a.per_message ? 0 : pos;
+    const uint32_t S = inst_len(a.lens, a.uniform_len, inst);
+    const uint8_t *row = a.rows + (size_t)inst * a.inst_pitch + (size_t)rowsel * a.row_pitch;
+    Sha256State s;
+    sha256_row(row, S, s);
+    uint32_t h[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) h[q] = s.h[q];
+    if (a.leaves) store_digest(a.leaves + (size_t)inst * a.leaves_inst_pitch + 32u * rowsel, h);
+    if (VERIFY) {
+        const uint8_t *br = a.branches + (size_t)inst * a.br_inst_pitch + (size_t)rowsel * a.depth * 32u;
+        uint32_t tix = (uint32_t)pos;
+        for (int l = 0; l < a.depth; ++l, tix >>= 1) {
+            const bool empty = (l == 0) && ((pos ^ 1) >= a.n);
+            uint32_t sib[8], o[8];
+            if (empty) {
+                sha256_node32(h, o);
+            } else {
+                load_digest(br + 32u * l, sib);
+                if (tix & 1u) sha256_node64(sib, h, o);
+                else sha256_node64(h, sib, o);
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) h[q] = o[q];
+        }
+        uint32_t root[8];
+        load_digest(a.roots + (size_t)inst * 32u, root);
+        bool ok = true;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) ok = ok && (h[q] == root[q]);
+        const bool inrange = pos < a.n;
+        if (a.per_message) {
+            a.valid[inst] = (ok && inrange) ? 1 : 0;
+        } else {
+            const bool present = a.present ? a.present[(size_t)inst * a.n + pos] != 0 : true;
+            a.valid[(size_t)inst * a.n + pos] = (ok && present) ? 1 : 0;
+        }
+    }
+}
+
+// ============================================================================
+// merkle: one wave per instance.  BUILD writes root + all N branches;
+// CHECK recomputes the root over the re-encoded leaves, compares it with the
+// expected root (interpolate's recheck) and writes the batch digest
+// SHA-256(leaf_0 || .. || leaf_{k-1}).  Node convention (frozen):
+// H(L || R), empty padding leaves contribute no bytes.
+// ============================================================================
+template <bool CHECK>
+__global__ __launch_bounds__(64) void merkle_kernel(MerkleArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t *nodes = reinterpret_cast<uint32_t *>(smem);  // [2W][8] big-endian words
+    const int inst = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (CHECK && a.status && a.status[inst] != 0) return;
+    const int W = a.width;
+    const uint8_t *lv = a.leaves + (size_t)inst * a.leaves_inst_pitch;
+    for (int j = lane; j < a.n; j += 64) {
+        uint32_t h[8];
+        load_digest(lv + 32u * j, h);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) nodes[(W + j) * 8 + q] = h[q];
+    }
+    __syncthreads();
+    for (int m = W >> 1; m >= 1; m >>= 1) {
+        for (int i = m + lane; i < 2 * m; i += 64) {
+            const int lc = 2 * i, rc = 2 * i + 1;
+            const bool leaf_level = (lc >= W);
+            const bool lempty = leaf_level && (lc - W >= a.n);
+            const bool rempty = leaf_level && (rc - W >= a.n);
+            uint32_t o[8];
+            if (lempty) {
+                sha256_empty(o);
+            } else {
+                uint32_t l[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) l[q] = nodes[lc * 8 + q];
+                if (rempty) {
+                    sha256_node32(l, o);
+                } else {
+                    uint32_t r[8];
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) r[q] = nodes[rc * 8 + q];
+                    sha256_node64(l, r, o);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) nodes[i * 8 + q] = o[q];
+        }
+        __syncthreads();
+    }
+    uint32_t root[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) root[q] = nodes[8 + q];
+    if (!CHECK) {
+        if (lane == 0) store_digest(a.roots + (size_t)inst * 32u, root);
+        if (a.branches) {
+            // branch[j][l] = nodes[((W + j) >> l) ^ 1]; one 16-byte half per item
+            uint8_t *br = a.branches + (size_t)inst * a.br_inst_pitch;
+            const int items = a.n * a.depth * 2;
+            for (int e = lane; e < items; e += 64) {
+                const int half = e & 1, jl = e >> 1;
+                const int j = jl / a.depth, l = jl - j * a.depth;
+                const int node = ((W + j) >> l) ^ 1;
+                const bool empty = (l == 0) && (node - W >= a.n);
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (!empty) {
+                    const uint32_t *nd = nodes + node * 8 + 4 * half;
+                    v = make_uint4(bswap32(nd[0]), bswap32(nd[1]), bswap32(nd[2]), bswap32(nd[3]));
+                }
+                *reinterpret_cast<uint4 *>(br + (size_t)jl * 32u + 16u * half) = v;
+            }
+        }
+    } else {
+        uint32_t ex[8];
+        load_digest(a.expect_roots + (size_t)inst * 32u, ex);
+        bool ok = true;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) ok = ok && (ex[q] == root[q]);
+        if (lane == 0) {
+            if (a.status) a.status[inst] = ok ? 0 : RBC_ERR_ROOT_MISMATCH;
+            if (a.roots) store_digest(a.roots + (size_t)inst * 32u, root);
+            if (a.digests) {
+                // batch digest over the k data leaves (8k big-endian words)
+                Sha256State s;
+                sha256_init(s);
+                const int nw = 8 * a.k;
+                const uint32_t *msg = nodes + W * 8;
+                int gw = 0;
+                bool done = false;
+                while (!done) {
+                    uint32_t w[16];
+                    bool last = false;
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        const int g = gw + q;
+                        w[q] = g < nw ? msg[g] : (g == nw ? 0x80000000u : 0u);
+                    }
+                    // the length fits this block if the pad byte is in it (or before) and words 14,15 free
+                    if (nw + 1 + 2 <= gw + 16) {
+                        const uint64_t bits = (uint64_t)nw * 32u;
+                        w[14] = (uint32_t)(bits >> 32);
+                        w[15] = (uint32_t)bits;
+                        last = true;
+                    }
+                    sha256_compress(s, w);
+                    gw += 16;
+                    done = last;
+                }
+                uint32_t d[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) d[q] = s.h[q];
+                store_digest(a.digests + (size_t)inst * 32u, d);
+            }
+        }
+    }
+}
+
+// ============================================================================
+// decode_prepare: per instance, pick the first k valid shards by index
+// (klauspost Reconstruct rule), invert the k x k sub-matrix of the encode
+// matrix by Gauss-Jordan in LDS, and form D = M[regen] * inv so one GF pass
+// regenerates every non-used position (data and parity) of the re-encoding.
+// ============================================================================
+__global__ __launch_bounds__(256) void decode_prepare_kernel(PrepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int n = a.n, k = a.k, k2 = 2 * a.k;
+    uint8_t *s_exp = smem;             // 512
+    uint8_t *s_log = smem + 512;       // 256
+    uint8_t *s_used = smem + 768;      // 256
+    uint8_t *s_regen = smem + 1024;    // 256
+    uint8_t *s_fac = smem + 1280;      // 256
+    int *s_misc = reinterpret_cast<int *>(smem + 1536);  // 4 ints
+    uint8_t *A = smem + 1552;          // k x 2k
+    const int inst = blockIdx.x, tid = threadIdx.x;
+
+    if (tid == 0) {
+        s_log[0] = 0;
+        int x = 1;
+        for (int i = 0; i < 255; ++i) {
+            s_exp[i] = (uint8_t)x;
+            s_exp[i + 255] = (uint8_t)x;
+            s_log[x] = (uint8_t)i;
+            x <<= 1;
+            if (x & 0x100) x ^= 0x11d;
+        }
+        s_exp[510] = s_exp[0];
+        s_exp[511] = s_exp[1];
+        int nu = 0, nr = 0;
+        const uint8_t *v = a.valid + (size_t)inst * a.valid_stride;
+        for (int j = 0; j < n; ++j) {
+            if (v[j] && nu < k) s_used[nu++] = (uint8_t)j;
+            else s_regen[nr++] = (uint8_t)j;
+        }
+        s_misc[0] = nu;
+        s_misc[1] = nr;
+        s_misc[2] = 0;
+    }
+    __syncthreads();
+    auto gmul = [&](uint32_t x, uint32_t y) -> uint32_t {
+        return (x && y) ? (uint32_t)s_exp[s_log[x] + s_log[y]] : 0u;
+    };
+    const int nu = s_misc[0], nr = s_misc[1];
+    if (nu < k) {
+        if (tid == 0) a.status[inst] = RBC_ERR_TOO_FEW_SHARDS;
+        return;
+    }
+    for (int t = tid; t < k; t += 256) a.used[(size_t)inst * a.used_stride + t] = s_used[t];
+    for (int t = tid; t < nr; t += 256) a.regen[(size_t)inst * a.regen_stride + t] = s_regen[t];
+    for (int e = tid; e < k * k2; e += 256) {
+        const int r = e / k2, c = e - r * k2;
+        A[e] = c < k ? a.M[(size_t)s_used[r] * k + c] : (uint8_t)((c - k) == r);
+    }
+    __syncthreads();
+    for (int col = 0; col < k; ++col) {
+        if (tid == 0) {
+            int piv = col;
+            if (A[col * k2 + col] == 0) {
+                piv = -1;
+                for (int b = col + 1; b < k; ++b)
+                    if (A[b * k2 + col]) { piv = b; break; }
+            }
+            s_misc[3] = piv;
+        }
+        __syncthreads();
+        const int piv = s_misc[3];
+        if (piv < 0) {  // cannot happen for an MDS code; report, don't hang
+            if (tid == 0) a.status[inst] = RBC_ERR_SINGULAR;
+            return;
+        }
+        if (piv != col) {
+            for (int c = tid; c < k2; c += 256) {
+                const uint8_t x = A[col * k2 + c];
+                A[col * k2 + c] = A[piv * k2 + c];
+                A[piv * k2 + c] = x;
+            }
+            __syncthreads();
+        }
+        const uint32_t pv = A[col * k2 + col];
+        const uint32_t inv = s_exp[255 - s_log[pv]];
+        __syncthreads();
+        for (int c = tid; c < k2; c += 256) A[col * k2 + c] = (uint8_t)gmul(inv, A[col * k2 + c]);
+        for (int r = tid; r < k; r += 256) s_fac[r] = (r == col) ? 0 : A[r * k2 + col];
+        __syncthreads();
+        for (int e = tid; e < k * k2; e += 256) {
+            const int r = e / k2, c = e - r * k2;
+            const uint32_t f = s_fac[r];
+            if (f) A[e] ^= (uint8_t)gmul(f, A[col * k2 + c]);
+        }
+        __syncthreads();
+    }
+    // D[r][c] = XOR_i M[regen_r][i] * inv[i][c]
+    uint8_t *D = a.dmat + (size_t)inst * a.dmat_stride;
+    for (int e = tid; e < nr * k; e += 256) {
+        const int r = e / k, c = e - r * k;
+        const uint8_t *mrow = a.M + (size_t)s_regen[r] * k;
+        uint32_t acc = 0;
+        for (int i = 0; i < k; ++i) acc ^= gmul(mrow[i], A[i * k2 + k + c]);
+        D[e] = (uint8_t)acc;
+    }
+    if (tid == 0) a.status[inst] = 0;
+}
+
+// ============================================================================
+// join: value = data shards 0..k-1 concatenated (k*S bytes, pad kept), one
+// thread per aligned 16-byte output chunk (a chunk may straddle two rows).
+// ============================================================================
+__global__ __launch_bounds__(256) void join_kernel(JoinArgs a) {
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long)a.count * a.chunks) return;
+    const int inst = (int)(t / a.chunks);
+    const uint32_t ch = (uint32_t)(t - (long)inst * a.chunks);
+    if (a.status && a.status[inst] != 0) return;
+    const uint32_t S = inst_len(a.lens, a.uniform_len, inst);
+    const uint32_t total = S * (uint32_t)a.k;
+    const uint32_t o = ch * 16u;
+    if (o >= a.value_pitch) return;
+    uint4 *dst = reinterpret_cast<uint4 *>(a.values + (size_t)inst * a.value_pitch + o);
+    if (o >= total) { *dst = make_uint4(0, 0, 0, 0); return; }
+    const uint8_t *rows = a.shards + (size_t)inst * a.inst_pitch;
+    const rsrc_t r = make_rsrc(rows, a.inst_bytes);
+    if (S >= 16) {
+        const uint32_t j0 = o / S;
+        const uint32_t s0 = o - j0 * S;
+        uint4 v = bload16(r, j0 * a.row_pitch + s0);
+        const int c0 = (int)min(16u, S - s0);
+        if (c0 < 16) {
+            // bytes c0..15 come from the start of row j0+1: read the 16 bytes
+            // that END at row j0+1 byte 16-c0, then blend by byte mask
+            uint4 w = make_uint4(0, 0, 0, 0);
+            if (j0 + 1 < (uint32_t)a.k) w = bload16(r, (j0 + 1) * a.row_pitch - (uint32_t)c0);
+            const uint4 m = mask16(make_uint4(~0u, ~0u, ~0u, ~0u), c0);
+            v.x = (v.x & m.x) | (w.x & ~m.x);
+            v.y = (v.y & m.y) | (w.y & ~m.y);
+            v.z = (v.z & m.z) | (w.z & ~m.z);
+            v.w = (v.w & m.w) | (w.w & ~m.w);
+        }
+        if (o + 16u > total) v = mask16(v, (int)(total - o));
+        *dst = v;
+    } else {
+        // tiny shards: byte path
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (int b = 0; b < 16; ++b) {
+            const uint32_t g = o + b;
+            if (g >= total) break;
+            const uint32_t j = g / S, off = g - j * S;
+            const uint32_t byte = rows[(size_t)j * a.row_pitch + off];
+            w[b >> 2] |= byte << (8 * (b & 3));
+        }
+        *dst = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
+// Synthetic Byzantine faults (bench/test input generation only): flip one
+// byte of shard corrupt[i] of instance i.
+__global__ void inject_faults_kernel(uint8_t *shards, uint64_t inst_pitch, uint32_t row_pitch,
+                                     const int32_t *corrupt, int count) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const int j = corrupt[i];
+    if (j >= 0) shards[(size_t)i * inst_pitch + (size_t)j * row_pitch] ^= 0x5a;
+}
+
+// ============================================================================
+// launchers
+// ============================================================================
+template <int RC>
+static hipError_t launch_gf_rc(const GfArgs &a, hipStream_t st) {
+    const int KP = (a.K + 1) & ~1;
+    const size_t lds = (size_t)20 * RC * KP + 512;
+    dim3 grid((unsigned)a.count * a.tiles);
+    hipLaunchKernelGGL(gf_rows_kernel<RC>, grid, dim3(256), lds, st, a);
+    return hipGetLastError();
+}
+
+int rbc_gf_pick_rc(int R) {
+    // fewest chunks of <= 24 rows, then the smallest RC covering them
+    if (R <= 0) return 1;
+    const int chunks = (R + 23) / 24;
+    return (R + chunks - 1) / chunks;
+}
+
+hipError_t rbc_launch_gf_rows(const GfArgs &a, hipStream_t st) {
+    if (a.count <= 0 || (a.R <= 0 && !a.copy)) return hipSuccess;
+    switch (a.rc) {
+#define RBC_RC_CASE(x) case x: return launch_gf_rc<x>(a, st);
+        RBC_RC_CASE(1) RBC_RC_CASE(2) RBC_RC_CASE(3) RBC_RC_CASE(4) RBC_RC_CASE(5) RBC_RC_CASE(6)
+        RBC_RC_CASE(7) RBC_RC_CASE(8) RBC_RC_CASE(9) RBC_RC_CASE(10) RBC_RC_CASE(11) RBC_RC_CASE(12)
+        RBC_RC_CASE(13) RBC_RC_CASE(14) RBC_RC_CASE(15) RBC_RC_CASE(16) RBC_RC_CASE(17) RBC_RC_CASE(18)
+        RBC_RC_CASE(19) RBC_RC_CASE(20) RBC_RC_CASE(21) RBC_RC_CASE(22) RBC_RC_CASE(23) RBC_RC_CASE(24)
+#undef RBC_RC_CASE
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t rbc_launch_sha_rows(const ShaArgs &a, bool verify, hipStream_t st) {
+    const long total = (long)a.count * a.rows_per_inst;
+    if (total <= 0) return hipSuccess;
+    dim3 grid((unsigned)((total + 255) / 256));
+    if (verify) hipLaunchKernelGGL(sha_rows_kernel<true>, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(sha_rows_kernel<false>, grid, dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t rbc_launch_merkle(const MerkleArgs &a, bool check, hipStream_t st) {
+    if (a.count <= 0) return hipSuccess;
+    const size_t lds = (size_t)64 * a.width;
+    if (check) hipLaunchKernelGGL(merkle_kernel<true>, dim3(a.count), dim3(64), lds, st, a);
+    else hipLaunchKernelGGL(merkle_kernel<false>, dim3(a.count), dim3(64), lds, st, a);
+    return hipGetLastError();
+}
+
+hipError_t rbc_launch_decode_prepare(const PrepArgs &a, hipStream_t st) {
+    if (a.count <= 0) return hipSuccess;
+    const size_t lds = 1552 + (size_t)a.k * 2 * a.k;
+    hipLaunchKernelGGL(decode_prepare_kernel, dim3(a.count), dim3(256), lds, st, a);
+    return hipGetLastError();
+}
+
+hipError_t rbc_launch_join(const JoinArgs &a, hipStream_t st) {
+    const long total = (long)a.count * a.chunks;
+    if (total <= 0) return hipSuccess;
+    hipLaunchKernelGGL(join_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t rbc_launch_inject_faults(uint8_t *shards, uint64_t inst_pitch, uint32_t row_pitch,
+                                    const int32_t *corrupt, int count, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(inject_faults_kernel, dim3((count + 255) / 256), dim3(256), 0, st, shards, inst_pitch,
+                       row_pitch, corrupt, count);
+    return hipGetLastError();
+}

@@ -1,0 +1,397 @@
+"""Host binding of the RBC data path (include/rbc_gpu.h), mirroring the
+reference's interfaces:
+
+* ``Context.shard(data)``            -> rbc/rbc.go:97-100 ``shard(enc, data)`` (+ Merkle commit, rbc.go:42)
+* ``Context.validate_message(...)``  -> rbc/rbc.go:92-95 ``validateMessage(echo)``
+* ``Context.interpolate(root, shards)`` -> rbc/rbc.go:86-90 ``interpolate(rootHash, shards)``
+* ``Encoder(k, p)``                  -> ``reedsolomon.New`` / ``reedsolomon.Encoder`` (rbc/rbc.go:20)
+* ``Context.dev_*``                  -> batched device-resident stages (the Go batcher's path)
+
+Missing shards are ``None`` or empty (Go ``len == 0``); errors raise
+``RBCError`` carrying the klauspost v1.9.1 error value as ``code``.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import byref, c_float, c_int, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import RBCError, check, lib
+
+__all__ = ["Context", "Encoder", "DeviceBuffer", "Stream", "Event", "RBCError", "device_count"]
+
+
+def device_count() -> int:
+    n = c_int(0)
+    check(lib.rbc_device_count(byref(n)), "rbc_device_count")
+    return n.value
+
+
+def _ptr(a: np.ndarray) -> c_void_p:
+    return c_void_p(a.ctypes.data)
+
+
+def _bytes_array(x) -> np.ndarray:
+    if x is None:
+        return np.zeros(0, dtype=np.uint8)
+    if isinstance(x, np.ndarray):
+        return np.ascontiguousarray(x, dtype=np.uint8)
+    return np.frombuffer(bytes(x), dtype=np.uint8)
+
+
+class DeviceBuffer:
+    """A device allocation made by the library (hipMalloc)."""
+
+    def __init__(self, nbytes: int, device: int = 0):
+        self.nbytes = int(nbytes)
+        self.device = device
+        p = c_void_p()
+        check(lib.rbc_dev_malloc(device, self.nbytes, byref(p)), "rbc_dev_malloc")
+        self.ptr = p
+
+    @property
+    def value(self) -> int:
+        return self.ptr.value
+
+    def upload(self, a: np.ndarray, offset: int = 0) -> None:
+        a = np.ascontiguousarray(a)
+        assert offset + a.nbytes <= self.nbytes
+        check(lib.rbc_memcpy_h2d(c_void_p(self.ptr.value + offset), _ptr(a), a.nbytes), "h2d")
+
+    def download(self, nbytes: Optional[int] = None, offset: int = 0) -> np.ndarray:
+        n = self.nbytes - offset if nbytes is None else nbytes
+        out = np.empty(n, dtype=np.uint8)
+        check(lib.rbc_memcpy_d2h(_ptr(out), c_void_p(self.ptr.value + offset), n), "d2h")
+        return out
+
+    def zero(self) -> None:
+        check(lib.rbc_dev_memset(self.ptr, 0, self.nbytes), "memset")
+
+    def free(self) -> None:
+        if self.ptr is not None and self.ptr.value:
+            lib.rbc_dev_free(self.ptr)
+        self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Stream:
+    def __init__(self, device: int = 0):
+        p = c_void_p()
+        check(lib.rbc_stream_create(device, byref(p)), "rbc_stream_create")
+        self.ptr = p
+
+    def sync(self) -> None:
+        check(lib.rbc_stream_sync(self.ptr), "rbc_stream_sync")
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                lib.rbc_stream_destroy(self.ptr)
+        except Exception:
+            pass
+
+
+class Event:
+    def __init__(self):
+        p = c_void_p()
+        check(lib.rbc_event_create(byref(p)), "rbc_event_create")
+        self.ptr = p
+
+    def record(self, stream: Optional[Stream] = None) -> None:
+        check(lib.rbc_event_record(self.ptr, stream.ptr if stream else None), "rbc_event_record")
+
+    def elapsed_ms(self, end: "Event") -> float:
+        ms = c_float(0)
+        check(lib.rbc_event_elapsed_ms(self.ptr, end.ptr, byref(ms)), "rbc_event_elapsed_ms")
+        return ms.value
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                lib.rbc_event_destroy(self.ptr)
+        except Exception:
+            pass
+
+
+def _dv(x) -> Optional[c_void_p]:
+    """DeviceBuffer / int / None -> c_void_p."""
+    if x is None:
+        return None
+    if isinstance(x, DeviceBuffer):
+        return x.ptr
+    if isinstance(x, int):
+        return c_void_p(x)
+    return x
+
+
+class Context:
+    """One (N, f) RBC geometry on one GPU (rbc/rbc.go:9-20)."""
+
+    def __init__(self, n: int, f: int, device: int = 0):
+        p = c_void_p()
+        check(lib.rbc_ctx_create(n, f, device, byref(p)), "rbc_ctx_create")
+        self._p = p
+        self.n, self.f, self.device = n, f, device
+        k, par, d = c_int(), c_int(), c_int()
+        check(lib.rbc_ctx_params(p, byref(k), byref(par), byref(d)))
+        self.k, self.p, self.depth = k.value, par.value, d.value
+
+    def close(self) -> None:
+        if getattr(self, "_p", None):
+            lib.rbc_ctx_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self) -> c_void_p:
+        return self._p
+
+    def encode_matrix(self) -> np.ndarray:
+        m = np.zeros(self.n * self.k, dtype=np.uint8)
+        check(lib.rbc_ctx_encode_matrix(self._p, _ptr(m)))
+        return m.reshape(self.n, self.k)
+
+    # ---- single-call drop-ins -------------------------------------------
+    def shard(self, data) -> dict:
+        """shard(enc, data) + Merkle commit -> {shards, root, branches (flat, Go form)}"""
+        d = _bytes_array(data)
+        S = (len(d) + self.k - 1) // self.k if len(d) else 0
+        out = np.zeros(max(self.n * S, 1), dtype=np.uint8)
+        br = np.zeros(max(self.n * self.depth * 32, 1), dtype=np.uint8)
+        root = np.zeros(32, dtype=np.uint8)
+        slen = c_size_t(0)
+        check(lib.rbc_shard(self._p, _ptr(d) if len(d) else None, len(d), _ptr(out), out.nbytes, byref(slen),
+                            _ptr(root), _ptr(br)), "rbc_shard")
+        S = slen.value
+        shards = [out[j * S:(j + 1) * S].copy() for j in range(self.n)]
+        brs = br[: self.n * self.depth * 32].reshape(self.n, self.depth, 32) if self.depth else None
+        flat = []
+        for j in range(self.n):
+            parts = []
+            for lvl in range(self.depth):
+                if lvl == 0 and (j ^ 1) >= self.n:
+                    continue
+                parts.append(bytes(brs[j, lvl]))
+            flat.append(b"".join(parts))
+        return {"shards": shards, "shard_len": S, "root": bytes(root), "branches": flat}
+
+    def validate_message(self, root: bytes, branch: bytes, shard, index: int) -> bool:
+        s = _bytes_array(shard)
+        b = _bytes_array(branch)
+        r = _bytes_array(root)
+        if len(r) != 32:
+            return False
+        ok = c_int(0)
+        check(lib.rbc_validate_message(self._p, _ptr(r), _ptr(b) if len(b) else None, len(b),
+                                       _ptr(s) if len(s) else None, len(s), index, byref(ok)),
+              "rbc_validate_message")
+        return bool(ok.value)
+
+    def interpolate(self, root: bytes, shards: Sequence) -> dict:
+        arrs = [_bytes_array(s) for s in shards]
+        if len(arrs) != self.n:
+            raise RBCError(_lib.RBC_ERR_TOO_FEW_SHARDS, "interpolate")
+        lens = (c_size_t * self.n)(*[len(a) for a in arrs])
+        ptrs = (c_void_p * self.n)(*[(a.ctypes.data if len(a) else None) for a in arrs])
+        S = max(len(a) for a in arrs)
+        value = np.zeros(max(self.k * S, 1), dtype=np.uint8)
+        vlen = c_size_t(0)
+        dig = np.zeros(32, dtype=np.uint8)
+        r = _bytes_array(root)
+        check(lib.rbc_interpolate(self._p, _ptr(r), ptrs, lens, _ptr(value), value.nbytes, byref(vlen), _ptr(dig)),
+              "rbc_interpolate")
+        return {"value": bytes(value[: vlen.value]), "digest": bytes(dig)}
+
+    # ---- host batch API ---------------------------------------------------
+    def shard_commit_batch(self, values: Sequence[bytes]) -> dict:
+        count = len(values)
+        arrs = [_bytes_array(v) for v in values]
+        Smax = max((len(a) + self.k - 1) // self.k for a in arrs)
+        pitch = Smax
+        shards = np.zeros((count, self.n, pitch), dtype=np.uint8)
+        roots = np.zeros((count, 32), dtype=np.uint8)
+        br = np.zeros((count, self.n, max(self.depth, 1), 32), dtype=np.uint8)
+        slens = np.zeros(count, dtype=np.uint32)
+        vlens = (c_size_t * count)(*[len(a) for a in arrs])
+        vptrs = (c_void_p * count)(*[a.ctypes.data if len(a) else None for a in arrs])
+        t = c_uint64(0)
+        check(lib.rbc_shard_commit(self._p, count, vptrs, vlens, _ptr(shards), pitch,
+                                   slens.ctypes.data_as(_lib.u32p), _ptr(roots), _ptr(br), byref(t)),
+              "rbc_shard_commit")
+        check(lib.rbc_wait(self._p, t.value))
+        return {"shards": shards, "shard_lens": slens, "roots": roots, "branches": br[:, :, : self.depth]}
+
+    def validate_batch(self, shards, indices, branches, roots) -> np.ndarray:
+        count = len(shards)
+        sh = [_bytes_array(s) for s in shards]
+        br = [_bytes_array(b) for b in branches]
+        rt = [_bytes_array(r) for r in roots]
+        slens = (c_size_t * count)(*[len(s) for s in sh])
+        blens = (c_size_t * count)(*[len(b) for b in br])
+        sp = (c_void_p * count)(*[s.ctypes.data if len(s) else None for s in sh])
+        bp = (c_void_p * count)(*[b.ctypes.data if len(b) else None for b in br])
+        rp = (c_void_p * count)(*[r.ctypes.data for r in rt])
+        idx = (c_uint32 * count)(*[int(i) for i in indices])
+        ok = np.zeros(count, dtype=np.uint8)
+        t = c_uint64(0)
+        check(lib.rbc_validate_batch(self._p, count, sp, slens, idx, bp, blens, rp, _ptr(ok), byref(t)),
+              "rbc_validate_batch")
+        return ok.astype(bool)
+
+    def interpolate_batch(self, shards: np.ndarray, shard_lens, present: np.ndarray, roots: np.ndarray) -> dict:
+        shards = np.ascontiguousarray(shards, dtype=np.uint8)
+        count, n, pitch = shards.shape
+        assert n == self.n
+        present = np.ascontiguousarray(present, dtype=np.uint8)
+        roots = np.ascontiguousarray(roots, dtype=np.uint8)
+        sl = (c_size_t * count)(*[int(x) for x in shard_lens])
+        Smax = int(max(shard_lens))
+        vp = self.k * Smax
+        values = np.zeros((count, max(vp, 1)), dtype=np.uint8)
+        digests = np.zeros((count, 32), dtype=np.uint8)
+        status = np.zeros(count, dtype=np.int32)
+        t = c_uint64(0)
+        check(lib.rbc_interpolate_batch(self._p, count, _ptr(shards), pitch, sl, _ptr(present), _ptr(roots),
+                                        _ptr(values), values.shape[1], _ptr(digests),
+                                        status.ctypes.data_as(_lib.i32p), byref(t)), "rbc_interpolate_batch")
+        return {"values": values, "digests": digests, "status": status}
+
+    # ---- device-resident stages --------------------------------------------
+    def dev_encode(self, stream, count, values, value_pitch, value_lens, uniform_len, shards, shard_pitch):
+        check(lib.rbc_dev_encode(self._p, _dv(stream), count, _dv(values), value_pitch, _dv(value_lens),
+                                 uniform_len, _dv(shards), shard_pitch), "rbc_dev_encode")
+
+    def dev_leaves(self, stream, count, shards, shard_pitch, shard_lens, uniform_len, leaves):
+        check(lib.rbc_dev_leaves(self._p, _dv(stream), count, _dv(shards), shard_pitch, _dv(shard_lens),
+                                 uniform_len, _dv(leaves)), "rbc_dev_leaves")
+
+    def dev_merkle_build(self, stream, count, leaves, roots, branches):
+        check(lib.rbc_dev_merkle_build(self._p, _dv(stream), count, _dv(leaves), _dv(roots), _dv(branches)),
+              "rbc_dev_merkle_build")
+
+    def dev_shard_commit(self, stream, count, values, value_pitch, value_lens, uniform_len, shards, shard_pitch,
+                         shard_lens, leaves, roots, branches):
+        check(lib.rbc_dev_shard_commit(self._p, _dv(stream), count, _dv(values), value_pitch, _dv(value_lens),
+                                       uniform_len, _dv(shards), shard_pitch, _dv(shard_lens), _dv(leaves),
+                                       _dv(roots), _dv(branches)), "rbc_dev_shard_commit")
+
+    def dev_verify(self, stream, count, shards, shard_pitch, shard_lens, uniform_len, branches, roots, present,
+                   valid, leaves):
+        check(lib.rbc_dev_verify(self._p, _dv(stream), count, _dv(shards), shard_pitch, _dv(shard_lens),
+                                 uniform_len, _dv(branches), _dv(roots), _dv(present), _dv(valid), _dv(leaves)),
+              "rbc_dev_verify")
+
+    def dev_interpolate(self, stream, count, shards, shard_pitch, shard_lens, uniform_len, valid, leaves,
+                        leaves_verified, roots, values_out, value_pitch, digests, status):
+        check(lib.rbc_dev_interpolate(self._p, _dv(stream), count, _dv(shards), shard_pitch, _dv(shard_lens),
+                                      uniform_len, _dv(valid), _dv(leaves), int(leaves_verified), _dv(roots),
+                                      _dv(values_out), value_pitch, _dv(digests), _dv(status)),
+              "rbc_dev_interpolate")
+
+    def dev_inject_faults(self, stream, count, shards, shard_pitch, corrupt):
+        check(lib.rbc_dev_inject_faults(self._p, _dv(stream), count, _dv(shards), shard_pitch, _dv(corrupt)),
+              "rbc_dev_inject_faults")
+
+    # ---- multi-GPU ------------------------------------------------------------
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = np.zeros(128, dtype=np.uint8)
+        check(lib.rbc_comm_unique_id(_ptr(buf)), "rbc_comm_unique_id")
+        return bytes(buf)
+
+    def comm_init(self, nranks: int, rank: int, uid: bytes) -> None:
+        b = np.frombuffer(uid, dtype=np.uint8).copy()
+        check(lib.rbc_comm_init(self._p, nranks, rank, _ptr(b)), "rbc_comm_init")
+
+    def dev_allgather_roots(self, stream, count, roots, digests, gathered) -> None:
+        check(lib.rbc_dev_allgather_roots(self._p, _dv(stream), count, _dv(roots), _dv(digests), _dv(gathered)),
+              "rbc_dev_allgather_roots")
+
+
+class Encoder:
+    """reedsolomon.Encoder mirror (klauspost v1.9.1 semantics), GPU-backed."""
+
+    def __init__(self, data_shards: int, parity_shards: int, device: int = 0):
+        p = c_void_p()
+        check(lib.rbc_rs_new(data_shards, parity_shards, device, byref(p)), "reedsolomon.New")
+        self._p = p
+        self.data_shards, self.parity_shards = data_shards, parity_shards
+        self.shards = data_shards + parity_shards
+
+    def __del__(self):
+        try:
+            if self._p:
+                lib.rbc_rs_free(self._p)
+        except Exception:
+            pass
+
+    @staticmethod
+    def _pack(shards):
+        arrs = [None if s is None else _bytes_array(s).copy() for s in shards]
+        n = len(arrs)
+        lens = (c_size_t * n)(*[0 if a is None else len(a) for a in arrs])
+        ptrs = (c_void_p * n)(*[(a.ctypes.data if (a is not None and len(a)) else None) for a in arrs])
+        return arrs, lens, ptrs
+
+    def encode(self, shards: List) -> None:
+        arrs, lens, ptrs = self._pack(shards)
+        check(lib.rbc_rs_encode(self._p, ptrs, lens, len(arrs)), "Encode")
+        for i in range(self.data_shards, min(len(arrs), self.shards)):
+            shards[i] = arrs[i]
+
+    def verify(self, shards) -> bool:
+        arrs, lens, ptrs = self._pack(shards)
+        ok = c_int(0)
+        check(lib.rbc_rs_verify(self._p, ptrs, lens, len(arrs), byref(ok)), "Verify")
+        return bool(ok.value)
+
+    def _reconstruct(self, shards: List, data_only: bool) -> None:
+        arrs = [None if s is None else _bytes_array(s).copy() for s in shards]
+        size = max([len(a) for a in arrs if a is not None] + [0])
+        n = len(arrs)
+        bufs = [a if (a is not None and len(a)) else np.zeros(max(size, 1), dtype=np.uint8) for a in arrs]
+        lens = (c_size_t * n)(*[0 if (a is None) else len(a) for a in arrs])
+        ptrs = (c_void_p * n)(*[b.ctypes.data for b in bufs])
+        fn = lib.rbc_rs_reconstruct_data if data_only else lib.rbc_rs_reconstruct
+        check(fn(self._p, ptrs, lens, n), "ReconstructData" if data_only else "Reconstruct")
+        for i in range(n):
+            if lens[i]:
+                shards[i] = bufs[i][: lens[i]].copy()
+
+    def reconstruct(self, shards: List) -> None:
+        self._reconstruct(shards, False)
+
+    def reconstruct_data(self, shards: List) -> None:
+        self._reconstruct(shards, True)
+
+    def split(self, data) -> List[np.ndarray]:
+        d = _bytes_array(data)
+        per = c_size_t(0)
+        per_est = (len(d) + self.data_shards - 1) // self.data_shards if len(d) else 0
+        out = np.zeros(max(self.shards * per_est, 1), dtype=np.uint8)
+        check(lib.rbc_rs_split(self._p, _ptr(d) if len(d) else None, len(d), _ptr(out), out.nbytes, byref(per)),
+              "Split")
+        p = per.value
+        return [out[i * p:(i + 1) * p].copy() for i in range(self.shards)]
+
+    def join(self, shards, out_size: int) -> bytes:
+        arrs = [None if s is None else _bytes_array(s) for s in shards]
+        n = len(arrs)
+        lens = (c_size_t * n)(*[0 if a is None else len(a) for a in arrs])
+        ptrs = (c_void_p * n)(*[(None if a is None else (a.ctypes.data if len(a) else 1)) for a in arrs])
+        out = np.zeros(max(out_size, 1), dtype=np.uint8)
+        check(lib.rbc_rs_join(self._p, ptrs, lens, n, out_size, _ptr(out)), "Join")
+        return bytes(out[:out_size])

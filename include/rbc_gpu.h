@@ -1,0 +1,216 @@
+/*
+ * rbc_gpu.h -- C ABI of the MI355X-native Reliable Broadcast data path.
+ *
+ * This is the drop-in boundary for joomanzi/cleisthenes' rbc package: the Go
+ * handlers (rbc/rbc.go:47-66) and the pb layout (pb/message.proto:25-35) stay
+ * unchanged; the three data-path functions and the third-party encoder they
+ * hold are served from here through a thin cgo shim:
+ *
+ *   rbc/rbc.go:97-100  shard(enc, data) ([][]byte, error)     -> rbc_shard / rbc_shard_commit
+ *   rbc/rbc.go:92-95   validateMessage(echo *EchoRequest) bool -> rbc_validate_message / rbc_validate_batch
+ *   rbc/rbc.go:86-90   interpolate(rootHash, shards) ([]byte, error)
+ *                                                             -> rbc_interpolate / rbc_interpolate_batch
+ *   rbc/rbc.go:42      broadcast(VAL): needs root + per-shard branch (Merkle build)
+ *                                                             -> rbc_shard_commit / rbc_dev_merkle_build
+ *   rbc/rbc.go:20      enc reedsolomon.Encoder (klauspost v1.9.1, go.mod:10)
+ *                                                             -> rbc_rs_* (New/Split/Encode/Verify/
+ *                                                                Reconstruct/ReconstructData/Join)
+ *   (BASELINE north_star (5)) ACS output assembly over xGMI  -> rbc_comm_* + rbc_dev_allgather_roots
+ *
+ * Plain pointers and sizes only.  All functions return an int status
+ * (RBC_OK = 0 or a negative RBC_ERR_*); rbc_strerror() names it.
+ * Error values map 1:1 onto klauspost/reedsolomon v1.9.1's error variables
+ * plus ROOT_MISMATCH (interpolate's Merkle recheck) and DEVICE.
+ *
+ * Frozen Merkle convention: leaf = SHA-256(shard, S bytes),
+ * node = SHA-256(left || right), bottom row padded to a power of two with EMPTY
+ * leaves that contribute no bytes.  A branch is d = ceil(log2 N) sibling digests
+ * leaf -> root; the flat Go form (rbc/request.go:11 `Branch []byte`) omits the
+ * level-0 sibling when it is empty ((index ^ 1) >= N), the device form keeps a
+ * zero-filled 32-byte slot there ([N][d][32]).
+ *
+ * Thread safety: every entry point may be called from many threads (the Go
+ * batcher's goroutines).  A context serialises its own submissions with a
+ * mutex; device-resident (rbc_dev_*) calls on one context must be ordered on
+ * one HIP stream (they share the context's decode workspace).
+ */
+#ifndef RBC_GPU_H
+#define RBC_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RBC_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------- */
+#define RBC_OK 0
+#define RBC_ERR_INV_SHARD_NUM (-1)        /* reedsolomon.ErrInvShardNum         */
+#define RBC_ERR_MAX_SHARD_NUM (-2)        /* reedsolomon.ErrMaxShardNum         */
+#define RBC_ERR_TOO_FEW_SHARDS (-3)       /* reedsolomon.ErrTooFewShards        */
+#define RBC_ERR_SHARD_NO_DATA (-4)        /* reedsolomon.ErrShardNoData         */
+#define RBC_ERR_SHARD_SIZE (-5)           /* reedsolomon.ErrShardSize           */
+#define RBC_ERR_SHORT_DATA (-6)           /* reedsolomon.ErrShortData           */
+#define RBC_ERR_RECONSTRUCT_REQUIRED (-7) /* reedsolomon.ErrReconstructRequired */
+#define RBC_ERR_ROOT_MISMATCH (-8)        /* interpolate: Merkle root recheck   */
+#define RBC_ERR_DEVICE (-9)               /* HIP / RCCL failure                 */
+#define RBC_ERR_INVALID_ARG (-10)
+#define RBC_ERR_SINGULAR (-11)            /* internal: singular sub-matrix      */
+#define RBC_ERR_NO_COMM (-12)             /* multi-GPU call before rbc_comm_init */
+
+const char *rbc_strerror(int status);
+int rbc_abi_version(void);
+int rbc_device_count(int *count);
+
+/* ---- context: one (N, f) RBC geometry on one GPU ------------------------
+ * rbc/rbc.go:9-20 keeps n, f and `enc` per RBC; N-2f data shards, 2f parity. */
+typedef struct rbc_ctx rbc_ctx;
+int rbc_ctx_create(int n, int f, int device, rbc_ctx **out);
+void rbc_ctx_destroy(rbc_ctx *ctx);
+int rbc_ctx_params(const rbc_ctx *ctx, int *k, int *p, int *depth);
+/* klauspost buildMatrix(k, n) as used by this context: n*k bytes, row-major */
+int rbc_ctx_encode_matrix(const rbc_ctx *ctx, uint8_t *out);
+
+/* ---- device memory / streams / events (so a host runtime needs no other
+ *      GPU library to drive the rbc_dev_* path) ---------------------------- */
+int rbc_dev_malloc(int device, size_t bytes, void **ptr);
+int rbc_dev_free(void *ptr);
+int rbc_dev_memset(void *ptr, int value, size_t bytes);
+int rbc_memcpy_h2d(void *dst, const void *src, size_t bytes);
+int rbc_memcpy_d2h(void *dst, const void *src, size_t bytes);
+int rbc_host_alloc(size_t bytes, void **ptr); /* pinned (hipHostMalloc) */
+int rbc_host_free(void *ptr);
+int rbc_stream_create(int device, void **stream);
+int rbc_stream_destroy(void *stream);
+int rbc_stream_sync(void *stream);
+int rbc_event_create(void **event);
+int rbc_event_destroy(void *event);
+int rbc_event_record(void *event, void *stream);
+int rbc_event_elapsed_ms(void *start, void *stop, float *ms);
+int rbc_device_sync(int device);
+
+/* ---- device-resident batch stages -----------------------------------------
+ * All buffers are device memory laid out per DESIGN.md section 4; `stream` is a
+ * hipStream_t (NULL = default).  `count` RBC instances per call.  Lengths are
+ * per instance (device uint32 array) or, when that pointer is NULL, uniform.
+ * shard_pitch % 64 == 0 and >= S_i; value rows must be readable for
+ * round_up(k*S_i, 16) + 16 bytes (value_pitch >= that; contents past B_i are
+ * ignored -- the Split zero pad is produced by masking).                    */
+
+/* shard(): Split + Encode.  values [count][value_pitch] (B_i bytes used) ->
+ * shards [count][n][shard_pitch] (data rows 0..k-1 + parity rows k..n-1;
+ * bytes past S_i = ceil(B_i/k) zeroed). */
+int rbc_dev_encode(rbc_ctx *ctx, void *stream, int count, const uint8_t *values, uint64_t value_pitch,
+                   const uint32_t *value_lens, uint32_t uniform_value_len, uint8_t *shards,
+                   uint32_t shard_pitch);
+/* leaves [count][n][32] = SHA-256 of each shard's S_i bytes. */
+int rbc_dev_leaves(rbc_ctx *ctx, void *stream, int count, const uint8_t *shards, uint32_t shard_pitch,
+                   const uint32_t *shard_lens, uint32_t uniform_shard_len, uint8_t *leaves);
+/* Merkle build: roots [count][32], branches [count][n][d][32] (nullable). */
+int rbc_dev_merkle_build(rbc_ctx *ctx, void *stream, int count, const uint8_t *leaves, uint8_t *roots,
+                         uint8_t *branches);
+/* encode + leaves + Merkle build in one call (VAL construction). */
+int rbc_dev_shard_commit(rbc_ctx *ctx, void *stream, int count, const uint8_t *values, uint64_t value_pitch,
+                         const uint32_t *value_lens, uint32_t uniform_value_len, uint8_t *shards,
+                         uint32_t shard_pitch, const uint32_t *shard_lens, uint8_t *leaves, uint8_t *roots,
+                         uint8_t *branches);
+/* ECHO-side validateMessage for every (instance, shard j): hash shard j,
+ * walk branch j, compare with roots[i].  valid[i][j] = present[i][j] && ok
+ * (present nullable = all).  leaves [count][n][32] (nullable) receives the
+ * shard hashes for interpolate's recheck. */
+int rbc_dev_verify(rbc_ctx *ctx, void *stream, int count, const uint8_t *shards, uint32_t shard_pitch,
+                   const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *branches,
+                   const uint8_t *roots, const uint8_t *present, uint8_t *valid, uint8_t *leaves);
+/* interpolate(): from the first k valid shards by index (klauspost rule)
+ * regenerate every other position of the full re-encoding IN PLACE in
+ * `shards`, recompute the Merkle root and compare with roots[i]; on success
+ * write value = data shards 0..k-1 concatenated (k*S_i bytes, pad kept) to
+ * values_out [count][value_pitch] and the batch digest
+ * SHA-256(leaf_0 || .. || leaf_{k-1}) to digests [count][32].
+ * status[i]: RBC_OK, RBC_ERR_TOO_FEW_SHARDS or RBC_ERR_ROOT_MISMATCH.
+ * leaves_verified != 0: `leaves` already holds SHA-256 of the valid shards
+ * (rbc_dev_verify output) and only regenerated rows are hashed; 0: all rows. */
+int rbc_dev_interpolate(rbc_ctx *ctx, void *stream, int count, uint8_t *shards, uint32_t shard_pitch,
+                        const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *valid,
+                        uint8_t *leaves, int leaves_verified, const uint8_t *roots, uint8_t *values_out,
+                        uint32_t value_pitch, uint8_t *digests, int32_t *status);
+/* Synthetic Byzantine input for tests/bench: shards[i][corrupt[i]][0] ^= 0x5a
+ * for every i with corrupt[i] >= 0 (corrupt: device int32[count]). */
+int rbc_dev_inject_faults(rbc_ctx *ctx, void *stream, int count, uint8_t *shards, uint32_t shard_pitch,
+                          const int32_t *corrupt);
+
+/* ---- host-memory batch API (the Go batcher's entry points) ----------------
+ * Copies through pinned staging on the context's own stream.  Each call
+ * returns a ticket; rbc_wait / rbc_poll complete it (no C->Go callbacks).
+ * Caller buffers must stay valid until the ticket completes. */
+/* shard() + Merkle commit for `count` proposals: values[i] (value_lens[i] bytes)
+ * -> shards_out [count][n][shard_pitch] (S_i bytes per row used),
+ * shard_lens_out [count] (S_i), roots_out [count][32],
+ * branches_out [count][n][d][32] (nullable). */
+int rbc_shard_commit(rbc_ctx *ctx, int count, const uint8_t *const *values, const size_t *value_lens,
+                     uint8_t *shards_out, size_t shard_pitch, uint32_t *shard_lens_out, uint8_t *roots_out,
+                     uint8_t *branches_out, uint64_t *ticket);
+/* validateMessage for `count` independent ECHO messages: shard i
+ * (shard_lens[i] bytes), leaf index indices[i], flat branch (branch_lens[i]
+ * bytes, Go form), root (32 bytes).  ok_out[i] = 1 valid / 0 invalid. */
+int rbc_validate_batch(rbc_ctx *ctx, int count, const uint8_t *const *shards, const size_t *shard_lens,
+                       const uint32_t *indices, const uint8_t *const *branches, const size_t *branch_lens,
+                       const uint8_t *const *roots, uint8_t *ok_out, uint64_t *ticket);
+/* interpolate() for `count` instances: shards [count][n][shard_pitch] with
+ * present [count][n] (0 = missing, the Go `len == 0`), shard_lens [count],
+ * roots [count][32] -> values_out [count][value_pitch] (k*S_i bytes),
+ * digests_out [count][32] (nullable), status_out [count]. */
+int rbc_interpolate_batch(rbc_ctx *ctx, int count, const uint8_t *shards, size_t shard_pitch,
+                          const size_t *shard_lens, const uint8_t *present, const uint8_t *roots,
+                          uint8_t *values_out, size_t value_pitch, uint8_t *digests_out, int32_t *status_out,
+                          uint64_t *ticket);
+int rbc_wait(rbc_ctx *ctx, uint64_t ticket);
+int rbc_poll(rbc_ctx *ctx, uint64_t ticket, int *done);
+
+/* ---- single-call drop-ins (batch of one, synchronous) --------------------- */
+/* shard(enc, data) + commit: shards_out n*S bytes (shard j at j*S),
+ * *shard_len_out = S, root_out 32 B, branches_out n*d*32 B (nullable). */
+int rbc_shard(rbc_ctx *ctx, const uint8_t *data, size_t len, uint8_t *shards_out, size_t shards_cap,
+              size_t *shard_len_out, uint8_t *root_out, uint8_t *branches_out);
+/* validateMessage(echo): *ok = 1 iff the branch proves shard at `index` under root. */
+int rbc_validate_message(rbc_ctx *ctx, const uint8_t *root, const uint8_t *branch, size_t branch_len,
+                         const uint8_t *shard, size_t shard_len, uint32_t index, int *ok);
+/* interpolate(rootHash, shards): shards[j] with lens[j] (0 = missing);
+ * value_out capacity k*S; *value_len = k*S; digest_out 32 B (nullable). */
+int rbc_interpolate(rbc_ctx *ctx, const uint8_t *root, const uint8_t *const *shards, const size_t *lens,
+                    uint8_t *value_out, size_t value_cap, size_t *value_len, uint8_t *digest_out);
+
+/* ---- reedsolomon.Encoder mirror (klauspost v1.9.1 semantics) ---------------
+ * Shards are host buffers; lens[i] == 0 marks a missing shard (Go len 0).
+ * Reconstruct writes missing shards into the caller's buffers (capacity >= the
+ * shard size) and sets their lens; present shards are never modified. */
+typedef struct rbc_rs rbc_rs;
+int rbc_rs_new(int data_shards, int parity_shards, int device, rbc_rs **out); /* reedsolomon.New */
+void rbc_rs_free(rbc_rs *rs);
+int rbc_rs_encode(rbc_rs *rs, uint8_t *const *shards, const size_t *lens, int n_shards);
+int rbc_rs_verify(rbc_rs *rs, const uint8_t *const *shards, const size_t *lens, int n_shards, int *ok);
+int rbc_rs_reconstruct(rbc_rs *rs, uint8_t *const *shards, size_t *lens, int n_shards);
+int rbc_rs_reconstruct_data(rbc_rs *rs, uint8_t *const *shards, size_t *lens, int n_shards);
+/* Split: out receives n*per bytes (shard i at i*per); *per_shard = per. */
+int rbc_rs_split(rbc_rs *rs, const uint8_t *data, size_t len, uint8_t *out, size_t out_cap, size_t *per_shard);
+/* Join: first k shards, out_size bytes; a NULL shard pointer is Go `nil`. */
+int rbc_rs_join(rbc_rs *rs, const uint8_t *const *shards, const size_t *lens, int n_shards, size_t out_size,
+                uint8_t *dst);
+
+/* ---- multi-GPU: RCCL all-gather of {root, digest} over xGMI ----------------
+ * One process per GPU.  Rank 0 creates the id, the host runtime broadcasts
+ * its 128 bytes, every rank calls rbc_comm_init.  gathered receives
+ * [nranks][count][64] = {root[32], digest[32]} per instance (ACS output set). */
+int rbc_comm_unique_id(uint8_t id_out[128]);
+int rbc_comm_init(rbc_ctx *ctx, int nranks, int rank, const uint8_t id[128]);
+int rbc_comm_destroy(rbc_ctx *ctx);
+int rbc_dev_allgather_roots(rbc_ctx *ctx, void *stream, int count, const uint8_t *roots,
+                            const uint8_t *digests, uint8_t *gathered);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RBC_GPU_H */
