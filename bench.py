@@ -1,0 +1,281 @@
+#!/usr/bin/env python3
+"""RBC data-path benchmark (BASELINE.json metric: "RBC shard GB/s (RS
+encode+decode + Merkle verify) per GPU & node, N=128").
+
+One step = one full RBC round of the data path over a batch of I instances
+resident in HBM (default C2: N=128, f=42, 1 MiB values, I=1024 per GPU):
+  1. shard+commit   rbc_dev_encode (Split+Encode), rbc_dev_leaves (SHA-256 of
+                    every shard), rbc_dev_merkle_build (root + N branches)
+  2. Byzantine input: 10 % of instances get one corrupted ECHO shard
+  3. ECHO verify    rbc_dev_verify: validateMessage for all N shards of every
+                    instance (hash shard + walk branch + compare root)
+  4. interpolate    rbc_dev_interpolate: first k valid of a seeded N-f
+                    present set -> regenerate the other N-k positions,
+                    re-hash them, recheck the root, emit value + digest
+  5. (N GPUs > 1)   RCCL all-gather of {root, digest} over xGMI (ACS set)
+value = I * N * S bytes of committed shard output per step, summed over all
+ranks, / (max over ranks of the timed wall time).
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run (one process per GPU).  Host-side coordination uses
+torch.distributed with the gloo backend (CPU tensors); all GPU work, including
+the RCCL all-gather, goes through librbc_gpu.so.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (N, f, value bytes, instances per GPU, description)
+    "c1": (64, 21, 1 << 20, 1024, "N=64 f=21 1MiB x1024"),
+    "c2": (128, 42, 1 << 20, 1024, "N=128 f=42 1MiB x1024"),
+    "c3": (128, 42, 4 << 20, 1024, "N=128 f=42 4MiB x1024 per GPU (8192 over 8 GPUs)"),
+    "c4": (256, 85, 64 << 10, 16384, "N=256 f=85 64KiB x16384"),
+}
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9  # 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz
+
+
+def round_up(x, a):
+    return (x + a - 1) // a * a
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--instances", type=int, default=0, help="override instances per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-instances", type=int, default=256)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # host-side coordination only (gloo, CPU tensors)
+        dist.init_process_group("gloo")
+
+    import cleisthenes_amd as ca
+
+    n, f, B, inst, desc = CONFIGS[args.config]
+    if args.instances:
+        inst = args.instances
+    dev = local_rank
+    ctx = ca.Context(n, f, device=dev)
+    k, d = ctx.k, ctx.depth
+    S = (B + k - 1) // k
+    spitch = round_up(S, 64)
+    vpitch = round_up(k * S + 32, 64)
+    opitch = round_up(k * S, 16)
+    I = inst
+
+    # ---- synthetic inputs (seeded per rank), uploaded once ----------------
+    rng = np.random.default_rng(20261015 + rank)
+    values_h = rng.integers(0, 256, size=(I, vpitch), dtype=np.uint8)
+    present_h = np.zeros((I, n), dtype=np.uint8)
+    corrupt_h = np.full(I, -1, dtype=np.int32)
+    for i in range(I):
+        pres = rng.permutation(n)[: n - f]
+        present_h[i, pres] = 1
+        if rng.random() < 0.10:
+            corrupt_h[i] = int(rng.choice(pres))
+
+    mb = lambda x: ca.DeviceBuffer(x, device=dev)  # noqa: E731
+    d_values = mb(I * vpitch)
+    d_values.upload(values_h)
+    del values_h
+    d_shards = mb(I * n * spitch)
+    d_leaves_p = mb(I * n * 32)
+    d_roots = mb(I * 32)
+    d_branches = mb(I * n * max(d, 1) * 32)
+    d_present = mb(I * n)
+    d_present.upload(present_h)
+    d_corrupt = mb(I * 4)
+    d_corrupt.upload(corrupt_h)
+    d_valid = mb(I * n)
+    d_leaves_r = mb(I * n * 32)
+    d_out = mb(I * opitch)
+    d_digests = mb(I * 32)
+    d_status = mb(I * 4)
+    d_gather = mb(world * I * 64) if world > 1 else None
+
+    if world > 1:
+        import torch
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            uid = torch.frombuffer(bytearray(ca.Context.comm_unique_id()), dtype=torch.uint8).clone()
+        dist.broadcast(uid, 0)
+        ctx.comm_init(world, rank, bytes(uid.numpy().tobytes()))
+
+    stream = ca.Stream(dev)
+    ev = {name: ca.Event() for name in ("t0", "enc", "leaf", "tree", "fault", "verify", "interp", "gather")}
+
+    def step(timed):
+        if timed:
+            ev["t0"].record(stream)
+        ctx.dev_encode(stream.ptr, I, d_values, vpitch, None, B, d_shards, spitch)
+        if timed:
+            ev["enc"].record(stream)
+        ctx.dev_leaves(stream.ptr, I, d_shards, spitch, None, S, d_leaves_p)
+        if timed:
+            ev["leaf"].record(stream)
+        ctx.dev_merkle_build(stream.ptr, I, d_leaves_p, d_roots, d_branches)
+        if timed:
+            ev["tree"].record(stream)
+        ctx.dev_inject_faults(stream.ptr, I, d_shards, spitch, d_corrupt)
+        if timed:
+            ev["fault"].record(stream)
+        ctx.dev_verify(stream.ptr, I, d_shards, spitch, None, S, d_branches, d_roots, d_present, d_valid,
+                       d_leaves_r)
+        if timed:
+            ev["verify"].record(stream)
+        ctx.dev_interpolate(stream.ptr, I, d_shards, spitch, None, S, d_valid, d_leaves_r, 1, d_roots, d_out,
+                            opitch, d_digests, d_status)
+        if timed:
+            ev["interp"].record(stream)
+        if world > 1:
+            ctx.dev_allgather_roots(stream.ptr, I, d_roots, d_digests, d_gather)
+        if timed:
+            ev["gather"].record(stream)
+
+    def barrier():
+        stream.sync()
+        ca.rbc.lib.rbc_device_sync(dev)
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step(False)
+    barrier()
+    # correctness guard on the warmed-up state: every instance must decode
+    status = np.frombuffer(d_status.download().tobytes(), dtype=np.int32)
+    n_ok = int((status == 0).sum())
+
+    stage_ms = {kk: 0.0 for kk in ("enc", "leaf", "tree", "fault", "verify", "interp", "gather")}
+    order = ["t0", "enc", "leaf", "tree", "fault", "verify", "interp", "gather"]
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+        stream.sync()
+        for a, b in zip(order[:-1], order[1:]):
+            stage_ms[b] += ev[a].elapsed_ms(ev[b])
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        okt = torch.tensor([n_ok], dtype=torch.int64)
+        dist.all_reduce(okt)
+        n_ok = int(okt.item())
+
+    for kk in stage_ms:
+        stage_ms[kk] /= args.steps
+    ms_per_step = elapsed * 1000.0 / args.steps
+    shard_bytes = I * n * S
+    value = shard_bytes * world * args.steps / elapsed / 1e9
+
+    # ---- roofline of the dominant kernel --------------------------------
+    blocks_per_shard = (S + 9 + 63) // 64
+    kern = {
+        # name: (avg ms, algorithmic HBM bytes per launch, sha compressions per launch)
+        "gf_rows_kernel<encode>": (stage_ms["enc"], I * (k * S + n * S), 0),
+        "sha_rows_kernel<leaves>": (stage_ms["leaf"], I * (n * S + n * 32), I * n * blocks_per_shard),
+        "sha_rows_kernel<verify>": (stage_ms["verify"], I * (n * S + n * d * 32 + n * 33 + 32 + n),
+                                    I * n * (blocks_per_shard + 2 * d)),
+    }
+    dom = max(kern, key=lambda x: kern[x][0])
+    dms, dbytes, dcomp = kern[dom]
+    achieved = dbytes / (dms / 1e3) / 1e9
+    roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "algorithmic_bytes_per_launch": int(dbytes), "avg_ms": round(dms, 4)}
+    if dcomp:
+        # SHA-256 compressions/s vs the integer-VALU roof (~1.4k VALU ops per compression)
+        cps = dcomp / (dms / 1e3)
+        roof["sha256_compressions_per_s"] = round(cps / 1e9, 3)
+        roof["sha256_compressions_per_s_unit"] = "G/s"
+        roof["valu_frac_est"] = round(cps * 1400.0 / VALU_PEAK_OPS, 4)
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic_r01.json")
+    if os.path.exists(pmc_path):
+        try:
+            pm = json.load(open(pmc_path))
+            if pm.get("config") == args.config and dom in pm.get("kernels", {}):
+                roof["traffic"] = pm["kernels"][dom]["hbm_bytes_per_launch"]
+                roof["traffic_source"] = os.path.relpath(pmc_path, ROOT)
+        except Exception:
+            pass
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(n, f, B, args.cpu_instances, args.cpu_threads)
+
+    line = {
+        "metric": "RBC shard GB/s (RS encode+decode + Merkle verify) per GPU & node, N=128",
+        "value": round(value, 3),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded uniform bytes, 10% instances with one corrupted ECHO shard)",
+        "config": {"workload": f"{args.config}: {desc}; shard+commit, ECHO verify all N, interpolate from N-f",
+                   "n": n, "f": f, "value_bytes": B, "shard_bytes": S, "instances_per_gpu": I,
+                   "parallelism": f"instances partitioned over {world} GPU(s), RCCL root all-gather"},
+        "stage_ms": {kk: round(v, 4) for kk, v in stage_ms.items()},
+        "decoded_ok": n_ok,
+        "roofline": roof,
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(n, f, B, count, threads):
+    """The C restatement (oracle/librbc_ref.so: AVX2 split-nibble GF +
+    SHA-NI) running the same per-instance pipeline on host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import rbc_ref
+
+    k = n - 2 * f
+    S = (B + k - 1) // k
+    rng = np.random.default_rng(7)
+    values = rng.integers(0, 256, size=(count, B), dtype=np.uint8)
+    present = np.zeros((count, n), dtype=np.uint8)
+    corrupt = np.full(count, -1, dtype=np.int32)
+    for i in range(count):
+        pres = rng.permutation(n)[: n - f]
+        present[i, pres] = 1
+        if rng.random() < 0.10:
+            corrupt[i] = int(rng.choice(pres))
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    secs, st = rbc_ref.pipeline(n, f, count, B, threads, values, present, corrupt)
+    feats = rbc_ref.lib().rbcref_cpu_features()
+    return {"value": round(count * n * S / secs / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"{count} instances x {B} B, N={n} f={f}, same per-instance pipeline, {secs:.2f} s wall",
+            "simd": ("avx2 " if feats & 1 else "") + ("sha-ni" if feats & 2 else ""), "status_sum": st}
+
+
+if __name__ == "__main__":
+    main()

@@ -9,6 +9,8 @@
 #include <rccl/rccl.h>
 #include <string.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 #include <mutex>
 #include <vector>
@@ -21,6 +23,16 @@ namespace {
 
 constexpr size_t kAlign = 64;
 inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// rows per GF chunk (accumulators held in VGPRs); RBC_GF_RCMAX overrides
+int gf_rcmax() {
+    static const int v = [] {
+        const char *e = getenv("RBC_GF_RCMAX");
+        int x = e ? atoi(e) : 0;
+        return (x >= 1 && x <= 48) ? x : 28;
+    }();
+    return v;
+}
 
 int tree_width(int n) {
     int w = 1;
@@ -73,7 +85,7 @@ struct rbc_ctx {
     std::mutex mu;
     hipStream_t stream = nullptr;  // host-API stream
     // interpolate workspace (device API)
-    DevBuf ws_used, ws_regen, ws_dmat;
+    DevBuf ws_used, ws_regen, ws_dmat, ws_nmiss, ws_flags, ws_list, ws_counter;
     // host-API staging
     DevBuf d_values, d_shards, d_leaves, d_roots, d_branches, d_valid, d_status, d_digests, d_lens, d_slens,
         d_idx, d_present;
@@ -137,7 +149,7 @@ int stage_encode(rbc_ctx *c, hipStream_t st, int count, const uint8_t *values, u
     g.tiles = (int)((shard_pitch + 4095) / 4096);
     g.R = c->p;
     g.K = c->k;
-    g.rc = rbc_gf_pick_rc(c->p > 0 ? c->p : 1);
+    g.rc = rbc_gf_pick_rc(c->p > 0 ? c->p : 1, gf_rcmax());
     g.mode = GF_MODE_ENCODE;
     g.in = values;
     g.in_inst_pitch = value_pitch;
@@ -229,15 +241,22 @@ int ensure_ws(rbc_ctx *c, int count) {
     RBC_HIP(c->ws_used.ensure((size_t)count * c->k));
     RBC_HIP(c->ws_regen.ensure((size_t)count * nr));
     RBC_HIP(c->ws_dmat.ensure((size_t)count * nr * c->k));
+    RBC_HIP(c->ws_nmiss.ensure((size_t)count * 4));
+    RBC_HIP(c->ws_flags.ensure((size_t)count * c->n * 4));
+    RBC_HIP(c->ws_list.ensure((size_t)count * nr * 4));
+    RBC_HIP(c->ws_counter.ensure(16));
     return RBC_OK;
 }
 
 // decode_prepare + GF regeneration (in place), no hashing
+// compare != 0: valid-but-unused rows are compared, not blindly rewritten,
+// and the rows that need hashing are collected in ws_list
 int stage_regenerate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, uint32_t shard_pitch,
                      const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *valid,
-                     int32_t *status) {
+                     int32_t *status, int compare = 0) {
     int rc = ensure_ws(c, count);
     if (rc) return rc;
+    if (compare) RBC_HIP(hipMemsetAsync(c->ws_counter.p, 0, 16, st));
     const int nr = c->n - c->k;
     PrepArgs pa{};
     pa.count = count;
@@ -253,6 +272,12 @@ int stage_regenerate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, uin
     pa.dmat = c->ws_dmat.as<uint8_t>();
     pa.dmat_stride = (uint64_t)std::max(nr, 1) * c->k;
     pa.status = status;
+    if (compare) {
+        pa.nmiss = c->ws_nmiss.as<int32_t>();
+        pa.flags = c->ws_flags.as<uint32_t>();
+        pa.list = c->ws_list.as<uint32_t>();
+        pa.counter = c->ws_counter.as<uint32_t>();
+    }
     RBC_HIP(rbc_launch_decode_prepare(pa, st));
     if (nr > 0) {
         GfArgs g{};
@@ -260,7 +285,7 @@ int stage_regenerate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, uin
         g.tiles = (int)((shard_pitch + 4095) / 4096);
         g.R = nr;
         g.K = c->k;
-        g.rc = rbc_gf_pick_rc(nr);
+        g.rc = rbc_gf_pick_rc(nr, gf_rcmax());
         g.mode = GF_MODE_DECODE;
         g.in = shards;
         g.in_inst_pitch = (uint64_t)c->n * shard_pitch;
@@ -279,6 +304,13 @@ int stage_regenerate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, uin
         g.idx_stride = pa.used_stride;
         g.idx_stride2 = pa.regen_stride;
         g.status = status;
+        if (compare) {
+            g.nmiss = pa.nmiss;
+            g.flags = pa.flags;
+            g.list = pa.list;
+            g.counter = pa.counter;
+            g.n = c->n;
+        }
         RBC_HIP(rbc_launch_gf_rows(g, st));
     }
     return RBC_OK;
@@ -296,7 +328,8 @@ int stage_interpolate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, ui
         return RBC_ERR_INVALID_ARG;
     if ((uint64_t)c->n * shard_pitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
     if (count == 0) return RBC_OK;
-    int rc = stage_regenerate(c, st, count, shards, shard_pitch, shard_lens, uniform_shard_len, valid, status);
+    int rc = stage_regenerate(c, st, count, shards, shard_pitch, shard_lens, uniform_shard_len, valid, status,
+                              leaves_verified);
     if (rc) return rc;
     const int nr = c->n - c->k;
     ShaArgs a{};
@@ -312,9 +345,11 @@ int stage_interpolate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, ui
     a.n = c->n;
     a.depth = c->depth;
     if (leaves_verified) {
-        a.rows_per_inst = nr;
-        a.idx = c->ws_regen.as<uint8_t>();
-        a.idx_stride = (uint32_t)std::max(nr, 1);
+        // hash only the rows in the device-built list: every missing position
+        // plus any valid-but-unused shard the re-encoding disagreed with
+        a.rows_per_inst = nr;  // grid bound (count * nr entries at most)
+        a.list = c->ws_list.as<uint32_t>();
+        a.list_count = c->ws_counter.as<uint32_t>();
     } else {
         a.rows_per_inst = c->n;
     }
@@ -451,7 +486,8 @@ void rbc_ctx_destroy(rbc_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->comm) (void)ncclCommDestroy(c->comm);
-    for (DevBuf *b : {&c->ws_used, &c->ws_regen, &c->ws_dmat, &c->d_values, &c->d_shards, &c->d_leaves,
+    for (DevBuf *b : {&c->ws_used, &c->ws_regen, &c->ws_dmat, &c->ws_nmiss, &c->ws_flags, &c->ws_list,
+                      &c->ws_counter, &c->d_values, &c->d_shards, &c->d_leaves,
                       &c->d_roots, &c->d_branches, &c->d_valid, &c->d_status, &c->d_digests, &c->d_lens,
                       &c->d_slens, &c->d_idx, &c->d_present, &c->h_stage, &c->h_small, &c->d_pack})
         b->release();

@@ -68,7 +68,7 @@ RBC_DEV void sha256_compress(Sha256State &s, uint32_t (&w)[16]) {
         const uint32_t ch = (e & f) ^ (~e & g);
         const uint32_t t1 = h + S1 + ch + kSHA_K[i] + wi;
         const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
-        const uint32_t mj = (a & b) | (c & (a | b));
+        const uint32_t mj = __builtin_amdgcn_bitop3_b32(a, b, c, 0xe8);  // Maj (symmetric)
         h = g; g = f; f = e; e = d + t1;
         d = c; c = b; b = a; a = t1 + S0 + mj;
     }
@@ -92,12 +92,32 @@ RBC_DEV void load_block_be(const uint8_t *p, uint32_t (&w)[16]) {
 // SHA-256 of `len` bytes at a 16-byte-aligned row whose storage is readable
 // up to round_up(len, 64) (the shard pitch guarantees it).  Byte-exact: the
 // bytes past `len` inside the last block are masked, never hashed.
+RBC_DEV void bswap_block(const uint4 (&q)[4], uint32_t (&w)[16]) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        w[4 * t + 0] = bswap32(q[t].x);
+        w[4 * t + 1] = bswap32(q[t].y);
+        w[4 * t + 2] = bswap32(q[t].z);
+        w[4 * t + 3] = bswap32(q[t].w);
+    }
+}
+RBC_DEV void load_block_raw(const uint8_t *p, uint4 (&q)[4]) {
+    const uint4 *v = reinterpret_cast<const uint4 *>(p);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) q[t] = v[t];
+}
+
 RBC_DEV void sha256_row(const uint8_t *row, uint32_t len, Sha256State &s) {
     sha256_init(s);
     const uint32_t nfull = len >> 6;
     uint32_t w[16];
+    // software pipeline: block b+1's loads are in flight while block b is
+    // compressed (a compression is ~1.4k VALU ops, longer than an HBM miss)
+    uint4 q[4];
+    if (nfull) load_block_raw(row, q);
     for (uint32_t b = 0; b < nfull; ++b) {
-        load_block_be(row + 64u * b, w);
+        bswap_block(q, w);
+        if (b + 1 < nfull) load_block_raw(row + 64u * (b + 1), q);
         sha256_compress(s, w);
     }
     const uint32_t rem = len & 63u;

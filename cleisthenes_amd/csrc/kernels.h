@@ -30,6 +30,15 @@ struct GfArgs {
     const uint8_t *out_idx;    // decode: [I][idx_stride2] output row positions (R regen)
     uint32_t idx_stride, idx_stride2;
     const int32_t *status;     // skip instances with status != 0 (nullable)
+    // decode compare mode (nmiss != nullptr): output rows r >= nmiss[inst] are
+    // present-and-verified shards; they are compared with the regenerated
+    // bytes instead of re-hashed, and only a mismatching row is stored,
+    // flagged and appended to the hash list
+    const int32_t *nmiss;
+    uint32_t *flags;           // [I][n]
+    uint32_t *list;            // (inst << 8 | pos) rows to hash
+    uint32_t *counter;
+    int n;
 };
 
 struct ShaArgs {
@@ -46,6 +55,8 @@ struct ShaArgs {
     uint8_t *leaves;           // [I][N][32] (nullable)
     uint64_t leaves_inst_pitch;
     int per_message;           // 1: each instance is one ECHO message (leaf index = idx[inst])
+    const uint32_t *list;      // list mode: rows (inst << 8 | pos), count in *list_count
+    const uint32_t *list_count;
     // verify
     int n, depth;
     const uint8_t *branches;   // [I][N][d][32]
@@ -79,6 +90,12 @@ struct PrepArgs {
     uint8_t *dmat;             // [I][dmat_stride] = (n-k) x k decode matrix
     uint64_t dmat_stride;
     int32_t *status;           // out
+    // compare mode: regen = [missing..., present-unused...], nmiss[i] = #missing,
+    // missing rows appended to list, flags[i][*] zeroed
+    int32_t *nmiss;
+    uint32_t *flags;
+    uint32_t *list;
+    uint32_t *counter;
 };
 
 struct JoinArgs {
@@ -95,7 +112,7 @@ struct JoinArgs {
     const int32_t *status;
 };
 
-int rbc_gf_pick_rc(int R);
+int rbc_gf_pick_rc(int R, int rcmax);
 hipError_t rbc_launch_gf_rows(const GfArgs &a, hipStream_t st);
 hipError_t rbc_launch_sha_rows(const ShaArgs &a, bool verify, hipStream_t st);
 hipError_t rbc_launch_merkle(const MerkleArgs &a, bool check, hipStream_t st);

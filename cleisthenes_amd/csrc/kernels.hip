@@ -120,6 +120,7 @@ __global__ __launch_bounds__(256) void gf_rows_kernel(GfArgs a) {
 
     // R == 0 (no parity, f = 0) still runs one chunk so Split's copy happens
     const int chunks = a.R > 0 ? (a.R + RC - 1) / RC : 1;
+    const int cmp_from = a.nmiss ? a.nmiss[inst] : 0x7fffffff;
     for (int c = 0; c < chunks; ++c) {
         const int r0 = c * RC;
         const int rows = min(RC, a.R - r0);
@@ -142,9 +143,11 @@ __global__ __launch_bounds__(256) void gf_rows_kernel(GfArgs a) {
         for (int r = 0; r < RC; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0;
 
         const bool do_copy = (c == 0) && a.copy && my_store;
+        // two input pairs in flight ahead of the pair being multiplied
         uint4 xa = load_row(0), xb = load_row(1);
+        uint4 pa = load_row(2), pb = load_row(3);
         for (int j = 0; j < KP; j += 2) {
-            const uint4 na = load_row(j + 2), nb = load_row(j + 3);  // prefetch next pair
+            const uint4 na = load_row(j + 4), nb = load_row(j + 5);
             if (do_copy) {
                 const uint32_t pa = (a.mode == GF_MODE_ENCODE) ? (uint32_t)j : s_in[j];
                 *reinterpret_cast<uint4 *>(a.copy + (size_t)inst * a.out_inst_pitch +
@@ -167,8 +170,10 @@ __global__ __launch_bounds__(256) void gf_rows_kernel(GfArgs a) {
                 acc[r][2] = xor3(acc[r][2], gf_mul4(ta, t2.x, sa2), gf_mul4(tb, t2.y, sb2));
                 acc[r][3] = xor3(acc[r][3], gf_mul4(ta, t2.x, sa3), gf_mul4(tb, t2.y, sb3));
             }
-            xa = na;
-            xb = nb;
+            xa = pa;
+            xb = pb;
+            pa = na;
+            pb = nb;
         }
         if (my_store) {
             const int nvalid = (int)S - (int)my_off;  // zero the bytes past S
@@ -178,7 +183,19 @@ __global__ __launch_bounds__(256) void gf_rows_kernel(GfArgs a) {
                     const uint32_t pos = (a.mode == GF_MODE_ENCODE) ? (uint32_t)(a.K + r0 + r) : s_out[r0 + r];
                     uint4 v = make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
                     if (nvalid < 16) v = mask16(v, nvalid);
-                    *reinterpret_cast<uint4 *>(out_inst + (size_t)pos * a.out_row_pitch + my_off) = v;
+                    uint4 *dst = reinterpret_cast<uint4 *>(out_inst + (size_t)pos * a.out_row_pitch + my_off);
+                    if (cmp_from <= r0 + r) {
+                        // valid shard that was not used: keep it unless the
+                        // re-encoding differs, then overwrite and queue a re-hash
+                        const uint4 o = *dst;
+                        if (o.x != v.x || o.y != v.y || o.z != v.z || o.w != v.w) {
+                            *dst = v;
+                            if (atomicOr(&a.flags[(size_t)inst * a.n + pos], 1u) == 0u)
+                                a.list[atomicAdd(a.counter, 1u)] = ((uint32_t)inst << 8) | pos;
+                        }
+                    } else {
+                        *dst = v;
+                    }
                 }
             }
         }
@@ -193,13 +210,21 @@ __global__ __launch_bounds__(256) void gf_rows_kernel(GfArgs a) {
 template <bool VERIFY>
 __global__ __launch_bounds__(256) void sha_rows_kernel(ShaArgs a) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= a.count * a.rows_per_inst) return;
-    const int inst = t / a.rows_per_inst;
-    const int slot = t - inst * a.rows_per_inst;
+    int inst, pos;
+    if (a.list) {  // compacted (inst, pos) work list built on the device
+        if (t >= (int)*a.list_count) return;
+        const uint32_t e = a.list[t];
+        inst = (int)(e >> 8);
+        pos = (int)(e & 0xffu);
+    } else {
+        if (t >= a.count * a.rows_per_inst) return;
+        inst = t / a.rows_per_inst;
+        const int slot = t - inst * a.rows_per_inst;
+        // per_message: every "instance" is one independent ECHO message whose
+        // leaf index is idx[inst]; otherwise slot -> row position (idx optional)
+        pos = a.idx ? (int)a.idx[(size_t)inst * a.idx_stride + slot] : slot;
+    }
     if (a.status && a.status[inst] != 0) return;
-    // per_message: every "instance" is one independent ECHO message whose
-    // leaf index is idx[inst]; otherwise slot -> row position (idx optional)
-    const int pos = a.idx ? (int)a.idx[(size_t)inst * a.idx_stride + slot] : slot;
     const int rowsel = a.per_message ? 0 : pos;
     const uint32_t S = inst_len(a.lens, a.uniform_len, inst);
     const uint8_t *row = a.rows + (size_t)inst * a.inst_pitch + (size_t)rowsel * a.row_pitch;
@@ -387,15 +412,22 @@ __global__ __launch_bounds__(256) void decode_prepare_kernel(PrepArgs a) {
         }
         s_exp[510] = s_exp[0];
         s_exp[511] = s_exp[1];
-        int nu = 0, nr = 0;
+        // used = first k valid by index (klauspost rule); regen = the missing
+        // positions first, then the valid-but-unused ones
+        int nu = 0, nm = 0;
         const uint8_t *v = a.valid + (size_t)inst * a.valid_stride;
         for (int j = 0; j < n; ++j) {
             if (v[j] && nu < k) s_used[nu++] = (uint8_t)j;
-            else s_regen[nr++] = (uint8_t)j;
+            else if (!v[j]) s_regen[nm++] = (uint8_t)j;
         }
+        int nr = nm;
+        for (int j = 0, seen = 0; j < n; ++j)
+            if (v[j] && seen++ >= k) s_regen[nr++] = (uint8_t)j;
         s_misc[0] = nu;
         s_misc[1] = nr;
-        s_misc[2] = 0;
+        s_misc[2] = (a.counter && nu >= k) ? (int)atomicAdd(a.counter, (unsigned)nm) : 0;
+        if (a.nmiss) a.nmiss[inst] = nm;
+        s_misc[3] = nm;
     }
     __syncthreads();
     auto gmul = [&](uint32_t x, uint32_t y) -> uint32_t {
@@ -406,6 +438,12 @@ __global__ __launch_bounds__(256) void decode_prepare_kernel(PrepArgs a) {
         if (tid == 0) a.status[inst] = RBC_ERR_TOO_FEW_SHARDS;
         return;
     }
+    if (a.counter) {
+        const int base = s_misc[2], nm = s_misc[3];
+        for (int t = tid; t < nm; t += 256) a.list[base + t] = ((uint32_t)inst << 8) | s_regen[t];
+        for (int t = tid; t < n; t += 256) a.flags[(size_t)inst * n + t] = 0;
+    }
+    __syncthreads();  // s_misc[3] (pivot slot) is reused below
     for (int t = tid; t < k; t += 256) a.used[(size_t)inst * a.used_stride + t] = s_used[t];
     for (int t = tid; t < nr; t += 256) a.regen[(size_t)inst * a.regen_stride + t] = s_regen[t];
     for (int e = tid; e < k * k2; e += 256) {
@@ -534,11 +572,19 @@ static hipError_t launch_gf_rc(const GfArgs &a, hipStream_t st) {
     return hipGetLastError();
 }
 
-int rbc_gf_pick_rc(int R) {
-    // fewest chunks of <= 24 rows, then the smallest RC covering them
+static const int kRC[] = {1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16, 17,
+                          18, 19, 20, 21, 22, 23, 24, 26, 28, 30, 32, 36, 40, 42, 44, 48};
+
+int rbc_gf_pick_rc(int R, int rcmax) {
+    // fewest chunks of <= rcmax rows, then the smallest instantiated RC covering them
     if (R <= 0) return 1;
-    const int chunks = (R + 23) / 24;
-    return (R + chunks - 1) / chunks;
+    if (rcmax < 1) rcmax = 1;
+    if (rcmax > 48) rcmax = 48;
+    const int chunks = (R + rcmax - 1) / rcmax;
+    const int want = (R + chunks - 1) / chunks;
+    for (int rc : kRC)
+        if (rc >= want) return rc;
+    return 48;
 }
 
 hipError_t rbc_launch_gf_rows(const GfArgs &a, hipStream_t st) {
@@ -549,6 +595,8 @@ hipError_t rbc_launch_gf_rows(const GfArgs &a, hipStream_t st) {
         RBC_RC_CASE(7) RBC_RC_CASE(8) RBC_RC_CASE(9) RBC_RC_CASE(10) RBC_RC_CASE(11) RBC_RC_CASE(12)
         RBC_RC_CASE(13) RBC_RC_CASE(14) RBC_RC_CASE(15) RBC_RC_CASE(16) RBC_RC_CASE(17) RBC_RC_CASE(18)
         RBC_RC_CASE(19) RBC_RC_CASE(20) RBC_RC_CASE(21) RBC_RC_CASE(22) RBC_RC_CASE(23) RBC_RC_CASE(24)
+        RBC_RC_CASE(26) RBC_RC_CASE(28) RBC_RC_CASE(30) RBC_RC_CASE(32) RBC_RC_CASE(36) RBC_RC_CASE(40)
+        RBC_RC_CASE(42) RBC_RC_CASE(44) RBC_RC_CASE(48)
 #undef RBC_RC_CASE
         default: return hipErrorInvalidValue;
     }

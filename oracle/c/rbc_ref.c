@@ -234,14 +234,13 @@ __attribute__((target("sha,sse4.1,ssse3"))) static void sha_blocks_ni(uint32_t s
     while (nblk--) {
         __m128i A = S0, C = S1, W[4], msg;
         for (int i = 0; i < 16; i++) {
-            if (i < 4) {
-                W[i] = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i *)(p + 16 * i)), MASK);
-            } else {
-                __m128i t = _mm_alignr_epi8(W[(i - 1) & 3], W[(i - 2) & 3], 4);
-                W[i & 3] = _mm_sha256msg2_epu32(_mm_add_epi32(W[i & 3], t), W[(i - 1) & 3]);
-            }
+            if (i < 4) W[i] = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i *)(p + 16 * i)), MASK);
             msg = _mm_add_epi32(W[i & 3], _mm_loadu_si128((const __m128i *)&K256[4 * i]));
             S1 = _mm_sha256rnds2_epu32(S1, S0, msg);
+            if (i >= 3 && i < 15) {  /* next schedule group, before W[i-1] gets msg1 */
+                __m128i t = _mm_alignr_epi8(W[i & 3], W[(i - 1) & 3], 4);
+                W[(i + 1) & 3] = _mm_sha256msg2_epu32(_mm_add_epi32(W[(i + 1) & 3], t), W[i & 3]);
+            }
             msg = _mm_shuffle_epi32(msg, 0x0E);
             S0 = _mm_sha256rnds2_epu32(S0, S1, msg);
             if (i >= 1 && i <= 12) W[(i - 1) & 3] = _mm_sha256msg1_epu32(W[(i - 1) & 3], W[i & 3]);
@@ -345,6 +344,27 @@ int rbcref_merkle_verify(int n, const uint8_t *shard, size_t S, uint32_t index, 
     return memcmp(h, root, 32) == 0;
 }
 
+/* klauspost builds the encode matrix once in New(); cache it per (k, n) so
+ * the CPU baseline does not rebuild it for every instance. */
+static pthread_mutex_t mat_mu = PTHREAD_MUTEX_INITIALIZER;
+static struct { int k, n; uint8_t *m; } mat_cache[16];
+static const uint8_t *cached_matrix(int k, int n) {
+    pthread_mutex_lock(&mat_mu);
+    for (int i = 0; i < 16; i++)
+        if (mat_cache[i].m && mat_cache[i].k == k && mat_cache[i].n == n) {
+            pthread_mutex_unlock(&mat_mu);
+            return mat_cache[i].m;
+        }
+    int slot = 0;
+    while (slot < 16 && mat_cache[slot].m) slot++;
+    if (slot == 16) { free(mat_cache[0].m); mat_cache[0].m = NULL; slot = 0; }
+    uint8_t *m = (uint8_t *)malloc((size_t)n * k);
+    rbcref_encode_matrix(k, n, m);
+    mat_cache[slot].k = k; mat_cache[slot].n = n; mat_cache[slot].m = m;
+    pthread_mutex_unlock(&mat_mu);
+    return m;
+}
+
 /* ------------------------------------------------------------ RBC path */
 /* shard(enc, data) + Merkle commit: value (B bytes) -> shards [n][pitch],
  * root, branches [n][d][32], leaves [n][32] (optional). */
@@ -357,8 +377,7 @@ int rbcref_encode_commit(int n, int f, const uint8_t *value, size_t B, uint8_t *
     if (B == 0) return -6;
     size_t S = (B + k - 1) / k;
     if (pitch < S) return -10;
-    uint8_t *m = (uint8_t *)malloc((size_t)n * k);
-    rbcref_encode_matrix(k, n, m);
+    const uint8_t *m = cached_matrix(k, n);
     for (int j = 0; j < k; j++) {
         uint8_t *dst = shards + (size_t)j * pitch;
         size_t off = (size_t)j * S;
@@ -375,7 +394,7 @@ int rbcref_encode_commit(int n, int f, const uint8_t *value, size_t B, uint8_t *
     for (int j = 0; j < n; j++) rbcref_sha256(shards + (size_t)j * pitch, S, lv + 32 * j);
     rbcref_merkle_from_leaves(n, lv, root, branches);
     if (!leaves_out) free(lv);
-    free(in); free(out); free(m);
+    free(in); free(out);
     return 0;
 }
 
@@ -393,12 +412,12 @@ int rbcref_interpolate(int n, int f, const uint8_t *shards, size_t pitch, size_t
     }
     if (nu < k) return -3;
     (void)p;
-    uint8_t *m = (uint8_t *)malloc((size_t)n * k), *sub = (uint8_t *)malloc((size_t)k * k),
+    const uint8_t *m = cached_matrix(k, n);
+    uint8_t *sub = (uint8_t *)malloc((size_t)k * k),
             *inv = (uint8_t *)malloc((size_t)k * k), *dm = (uint8_t *)malloc((size_t)(nr ? nr : 1) * k);
-    rbcref_encode_matrix(k, n, m);
     for (int r = 0; r < k; r++) memcpy(sub + r * k, m + (size_t)used[r] * k, k);
     int rc = rbcref_invert(k, sub, inv);
-    if (rc) { free(m); free(sub); free(inv); free(dm); return rc; }
+    if (rc) { free(sub); free(inv); free(dm); return rc; }
     /* D = M[regen] * inv : regenerated shard = D row . used shards */
     for (int r = 0; r < nr; r++)
         for (int c = 0; c < k; c++) {
@@ -423,7 +442,7 @@ int rbcref_interpolate(int n, int f, const uint8_t *shards, size_t pitch, size_t
         if (value_out) memcpy(value_out, full, (size_t)k * S);
         if (digest_out) rbcref_sha256(lv, (size_t)32 * k, digest_out);
     }
-    free(lv); free(full); free(in); free(out); free(m); free(sub); free(inv); free(dm);
+    free(lv); free(full); free(in); free(out); free(sub); free(inv); free(dm);
     return ok ? 0 : -8;
 }
 

@@ -1,0 +1,375 @@
+"""GPU parity tests: librbc_gpu.so on an MI355X vs the CPU oracle.
+
+* golden fixtures (tests/golden/rbc_golden.json) through the single-call
+  drop-ins (shard / validateMessage / interpolate) and the Encoder mirror;
+* seeded batches at BASELINE.json's full shapes (C1..C4 geometry, 1 MiB /
+  4 MiB / 64 KiB values) through the device-resident batch stages, compared
+  with the C restatement (oracle/librbc_ref.so) on sampled instances and with
+  size-independent properties on all of them (encode -> erase -> decode
+  round trip, every valid ECHO verifies, corrupted ECHOs never do, roots
+  recheck);
+* edge cases the reference's domain has: ragged value lengths in one batch,
+  S < 16, S % 64 == 0 and SHA-256 padding boundaries, N = 1, f = 0,
+  non-power-of-two N, too few shards, Byzantine non-codeword commitments.
+All comparisons are bit-exact (integer/byte work)."""
+import numpy as np
+import pytest
+
+import rbc_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def rup(x, a):
+    return (x + a - 1) // a * a
+
+
+# ------------------------------------------------------------------ golden
+
+
+def test_golden_shard_commit(gpu, golden):
+    for c in golden["cases"]:
+        if c["kind"] != "commit" or c.get("byzantine_noncodeword"):
+            continue
+        ctx = gpu.Context(c["n"], c["f"])
+        out = ctx.shard(bytes.fromhex(c["value"]))
+        assert [bytes(s).hex() for s in out["shards"]] == c["shards"], (c["n"], c["f"])
+        assert out["root"].hex() == c["root"]
+        if c["branches"] is not None:
+            assert [b.hex() for b in out["branches"]] == c["branches"]
+
+
+def test_golden_validate_message(gpu, golden):
+    ctxs = {}
+    shards, idx, brs, roots, want = [], [], [], [], []
+    for v in golden["validate"]:
+        key = (v["n"], v["f"])
+        if key not in ctxs:
+            ctxs[key] = gpu.Context(*key)
+        ok = ctxs[key].validate_message(bytes.fromhex(v["root"]), bytes.fromhex(v["branch"]),
+                                        bytes.fromhex(v["shard"]), v["index"])
+        assert ok == v["ok"], v
+        if key == (16, 5):
+            shards.append(bytes.fromhex(v["shard"]))
+            idx.append(v["index"])
+            brs.append(bytes.fromhex(v["branch"]))
+            roots.append(bytes.fromhex(v["root"]))
+            want.append(v["ok"])
+    got = ctxs[(16, 5)].validate_batch(shards, idx, brs, roots)
+    assert got.tolist() == want
+
+
+def _interp_groups(golden):
+    last = None
+    for c in golden["cases"]:
+        if c["kind"] == "commit":
+            last = c
+        else:
+            yield last, c
+
+
+def test_golden_interpolate(gpu, golden):
+    ctxs = {}
+    for com, case in _interp_groups(golden):
+        key = (case["n"], case["f"])
+        if key not in ctxs:
+            ctxs[key] = gpu.Context(*key)
+        n = case["n"]
+        shards = [bytes.fromhex(s) for s in com["shards"]]
+        given = [None] * n
+        for j in case["present"]:
+            s = bytearray(shards[j])
+            if str(j) in case["tamper"]:
+                s[0] ^= case["tamper"][str(j)]
+            given[j] = bytes(s)
+        try:
+            out = ctxs[key].interpolate(bytes.fromhex(case["root"]), given)
+            status = 0
+        except gpu.RBCError as e:
+            status = e.code
+        assert status == case["status"], (case["name"], key)
+        if status == 0:
+            assert out["value"].hex() == case["value"], (case["name"], key)
+            assert out["digest"].hex() == case["digest"], (case["name"], key)
+
+
+# ------------------------------------------------------- Encoder mirror
+
+
+def test_encoder_mirror_matches_klauspost_semantics(gpu):
+    # TestOneEncode known answer through the GPU encoder
+    e = gpu.Encoder(5, 5)
+    sh = [np.array(x, np.uint8) for x in ([0, 1], [4, 5], [2, 3], [6, 7], [8, 9])] + [np.zeros(2, np.uint8)] * 5
+    e.encode(sh)
+    assert [list(map(int, s)) for s in sh[5:]] == [[12, 13], [10, 11], [14, 15], [90, 91], [94, 95]]
+    assert e.verify(sh)
+    bad = [s.copy() for s in sh]
+    bad[9][1] ^= 4
+    assert not e.verify(bad)
+    rng = np.random.default_rng(3)
+    for k, p, S in [(10, 4, 1000), (22, 42, 4097), (44, 84, 333), (86, 170, 63), (3, 0, 17), (1, 5, 129)]:
+        enc = gpu.Encoder(k, p)
+        ref = orc.Encoder(k, p)
+        data = rng.integers(0, 256, k * S, dtype=np.uint8)
+        shards = enc.split(data)
+        want = ref.split(data)
+        assert all(np.array_equal(a, b) for a, b in zip(shards, want))
+        enc.encode(shards)
+        ref.encode(want)
+        assert all(np.array_equal(a, b) for a, b in zip(shards, want))
+        if p == 0:
+            continue
+        # erase data and parity; Reconstruct restores exactly, present untouched
+        keep = set(rng.permutation(k + p)[:k].tolist())
+        part = [s.copy() if j in keep else None for j, s in enumerate(shards)]
+        enc.reconstruct(part)
+        assert all(np.array_equal(a, b) for a, b in zip(part, want))
+        part = [s.copy() if j in keep else None for j, s in enumerate(shards)]
+        enc.reconstruct_data(part)
+        for j in range(k + p):
+            if j < k:
+                assert np.array_equal(part[j], want[j])
+            elif j not in keep:
+                assert part[j] is None
+        assert enc.join(part, k * S - 5) == data.tobytes()[: k * S - 5]
+    e = gpu.Encoder(4, 2)
+    with pytest.raises(gpu.RBCError) as ei:
+        e.reconstruct([np.zeros(3, np.uint8), None, None, None, np.zeros(3, np.uint8), None])
+    assert ei.value.code == -3
+    with pytest.raises(gpu.RBCError) as ei:
+        e.encode([np.zeros(3, np.uint8)] * 5 + [np.zeros(2, np.uint8)])
+    assert ei.value.code == -5
+    with pytest.raises(gpu.RBCError) as ei:
+        e.split(b"")
+    assert ei.value.code == -6
+    with pytest.raises(gpu.RBCError) as ei:
+        e.join([np.zeros(3, np.uint8), None, np.zeros(3, np.uint8), np.zeros(3, np.uint8)], 9)
+    assert ei.value.code == -7
+
+
+# ---------------------------------------------------- host batch API
+
+
+def test_host_batch_ragged_lengths(gpu, ref):
+    n, f = 64, 21
+    ctx = gpu.Context(n, f)
+    rng = np.random.default_rng(9)
+    lens = [1, 21, 22, 23, 1000, 4096 * 3 + 5, 47663 * 22, 64 * 22, 64 * 22 + 1, 55 * 22]
+    values = [rng.integers(0, 256, L, dtype=np.uint8) for L in lens]
+    out = ctx.shard_commit_batch(values)
+    for i, v in enumerate(values):
+        shards, root, br, leaves = ref.encode_commit(n, f, v)
+        S = shards.shape[1]
+        assert out["shard_lens"][i] == S
+        assert np.array_equal(out["shards"][i, :, :S], shards), i
+        assert bytes(out["roots"][i]) == root, i
+        assert np.array_equal(out["branches"][i], br), i
+    # interpolate the batch back, dropping a random N-k+... subset per instance
+    count = len(values)
+    Smax = out["shards"].shape[2]
+    present = np.zeros((count, n), np.uint8)
+    for i in range(count):
+        present[i, rng.permutation(n)[: n - 2 * f]] = 1
+    res = ctx.interpolate_batch(out["shards"] * present[:, :, None], out["shard_lens"], present, out["roots"])
+    assert (res["status"] == 0).all()
+    for i, v in enumerate(values):
+        S = int(out["shard_lens"][i])
+        assert res["values"][i, : len(v)].tobytes() == v.tobytes()
+        assert not res["values"][i, len(v): ctx.k * S].any()
+
+
+# -------------------------------------------- device pipeline at full size
+
+
+class Pipeline:
+    """Device buffers + the bench's step for `I` instances of (n, f, B)."""
+
+    def __init__(self, gpu, n, f, B, I, seed, corrupt_frac=0.1, present_n=None):
+        self.ca = gpu
+        self.ctx = gpu.Context(n, f)
+        self.n, self.f, self.B, self.I = n, f, B, I
+        k = self.ctx.k
+        self.k = k
+        self.S = S = (B + k - 1) // k
+        self.d = self.ctx.depth
+        self.spitch = rup(S, 64)
+        self.vpitch = rup(k * S + 32, 64)
+        self.opitch = rup(k * S, 16)
+        rng = np.random.default_rng(seed)
+        self.values = rng.integers(0, 256, size=(I, self.vpitch), dtype=np.uint8)
+        self.present = np.zeros((I, n), np.uint8)
+        self.corrupt = np.full(I, -1, np.int32)
+        pn = n - f if present_n is None else present_n
+        for i in range(I):
+            pres = rng.permutation(n)[:pn]
+            self.present[i, pres] = 1
+            if rng.random() < corrupt_frac:
+                self.corrupt[i] = int(rng.choice(pres))
+        mb = gpu.DeviceBuffer
+        self.b = dict(values=mb(I * self.vpitch), shards=mb(I * n * self.spitch), leaves=mb(I * n * 32),
+                      roots=mb(I * 32), branches=mb(I * n * max(self.d, 1) * 32), present=mb(I * n),
+                      corrupt=mb(I * 4), valid=mb(I * n), leaves_r=mb(I * n * 32), out=mb(I * self.opitch),
+                      digests=mb(I * 32), status=mb(I * 4))
+        self.b["values"].upload(self.values)
+        self.b["present"].upload(self.present)
+        self.b["corrupt"].upload(self.corrupt)
+
+    def commit(self):
+        b, c = self.b, self.ctx
+        c.dev_encode(None, self.I, b["values"], self.vpitch, None, self.B, b["shards"], self.spitch)
+        c.dev_leaves(None, self.I, b["shards"], self.spitch, None, self.S, b["leaves"])
+        c.dev_merkle_build(None, self.I, b["leaves"], b["roots"], b["branches"])
+
+    def receive(self):
+        b, c = self.b, self.ctx
+        c.dev_inject_faults(None, self.I, b["shards"], self.spitch, b["corrupt"])
+        c.dev_verify(None, self.I, b["shards"], self.spitch, None, self.S, b["branches"], b["roots"],
+                     b["present"], b["valid"], b["leaves_r"])
+        c.dev_interpolate(None, self.I, b["shards"], self.spitch, None, self.S, b["valid"], b["leaves_r"], 1,
+                          b["roots"], b["out"], self.opitch, b["digests"], b["status"])
+
+    def shards(self):
+        return self.b["shards"].download().reshape(self.I, self.n, self.spitch)
+
+    def arr(self, name, dtype=np.uint8, shape=None):
+        a = np.frombuffer(self.b[name].download().tobytes(), dtype=dtype)
+        return a.reshape(shape) if shape else a
+
+
+FULL = [
+    ("c1", 64, 21, 1 << 20, 6),
+    ("c2", 128, 42, 1 << 20, 6),
+    ("c3", 128, 42, 4 << 20, 2),
+    ("c4", 256, 85, 64 << 10, 24),
+]
+
+
+@pytest.mark.parametrize("name,n,f,B,I", FULL, ids=[x[0] for x in FULL])
+def test_device_pipeline_full_size_vs_c_oracle(gpu, ref, name, n, f, B, I):
+    pl = Pipeline(gpu, n, f, B, I, seed=hash(name) & 0xffff)
+    pl.commit()
+    sh = pl.shards()
+    roots = pl.arr("roots", shape=(I, 32))
+    brs = pl.arr("branches", shape=(I, n, max(pl.d, 1), 32))
+    leaves = pl.arr("leaves", shape=(I, n, 32))
+    S = pl.S
+    for i in range(I):
+        want_sh, want_root, want_br, want_leaves = ref.encode_commit(n, f, pl.values[i, :B])
+        assert np.array_equal(sh[i, :, :S], want_sh), (name, i)
+        assert not sh[i, :, S:].any(), "pad bytes past S must be zero"
+        assert bytes(roots[i]) == want_root
+        assert np.array_equal(brs[i], want_br)
+        assert np.array_equal(leaves[i], want_leaves)
+    pl.receive()
+    valid = pl.arr("valid", shape=(I, n))
+    status = pl.arr("status", np.int32)
+    out = pl.arr("out", shape=(I, pl.opitch))
+    digests = pl.arr("digests", shape=(I, 32))
+    for i in range(I):
+        exp_valid = pl.present[i].copy()
+        if pl.corrupt[i] >= 0:
+            exp_valid[pl.corrupt[i]] = 0
+        assert np.array_equal(valid[i], exp_valid), (name, i)
+        # C oracle interpolate from the received (corrupted) shards
+        rx = sh[i, :, :S].copy()
+        if pl.corrupt[i] >= 0:
+            rx[pl.corrupt[i], 0] ^= 0x5A
+        rc, value, dig = ref.interpolate(n, f, rx, exp_valid, bytes(roots[i]))
+        assert status[i] == rc == 0, (name, i)
+        assert np.array_equal(out[i, : pl.k * S], value)
+        assert bytes(digests[i]) == dig
+        # round-trip property: the decoded value is the proposer's input
+        assert out[i, :B].tobytes() == pl.values[i, :B].tobytes()
+        assert not out[i, B: pl.k * S].any()
+
+
+def test_device_pipeline_many_instances_properties(gpu, ref):
+    """Bench-shaped batch (N=128 f=42, 1 MiB, 256 instances): every
+    instance round-trips; 16 sampled instances bit-exact vs the C port."""
+    n, f, B, I = 128, 42, 1 << 20, 256
+    pl = Pipeline(gpu, n, f, B, I, seed=77)
+    pl.commit()
+    roots = pl.arr("roots", shape=(I, 32))
+    sample = np.random.default_rng(0).permutation(I)[:16]
+    sh = pl.shards()
+    for i in sample:
+        _, want_root, _, _ = ref.encode_commit(n, f, pl.values[i, :B])
+        assert bytes(roots[i]) == want_root
+    del sh
+    pl.receive()
+    status = pl.arr("status", np.int32)
+    assert (status == 0).all()
+    out = pl.arr("out", shape=(I, pl.opitch))
+    assert np.array_equal(out[:, :B], pl.values[:, :B])
+    # a second round over the regenerated codeword is idempotent
+    pl.corrupt[:] = -1
+    pl.b["corrupt"].upload(pl.corrupt)
+    pl.commit()
+    roots2 = pl.arr("roots", shape=(I, 32))
+    assert np.array_equal(roots, roots2)
+
+
+def test_device_too_few_and_root_mismatch(gpu):
+    """present = k-1 -> TOO_FEW_SHARDS; wrong expected root -> ROOT_MISMATCH;
+    a corrupted used shard that passes verify (present mask forged) ->
+    ROOT_MISMATCH, never a wrong value."""
+    n, f, B, I = 16, 5, 5000, 6
+    pl = Pipeline(gpu, n, f, B, I, seed=5, corrupt_frac=0.0, present_n=n - 2 * f - 1)
+    pl.commit()
+    pl.receive()
+    assert (pl.arr("status", np.int32) == -3).all()
+    pl = Pipeline(gpu, n, f, B, I, seed=6, corrupt_frac=0.0)
+    pl.commit()
+    roots = pl.arr("roots", shape=(I, 32)).copy()
+    bad = roots.copy()
+    bad[::2, 0] ^= 1
+    pl.b["roots"].upload(bad)
+    c, b = pl.ctx, pl.b
+    c.dev_verify(None, I, b["shards"], pl.spitch, None, pl.S, b["branches"], b["roots"], b["present"], b["valid"],
+                 b["leaves_r"])
+    assert not pl.arr("valid", shape=(I, n))[::2].any()
+    # forge: mark all present as valid against the wrong root, decode
+    b["valid"].upload(pl.present)
+    c.dev_interpolate(None, I, b["shards"], pl.spitch, None, pl.S, b["valid"], b["leaves"], 0, b["roots"],
+                      b["out"], pl.opitch, b["digests"], b["status"])
+    st = pl.arr("status", np.int32)
+    assert (st[::2] == -8).all() and (st[1::2] == 0).all()
+
+
+@pytest.mark.parametrize("n,f,B", [
+    (4, 1, 1024), (4, 1, 1), (5, 0, 77), (1, 0, 10), (7, 2, 333), (13, 4, 5 * 64), (13, 4, 5 * 55),
+    (13, 4, 5 * 56), (13, 4, 5 * 63), (64, 21, 22 * 16), (64, 21, 22 * 15), (256, 85, 86 * 4096 + 3),
+])
+def test_device_pipeline_edge_geometries(gpu, ref, n, f, B):
+    I = 5
+    pl = Pipeline(gpu, n, f, B, I, seed=n * 1000 + B, corrupt_frac=0.5)
+    pl.commit()
+    sh = pl.shards()
+    roots = pl.arr("roots", shape=(I, 32))
+    for i in range(I):
+        want_sh, want_root, _, _ = ref.encode_commit(n, f, pl.values[i, :B])
+        assert np.array_equal(sh[i, :, : pl.S], want_sh)
+        assert bytes(roots[i]) == want_root
+    pl.receive()
+    status = pl.arr("status", np.int32)
+    out = pl.arr("out", shape=(I, pl.opitch))
+    valid = pl.arr("valid", shape=(I, n))
+    for i in range(I):
+        ok = valid[i].sum() >= pl.k
+        assert status[i] == (0 if ok else -3)
+        if ok:
+            assert out[i, :B].tobytes() == pl.values[i, :B].tobytes()
+
+
+def test_byzantine_noncodeword_rejected_by_every_subset(gpu, golden):
+    com = [c for c in golden["cases"] if c.get("byzantine_noncodeword")][0]
+    n, f = com["n"], com["f"]
+    ctx = gpu.Context(n, f)
+    shards = [bytes.fromhex(s) for s in com["shards"]]
+    root = bytes.fromhex(com["root"])
+    rng = np.random.default_rng(0)
+    for _ in range(8):
+        keep = set(rng.permutation(n)[: n - 2 * f].tolist())
+        with pytest.raises(gpu.RBCError) as ei:
+            ctx.interpolate(root, [s if j in keep else None for j, s in enumerate(shards)])
+        assert ei.value.code == -8

@@ -1,0 +1,278 @@
+"""Oracle tests (CPU).  Pins the restatement of klauspost/reedsolomon v1.9.1
+to klauspost's own unit-test vectors, SHA-256 to FIPS 180-4, and checks the
+C restatement (oracle/librbc_ref.so) against the Python one and against the
+committed golden fixtures."""
+import hashlib
+
+import numpy as np
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+import rbc_oracle as orc
+
+# ---- klauspost/reedsolomon known answers (galois_test.go, matrix_test.go,
+#      reedsolomon_test.go TestOneEncode; Backblaze JavaReedSolomon shares them)
+
+
+def test_galois_known_answers():
+    assert orc.gal_mul(3, 4) == 12
+    assert orc.gal_mul(7, 7) == 21
+    assert orc.gal_mul(23, 45) == 41
+    assert orc.gal_exp(2, 2) == 4
+    assert orc.gal_exp(5, 20) == 235
+    assert orc.gal_exp(13, 7) == 43
+    assert orc.gal_div(6, 3) == 2
+    assert orc.gal_exp(0, 0) == 1 and orc.gal_exp(0, 5) == 0
+
+
+def test_matrix_known_answers():
+    m = np.array([[1, 2], [3, 4]], dtype=np.uint8)
+    n = np.array([[5, 6], [7, 8]], dtype=np.uint8)
+    assert orc.mat_mul(m, n).tolist() == [[11, 22], [19, 42]]
+    inv = orc.mat_invert(np.array([[56, 23, 98], [3, 100, 200], [45, 201, 123]], dtype=np.uint8))
+    assert inv.tolist() == [[175, 133, 33], [130, 13, 245], [112, 35, 126]]
+    inv2 = orc.mat_invert(np.array([[1, 0, 0, 0, 0], [0, 1, 0, 0, 0], [0, 0, 0, 1, 0], [0, 0, 0, 0, 1],
+                                    [7, 7, 6, 6, 1]], dtype=np.uint8))
+    assert inv2.tolist() == [[1, 0, 0, 0, 0], [0, 1, 0, 0, 0], [123, 123, 1, 122, 122], [0, 0, 1, 0, 0],
+                             [0, 0, 0, 1, 0]]
+    with pytest.raises(orc.ErrSingular):
+        orc.mat_invert(np.array([[4, 2], [12, 6]], dtype=np.uint8))
+
+
+def test_one_encode_known_answer():
+    """klauspost reedsolomon_test.go TestOneEncode (5 data + 5 parity)."""
+    e = orc.Encoder(5, 5)
+    sh = [np.array(x, dtype=np.uint8) for x in ([0, 1], [4, 5], [2, 3], [6, 7], [8, 9])]
+    sh += [np.zeros(2, dtype=np.uint8) for _ in range(5)]
+    e.encode(sh)
+    assert [list(map(int, s)) for s in sh[5:]] == [[12, 13], [10, 11], [14, 15], [90, 91], [94, 95]]
+    assert e.verify(sh)
+    sh[7][0] ^= 1
+    assert not e.verify(sh)
+
+
+def test_encode_matrix_is_systematic_and_mds():
+    m = orc.encode_matrix(4, 6)
+    assert m[:4].tolist() == np.eye(4, dtype=np.uint8).tolist()
+    assert m[4:].tolist() == [[27, 28, 18, 20], [28, 27, 20, 18]]
+    rng = np.random.default_rng(1)
+    m = orc.encode_matrix(10, 16)
+    for _ in range(20):
+        rows = sorted(rng.permutation(16)[:10])
+        orc.mat_invert(m[rows])  # any k rows invertible
+
+
+# ---- SHA-256 (FIPS 180-4 known answers; Go crypto/sha256 == hashlib)
+
+
+FIPS = [
+    (b"", "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"),
+    (b"abc", "ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad"),
+    (b"abcdbcdecdefdefgefghfghighijhijkijkljklmklmnlmnomnopnopq",
+     "248d6a61d20638b8e5c026930c3e6039a33ce45964ff2167f6ecedd419db06c1"),
+]
+
+
+def test_sha256_fips_vectors(ref):
+    for msg, want in FIPS[:3]:
+        assert orc.sha256(msg).hex() == want
+        assert ref.sha256(msg).hex() == want
+    big = b"a" * 1000000
+    assert ref.sha256(big) == hashlib.sha256(big).digest()
+
+
+@pytest.mark.parametrize("scalar", [0, 1])
+def test_c_sha256_matches_hashlib_all_tail_lengths(ref, scalar):
+    lib = ref.lib()
+    lib.rbcref_force_scalar(scalar)
+    try:
+        rng = np.random.default_rng(5)
+        for n in list(range(0, 200)) + [1023, 1024, 4095, 23832, 47663, 95326, 763]:
+            b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+            assert ref.sha256(b) == hashlib.sha256(b).digest(), n
+    finally:
+        lib.rbcref_force_scalar(0)
+
+
+# ---- C restatement vs Python restatement
+
+
+@pytest.mark.parametrize("k,n", [(2, 4), (5, 10), (22, 64), (44, 128), (86, 256), (1, 1), (17, 17)])
+def test_c_encode_matrix_matches_python(ref, k, n):
+    assert ref.encode_matrix(k, n).tolist() == orc.encode_matrix(k, n).tolist()
+
+
+@pytest.mark.parametrize("scalar", [0, 1])
+def test_c_encode_commit_matches_python(ref, scalar):
+    ref.lib().rbcref_force_scalar(scalar)
+    try:
+        rng = np.random.default_rng(11)
+        for n, f, B in [(4, 1, 1024), (7, 2, 333), (16, 5, 1001), (64, 21, 5000), (128, 42, 9000), (256, 85, 700)]:
+            value = rng.integers(0, 256, B, dtype=np.uint8)
+            shards, root, br, leaves = ref.encode_commit(n, f, value)
+            enc = orc.Encoder(n - 2 * f, 2 * f)
+            want = orc.rbc_shard(enc, value)
+            com = orc.rbc_commit(want)
+            assert all(np.array_equal(shards[j], want[j]) for j in range(n))
+            assert root == com["root"]
+            for j in range(n):
+                assert [bytes(x) for x in br[j]] == [b if b else b"\0" * 32 for b in com["branches"][j]]
+    finally:
+        ref.lib().rbcref_force_scalar(0)
+
+
+# ---- golden fixtures: the oracle reproduces them, the C port agrees
+
+
+def _commit_cases(golden):
+    return [c for c in golden["cases"] if c["kind"] == "commit"]
+
+
+def test_golden_commit_reproduced_by_python_oracle(golden):
+    for c in _commit_cases(golden):
+        n, f = c["n"], c["f"]
+        enc = orc.Encoder(n - 2 * f, 2 * f)
+        value = bytes.fromhex(c["value"])
+        shards = orc.rbc_shard(enc, value)
+        if c.get("byzantine_noncodeword"):
+            shards = [np.frombuffer(bytes.fromhex(s), dtype=np.uint8) for s in c["shards"]]
+        else:
+            assert [bytes(s).hex() for s in shards] == c["shards"]
+        com = orc.rbc_commit(shards)
+        assert com["root"].hex() == c["root"]
+        assert [x.hex() for x in com["leaves"]] == c["leaves"]
+        if c["branches"] is not None:
+            assert [orc.flat_branch(b).hex() for b in com["branches"]] == c["branches"]
+
+
+def test_golden_commit_matches_c_port(golden, ref):
+    for c in _commit_cases(golden):
+        if c.get("byzantine_noncodeword"):
+            continue
+        n, f = c["n"], c["f"]
+        shards, root, br, leaves = ref.encode_commit(n, f, np.frombuffer(bytes.fromhex(c["value"]), np.uint8))
+        assert [bytes(s).hex() for s in shards] == c["shards"]
+        assert root.hex() == c["root"]
+        assert [bytes(x).hex() for x in leaves] == c["leaves"]
+
+
+def _interp_groups(golden):
+    """Pair each interpolate case with the commit case generated just before it."""
+    out = []
+    last = None
+    for c in golden["cases"]:
+        if c["kind"] == "commit":
+            last = c
+        else:
+            out.append((last, c))
+    return out
+
+
+def test_golden_interpolate_reproduced_by_python_and_c(golden, ref):
+    for com, case in _interp_groups(golden):
+        n, f = case["n"], case["f"]
+        k = n - 2 * f
+        enc = orc.Encoder(k, 2 * f)
+        shards = [np.frombuffer(bytes.fromhex(s), dtype=np.uint8).copy() for s in com["shards"]]
+        given_ = [None] * n
+        for j in case["present"]:
+            s = shards[j].copy()
+            if str(j) in case["tamper"]:
+                s[0] ^= case["tamper"][str(j)]
+            given_[j] = s
+        root = bytes.fromhex(case["root"])
+        try:
+            r = orc.rbc_interpolate(enc, root, given_)
+            st_py = 0
+        except orc.RSError as e:
+            st_py = e.code
+            r = None
+        assert st_py == case["status"], case["name"]
+        if st_py == 0:
+            assert r["value"].hex() == case["value"] and r["digest"].hex() == case["digest"]
+        # C port (ErrTooFewShards is decided before any GF work in both)
+        S = len(shards[0])
+        arr = np.zeros((n, S), dtype=np.uint8)
+        valid = np.zeros(n, dtype=np.uint8)
+        for j in range(n):
+            if given_[j] is not None:
+                arr[j] = given_[j]
+                valid[j] = 1
+        rc, value, dig = ref.interpolate(n, f, arr, valid, root)
+        assert rc == case["status"], case["name"]
+        if rc == 0:
+            assert bytes(value).hex() == case["value"] and dig.hex() == case["digest"]
+
+
+def test_golden_validate_vectors(golden, ref):
+    for v in golden["validate"]:
+        n = v["n"]
+        br = orc.unflatten_branch(bytes.fromhex(v["branch"]), v["index"], n)
+        ok = br is not None and orc.merkle_verify(n, bytes.fromhex(v["shard"]), bytes.fromhex(v["root"]), br,
+                                                   v["index"])
+        assert ok == v["ok"]
+        if br is not None:
+            d = orc.tree_depth(n)
+            slots = np.zeros((max(d, 1), 32), dtype=np.uint8)
+            for lvl, b in enumerate(br):
+                if b:
+                    slots[lvl] = np.frombuffer(b, np.uint8)
+            got = ref.verify(n, np.frombuffer(bytes.fromhex(v["shard"]), np.uint8), v["index"], slots,
+                             bytes.fromhex(v["root"]))
+            assert got == v["ok"]
+
+
+# ---- Encoder API semantics (klauspost v1.9.1 error values)
+
+
+def test_encoder_errors():
+    with pytest.raises(orc.ErrInvShardNum):
+        orc.Encoder(0, 1)
+    with pytest.raises(orc.ErrInvShardNum):
+        orc.Encoder(1, -1)
+    with pytest.raises(orc.ErrMaxShardNum):
+        orc.Encoder(200, 57)
+    e = orc.Encoder(3, 2)
+    with pytest.raises(orc.ErrShortData):
+        e.split(b"")
+    sh = e.split(b"hello world")
+    assert len(sh) == 5 and all(len(s) == 4 for s in sh)
+    with pytest.raises(orc.ErrTooFewShards):
+        e.encode(sh[:4])
+    with pytest.raises(orc.ErrShardNoData):
+        e.encode([np.zeros(0, np.uint8)] * 5)
+    bad = [s.copy() for s in sh]
+    bad[1] = bad[1][:3]
+    with pytest.raises(orc.ErrShardSize):
+        e.encode(bad)
+    e.encode(sh)
+    miss = [sh[0], None, None, None, sh[4]]
+    with pytest.raises(orc.ErrTooFewShards):
+        e.reconstruct(miss)
+    with pytest.raises(orc.ErrReconstructRequired):
+        e.join([sh[0], None, sh[2]], 11)
+    with pytest.raises(orc.ErrShortData):
+        e.join(sh, 100)
+    assert e.join(sh, 11) == b"hello world"
+
+
+@settings(max_examples=40, deadline=None)
+@given(n=st.integers(2, 40), fr=st.floats(0, 0.49), B=st.integers(1, 600), seed=st.integers(0, 2**32 - 1))
+def test_reconstruct_roundtrip_property(n, fr, B, seed):
+    f = int(fr * n) // 2
+    k = n - 2 * f
+    if k < 1:
+        return
+    rng = np.random.default_rng(seed)
+    e = orc.Encoder(k, n - k)
+    value = rng.integers(0, 256, B, dtype=np.uint8)
+    sh = orc.rbc_shard(e, value)
+    keep = set(rng.permutation(n)[:k].tolist())
+    part = [sh[j] if j in keep else None for j in range(n)]
+    e.reconstruct(part)
+    assert all(np.array_equal(part[j], sh[j]) for j in range(n))
+    com = orc.rbc_commit(sh)
+    part = [sh[j] if j in keep else None for j in range(n)]
+    out = orc.rbc_interpolate(e, com["root"], part)
+    assert out["value"][:B] == value.tobytes()
