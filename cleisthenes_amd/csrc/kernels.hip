@@ -71,8 +71,17 @@ __global__ __launch_bounds__(256) void gf_rows_kernel(GfArgs a) {
     uint8_t *s_in = reinterpret_cast<uint8_t *>(smem + (size_t)20 * RC * KP);
     uint8_t *s_out = s_in + 256;
 
-    const int inst = blockIdx.x / a.tiles;
-    const int tile = blockIdx.x - inst * a.tiles;
+    // block -> (work item = instance x column tile, row chunk c).  The chunks
+    // of one item are 8 block ids apart, i.e. dispatched to the same XCD under
+    // round-robin placement, so the item's input rows are re-read from that
+    // XCD's L2 (speed only; any placement is correct).
+    const int chunks = a.R > 0 ? (a.R + RC - 1) / RC : 1;  // R == 0: Split copy only
+    const int grp = blockIdx.x / (8 * chunks), rem = blockIdx.x - grp * 8 * chunks;
+    const int c = rem >> 3;
+    const int item = grp * 8 + (rem & 7);
+    if (item >= a.count * a.tiles) return;
+    const int inst = item / a.tiles;
+    const int tile = item - inst * a.tiles;
     const int tid = threadIdx.x;
     if (a.status && a.status[inst] != 0) return;
 
@@ -118,13 +127,10 @@ __global__ __launch_bounds__(256) void gf_rows_kernel(GfArgs a) {
         }
     };
 
-    // R == 0 (no parity, f = 0) still runs one chunk so Split's copy happens
-    const int chunks = a.R > 0 ? (a.R + RC - 1) / RC : 1;
     const int cmp_from = a.nmiss ? a.nmiss[inst] : 0x7fffffff;
-    for (int c = 0; c < chunks; ++c) {
+    {
         const int r0 = c * RC;
         const int rows = min(RC, a.R - r0);
-        __syncthreads();  // previous chunk's tables no longer read; idx lists visible
         for (int e = tid; e < RC * KP; e += 256) {
             const int r = e / KP, j = e - r * KP;
             uint32_t cf = 0;
@@ -567,7 +573,9 @@ template <int RC>
 static hipError_t launch_gf_rc(const GfArgs &a, hipStream_t st) {
     const int KP = (a.K + 1) & ~1;
     const size_t lds = (size_t)20 * RC * KP + 512;
-    dim3 grid((unsigned)a.count * a.tiles);
+    const int chunks = a.R > 0 ? (a.R + RC - 1) / RC : 1;
+    const long items = (long)a.count * a.tiles;
+    dim3 grid((unsigned)(((items + 7) / 8) * 8 * chunks));
     hipLaunchKernelGGL(gf_rows_kernel<RC>, grid, dim3(256), lds, st, a);
     return hipGetLastError();
 }

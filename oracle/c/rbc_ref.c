@@ -451,9 +451,9 @@ int rbcref_interpolate(int n, int f, const uint8_t *shards, size_t pitch, size_t
  * encode+commit -> (corrupt) -> verify all N echoes -> interpolate from the
  * first k valid of a present subset -> value + digest. */
 typedef struct {
-    int n, f, first, count;
+    int n, f, first, count, nvals;
     size_t B;
-    const uint8_t *values;      /* count x B (instance first..) */
+    const uint8_t *values;      /* nvals x B; instance i uses value i % nvals */
     const uint8_t *present;     /* count x n */
     const int32_t *corrupt;     /* count: shard index to corrupt or -1 */
     int status_sum;
@@ -468,7 +468,8 @@ static void *pipeline_worker(void *arg) {
     uint8_t *value = (uint8_t *)malloc((size_t)k * S);
     uint8_t root[32], dig[32], valid[256];
     for (int i = 0; i < jb->count; i++) {
-        rbcref_encode_commit(n, f, jb->values + (size_t)i * jb->B, jb->B, shards, pitch, root, br, NULL);
+        const int vi = (jb->first + i) % jb->nvals;
+        rbcref_encode_commit(n, f, jb->values + (size_t)vi * jb->B, jb->B, shards, pitch, root, br, NULL);
         int cj = jb->corrupt[i];
         if (cj >= 0) shards[(size_t)cj * pitch] ^= 0x5a;
         for (int j = 0; j < n; j++)
@@ -483,7 +484,7 @@ static void *pipeline_worker(void *arg) {
 }
 
 /* Returns wall seconds for `count` instances split over `threads`. */
-double rbcref_pipeline(int n, int f, int count, size_t B, int threads, const uint8_t *values,
+double rbcref_pipeline(int n, int f, int count, size_t B, int threads, const uint8_t *values, int nvals,
                        const uint8_t *present, const int32_t *corrupt, int *status_sum) {
     gf_init();
     cpu_detect();
@@ -496,8 +497,7 @@ double rbcref_pipeline(int n, int f, int count, size_t B, int threads, const uin
     int per = count / threads, extra = count % threads, first = 0;
     for (int t = 0; t < threads; t++) {
         int c = per + (t < extra);
-        jobs[t] = (job_t){n, f, first, c, B, values + (size_t)first * B, present + (size_t)first * n,
-                          corrupt + first, 0};
+        jobs[t] = (job_t){n, f, first, c, nvals, B, values, present + (size_t)first * n, corrupt + first, 0};
         pthread_create(&th[t], NULL, pipeline_worker, &jobs[t]);
         first += c;
     }

@@ -31,7 +31,7 @@ def load():
                                          c_void_p]
     lib.rbcref_interpolate.argtypes = [c_int, c_int, c_void_p, c_size_t, c_size_t, c_void_p, c_void_p, c_void_p,
                                        c_void_p]
-    lib.rbcref_pipeline.argtypes = [c_int, c_int, c_int, c_size_t, c_int, c_void_p, c_void_p, c_void_p,
+    lib.rbcref_pipeline.argtypes = [c_int, c_int, c_int, c_size_t, c_int, c_void_p, c_int, c_void_p, c_void_p,
                                     POINTER(c_int)]
     lib.rbcref_pipeline.restype = c_double
     lib.rbcref_tree_depth.argtypes = [c_int]
@@ -106,6 +106,9 @@ def interpolate(n: int, f: int, shards: np.ndarray, valid: np.ndarray, root: byt
 
 
 def pipeline(n, f, count, B, threads, values, present, corrupt):
+    """values: [nvals][B]; instance i encodes values[i % nvals]."""
     st = c_int(0)
-    secs = lib().rbcref_pipeline(n, f, count, B, threads, p(values), p(present), p(corrupt), ctypes.byref(st))
+    values = np.ascontiguousarray(values, dtype=np.uint8)
+    secs = lib().rbcref_pipeline(n, f, count, B, threads, p(values), values.shape[0], p(present), p(corrupt),
+                                 ctypes.byref(st))
     return secs, st.value
