@@ -40,7 +40,9 @@ CONFIGS = {
     "c4": (256, 85, 64 << 10, 16384, "N=256 f=85 64KiB x16384"),
 }
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
-VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9  # 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz
+# integer VOP3 (alignbit/bitop3/perm/add3): one wave64 instruction per 4 clk per SIMD
+# (16 lanes/clk), measured (profiles/r01_pmc_summary.json); 1024 SIMDs at 2.4 GHz
+VALU_ISSUE_PEAK = 1024 * 2.4e9 / 4      # wave-instructions/s
 
 
 def round_up(x, a):
@@ -57,13 +59,18 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-instances", type=int, default=2048)
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--streams", type=int, default=1,
+                    help="split the batch over S HIP streams (one context each) so stages of different "
+                         "instance groups overlap")
+    ap.add_argument("--force-gather", action="store_true",
+                    help="run the RCCL all-gather even with one rank (exercises rbc_comm_*)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    if world > 1 or "RANK" in os.environ:  # launched by torch.distributed.run
         import torch.distributed as dist  # host-side coordination only (gloo, CPU tensors)
         dist.init_process_group("gloo")
 
@@ -109,9 +116,12 @@ def main():
     d_out = mb(I * opitch)
     d_digests = mb(I * 32)
     d_status = mb(I * 4)
-    d_gather = mb(world * I * 64) if world > 1 else None
+    gather = world > 1 or args.force_gather
+    d_gather = mb(world * I * 64) if gather else None
 
-    if world > 1:
+    if dist is None and gather:
+        ctx.comm_init(1, 0, ca.Context.comm_unique_id())
+    if dist is not None and gather:
         import torch
         uid = torch.zeros(128, dtype=torch.uint8)
         if rank == 0:
@@ -119,39 +129,55 @@ def main():
         dist.broadcast(uid, 0)
         ctx.comm_init(world, rank, bytes(uid.numpy().tobytes()))
 
-    stream = ca.Stream(dev)
+    nstreams = max(1, min(args.streams, I))
+    streams = [ca.Stream(dev) for _ in range(nstreams)]
+    ctxs = [ctx] + [ca.Context(n, f, device=dev) for _ in range(nstreams - 1)]  # own decode workspace each
+    bounds = [(g * I // nstreams, (g + 1) * I // nstreams) for g in range(nstreams)]
+    stream = streams[0]
     ev = {name: ca.Event() for name in ("t0", "enc", "leaf", "tree", "fault", "verify", "interp", "gather")}
 
+    def at(buf, i0, per):
+        return buf.value + i0 * per
+
     def step(timed):
-        if timed:
-            ev["t0"].record(stream)
-        ctx.dev_encode(stream.ptr, I, d_values, vpitch, None, B, d_shards, spitch)
-        if timed:
-            ev["enc"].record(stream)
-        ctx.dev_leaves(stream.ptr, I, d_shards, spitch, None, S, d_leaves_p)
-        if timed:
-            ev["leaf"].record(stream)
-        ctx.dev_merkle_build(stream.ptr, I, d_leaves_p, d_roots, d_branches)
-        if timed:
-            ev["tree"].record(stream)
-        ctx.dev_inject_faults(stream.ptr, I, d_shards, spitch, d_corrupt)
-        if timed:
-            ev["fault"].record(stream)
-        ctx.dev_verify(stream.ptr, I, d_shards, spitch, None, S, d_branches, d_roots, d_present, d_valid,
-                       d_leaves_r)
-        if timed:
-            ev["verify"].record(stream)
-        ctx.dev_interpolate(stream.ptr, I, d_shards, spitch, None, S, d_valid, d_leaves_r, 1, d_roots, d_out,
-                            opitch, d_digests, d_status)
-        if timed:
-            ev["interp"].record(stream)
-        if world > 1:
+        for g, (i0, i1) in enumerate(bounds):
+            st, cx, cnt = streams[g].ptr, ctxs[g], i1 - i0
+            rec = timed and g == 0  # per-stage events on stream 0 (group 0)
+            if rec:
+                ev["t0"].record(stream)
+            cx.dev_encode(st, cnt, at(d_values, i0, vpitch), vpitch, None, B, at(d_shards, i0, n * spitch), spitch)
+            if rec:
+                ev["enc"].record(stream)
+            cx.dev_leaves(st, cnt, at(d_shards, i0, n * spitch), spitch, None, S, at(d_leaves_p, i0, n * 32))
+            if rec:
+                ev["leaf"].record(stream)
+            cx.dev_merkle_build(st, cnt, at(d_leaves_p, i0, n * 32), at(d_roots, i0, 32),
+                                at(d_branches, i0, n * max(d, 1) * 32))
+            if rec:
+                ev["tree"].record(stream)
+            cx.dev_inject_faults(st, cnt, at(d_shards, i0, n * spitch), spitch, at(d_corrupt, i0, 4))
+            if rec:
+                ev["fault"].record(stream)
+            cx.dev_verify(st, cnt, at(d_shards, i0, n * spitch), spitch, None, S,
+                          at(d_branches, i0, n * max(d, 1) * 32), at(d_roots, i0, 32), at(d_present, i0, n),
+                          at(d_valid, i0, n), at(d_leaves_r, i0, n * 32))
+            if rec:
+                ev["verify"].record(stream)
+            cx.dev_interpolate(st, cnt, at(d_shards, i0, n * spitch), spitch, None, S, at(d_valid, i0, n),
+                               at(d_leaves_r, i0, n * 32), 1, at(d_roots, i0, 32), at(d_out, i0, opitch), opitch,
+                               at(d_digests, i0, 32), at(d_status, i0, 4))
+            if rec:
+                ev["interp"].record(stream)
+        if gather:
+            for s_ in streams[1:]:
+                s_.sync()
             ctx.dev_allgather_roots(stream.ptr, I, d_roots, d_digests, d_gather)
         if timed:
             ev["gather"].record(stream)
 
     def barrier():
-        stream.sync()
+        for s_ in streams:
+            s_.sync()
         ca.rbc.lib.rbc_device_sync(dev)
         if dist is not None:
             dist.barrier()
@@ -162,6 +188,12 @@ def main():
     # correctness guard on the warmed-up state: every instance must decode
     status = np.frombuffer(d_status.download().tobytes(), dtype=np.int32)
     n_ok = int((status == 0).sum())
+    if gather:
+        # the gathered ACS records of this rank must equal its own {root, digest}
+        from cleisthenes_amd import acs
+        g = d_gather.download().reshape(world, I, 64)
+        mine = acs.pack_records(d_roots.download().reshape(I, 32), d_digests.download().reshape(I, 32), I)
+        assert np.array_equal(g[rank], mine), "RCCL all-gather returned wrong records"
 
     stage_ms = {kk: 0.0 for kk in ("enc", "leaf", "tree", "fault", "verify", "interp", "gather")}
     order = ["t0", "enc", "leaf", "tree", "fault", "verify", "interp", "gather"]
@@ -169,7 +201,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
-        stream.sync()
+        for s_ in streams:
+            s_.sync()
         for a, b in zip(order[:-1], order[1:]):
             stage_ms[b] += ev[a].elapsed_ms(ev[b])
     barrier()
@@ -191,12 +224,13 @@ def main():
 
     # ---- roofline of the dominant kernel --------------------------------
     blocks_per_shard = (S + 9 + 63) // 64
+    Ig = bounds[0][1] - bounds[0][0]  # instances per launch (group 0's stream when --streams > 1)
     kern = {
         # name: (avg ms, algorithmic HBM bytes per launch, sha compressions per launch)
-        "gf_rows_kernel<encode>": (stage_ms["enc"], I * (k * S + n * S), 0),
-        "sha_rows_kernel<leaves>": (stage_ms["leaf"], I * (n * S + n * 32), I * n * blocks_per_shard),
-        "sha_rows_kernel<verify>": (stage_ms["verify"], I * (n * S + n * d * 32 + n * 33 + 32 + n),
-                                    I * n * (blocks_per_shard + 2 * d)),
+        "gf_rows_kernel<encode>": (stage_ms["enc"], Ig * (k * S + n * S), 0),
+        "sha_rows_kernel<leaves>": (stage_ms["leaf"], Ig * (n * S + n * 32), Ig * n * blocks_per_shard),
+        "sha_rows_kernel<verify>": (stage_ms["verify"], Ig * (n * S + n * d * 32 + n * 33 + 32 + n),
+                                    Ig * n * (blocks_per_shard + 2 * d)),
     }
     dom = max(kern, key=lambda x: kern[x][0])
     dms, dbytes, dcomp = kern[dom]
@@ -209,7 +243,7 @@ def main():
         cps = dcomp / (dms / 1e3)
         roof["sha256_compressions_per_s"] = round(cps / 1e9, 3)
         roof["sha256_compressions_per_s_unit"] = "G/s"
-        roof["valu_frac_est"] = round(cps * 1400.0 / VALU_PEAK_OPS, 4)
+        roof["valu_frac_est"] = round(cps * 1470.0 / 64 / VALU_ISSUE_PEAK, 4)  # ~1470 VALU per compression
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic_r01.json")
     if os.path.exists(pmc_path):
         try:
@@ -239,7 +273,8 @@ def main():
         "data": "synthetic (seeded uniform bytes, 10% instances with one corrupted ECHO shard)",
         "config": {"workload": f"{args.config}: {desc}; shard+commit, ECHO verify all N, interpolate from N-f",
                    "n": n, "f": f, "value_bytes": B, "shard_bytes": S, "instances_per_gpu": I,
-                   "parallelism": f"instances partitioned over {world} GPU(s), RCCL root all-gather"},
+                   "parallelism": f"instances partitioned over {world} GPU(s), RCCL root all-gather",
+                   "streams_per_gpu": nstreams},
         "stage_ms": {kk: round(v, 4) for kk, v in stage_ms.items()},
         "decoded_ok": n_ok,
         "roofline": roof,

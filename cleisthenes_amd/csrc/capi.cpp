@@ -29,7 +29,7 @@ int gf_rcmax() {
     static const int v = [] {
         const char *e = getenv("RBC_GF_RCMAX");
         int x = e ? atoi(e) : 0;
-        return (x >= 1 && x <= 48) ? x : 28;
+        return (x >= 1 && x <= 48) ? x : 21;
     }();
     return v;
 }
@@ -364,8 +364,9 @@ int stage_interpolate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, ui
     m.leaves_inst_pitch = (uint64_t)c->n * 32;
     m.expect_roots = roots;
     m.status = status;
-    m.digests = digests;
     RBC_HIP(rbc_launch_merkle(m, true, st));
+    if (digests)
+        RBC_HIP(rbc_launch_digest(leaves, (uint64_t)c->n * 32, c->k, status, digests, count, st));
     JoinArgs j{};
     j.count = count;
     j.k = c->k;

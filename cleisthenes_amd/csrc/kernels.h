@@ -96,6 +96,7 @@ struct PrepArgs {
     uint32_t *flags;
     uint32_t *list;
     uint32_t *counter;
+    int stage_lds;             // set by the launcher: LDS holds log-domain M rows + inverse
 };
 
 struct JoinArgs {
@@ -117,6 +118,8 @@ hipError_t rbc_launch_gf_rows(const GfArgs &a, hipStream_t st);
 hipError_t rbc_launch_sha_rows(const ShaArgs &a, bool verify, hipStream_t st);
 hipError_t rbc_launch_merkle(const MerkleArgs &a, bool check, hipStream_t st);
 hipError_t rbc_launch_decode_prepare(const PrepArgs &a, hipStream_t st);
+hipError_t rbc_launch_digest(const uint8_t *leaves, uint64_t leaves_inst_pitch, int k, const int32_t *status,
+                             uint8_t *digests, int count, hipStream_t st);
 hipError_t rbc_launch_join(const JoinArgs &a, hipStream_t st);
 hipError_t rbc_launch_inject_faults(uint8_t *shards, uint64_t inst_pitch, uint32_t row_pitch,
                                     const int32_t *corrupt, int count, hipStream_t st);

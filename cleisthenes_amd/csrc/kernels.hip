@@ -63,7 +63,7 @@ RBC_DEV uint4 mask16(uint4 v, int nvalid) {
 // data rows through to shards[0..k) on the first chunk.
 // ============================================================================
 template <int RC>
-__global__ __launch_bounds__(256) void gf_rows_kernel(GfArgs a) {
+__global__ __launch_bounds__(256, (RC <= 21 ? 3 : 2)) void gf_rows_kernel(GfArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int KP = (a.K + 1) & ~1;
     uint4 *s_t01 = reinterpret_cast<uint4 *>(smem);
@@ -139,8 +139,11 @@ __global__ __launch_bounds__(256) void gf_rows_kernel(GfArgs a) {
             uint4 t01;
             uint32_t t2;
             gf_tables(cf, t01, t2);
-            s_t01[e] = t01;
-            s_t2[e] = t2;
+            // layout [j][r] (t2 as {j even, j odd} pairs): the RC rows of one
+            // input column are consecutive, so every LDS read in the hot loop
+            // is one base VGPR plus a compile-time immediate offset
+            s_t01[j * RC + r] = t01;
+            s_t2[((j >> 1) * RC + r) * 2 + (j & 1)] = t2;
         }
         __syncthreads();
 
@@ -168,9 +171,9 @@ __global__ __launch_bounds__(256) void gf_rows_kernel(GfArgs a) {
             const GfSel sb0 = gf_sel(xb.x), sb1 = gf_sel(xb.y), sb2 = gf_sel(xb.z), sb3 = gf_sel(xb.w);
 #pragma unroll
             for (int r = 0; r < RC; ++r) {
-                const uint4 ta = s_t01[r * KP + j];
-                const uint4 tb = s_t01[r * KP + j + 1];
-                const uint2 t2 = *reinterpret_cast<const uint2 *>(&s_t2[r * KP + j]);
+                const uint4 ta = s_t01[j * RC + r];
+                const uint4 tb = s_t01[(j + 1) * RC + r];
+                const uint2 t2 = *reinterpret_cast<const uint2 *>(&s_t2[((j >> 1) * RC + r) * 2]);
                 acc[r][0] = xor3(acc[r][0], gf_mul4(ta, t2.x, sa0), gf_mul4(tb, t2.y, sb0));
                 acc[r][1] = xor3(acc[r][1], gf_mul4(ta, t2.x, sa1), gf_mul4(tb, t2.y, sb1));
                 acc[r][2] = xor3(acc[r][2], gf_mul4(ta, t2.x, sa2), gf_mul4(tb, t2.y, sb2));
@@ -352,40 +355,55 @@ __global__ __launch_bounds__(64) void merkle_kernel(MerkleArgs a) {
         if (lane == 0) {
             if (a.status) a.status[inst] = ok ? 0 : RBC_ERR_ROOT_MISMATCH;
             if (a.roots) store_digest(a.roots + (size_t)inst * 32u, root);
-            if (a.digests) {
-                // batch digest over the k data leaves (8k big-endian words)
-                Sha256State s;
-                sha256_init(s);
-                const int nw = 8 * a.k;
-                const uint32_t *msg = nodes + W * 8;
-                int gw = 0;
-                bool done = false;
-                while (!done) {
-                    uint32_t w[16];
-                    bool last = false;
-#pragma unroll
-                    for (int q = 0; q < 16; ++q) {
-                        const int g = gw + q;
-                        w[q] = g < nw ? msg[g] : (g == nw ? 0x80000000u : 0u);
-                    }
-                    // the length fits this block if the pad byte is in it (or before) and words 14,15 free
-                    if (nw + 1 + 2 <= gw + 16) {
-                        const uint64_t bits = (uint64_t)nw * 32u;
-                        w[14] = (uint32_t)(bits >> 32);
-                        w[15] = (uint32_t)bits;
-                        last = true;
-                    }
-                    sha256_compress(s, w);
-                    gw += 16;
-                    done = last;
-                }
-                uint32_t d[8];
-#pragma unroll
-                for (int q = 0; q < 8; ++q) d[q] = s.h[q];
-                store_digest(a.digests + (size_t)inst * 32u, d);
-            }
         }
     }
+}
+
+// ============================================================================
+// digest: batch digest = SHA-256(leaf_0 || .. || leaf_{k-1}) of every
+// instance that passed the root recheck, one lane per instance.  The message
+// is the first 32k bytes of the instance's leaves; the last partial block is
+// assembled from 16-byte reads inside that range only (no over-read).
+// ============================================================================
+__global__ __launch_bounds__(64) void digest_kernel(const uint8_t *leaves, uint64_t leaves_inst_pitch, int k,
+                                                    const int32_t *status, uint8_t *digests, int count) {
+    const int inst = blockIdx.x * blockDim.x + threadIdx.x;
+    if (inst >= count) return;
+    if (status && status[inst] != 0) return;
+    const uint8_t *msg = leaves + (size_t)inst * leaves_inst_pitch;
+    const uint32_t len = 32u * (uint32_t)k;
+    Sha256State s;
+    sha256_init(s);
+    uint32_t w[16];
+    const uint32_t nfull = len >> 6;
+    uint4 q[4];
+    if (nfull) load_block_raw(msg, q);
+    for (uint32_t b = 0; b < nfull; ++b) {
+        bswap_block(q, w);
+        if (b + 1 < nfull) load_block_raw(msg + 64u * (b + 1), q);
+        sha256_compress(s, w);
+    }
+    // len % 64 is 0 or 32: tail = [32 bytes of leaf k-1 | 0x80 ...] or [0x80 ...]
+    const uint32_t rem = len & 63u;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) w[t] = 0;
+    if (rem) {
+        const uint4 *v = reinterpret_cast<const uint4 *>(msg + 64u * nfull);
+        const uint4 x0 = v[0], x1 = v[1];
+        w[0] = bswap32(x0.x); w[1] = bswap32(x0.y); w[2] = bswap32(x0.z); w[3] = bswap32(x0.w);
+        w[4] = bswap32(x1.x); w[5] = bswap32(x1.y); w[6] = bswap32(x1.z); w[7] = bswap32(x1.w);
+        w[8] = 0x80000000u;
+    } else {
+        w[0] = 0x80000000u;
+    }
+    const uint64_t bits = (uint64_t)len * 8u;
+    w[14] = (uint32_t)(bits >> 32);
+    w[15] = (uint32_t)bits;
+    sha256_compress(s, w);
+    uint32_t d[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) d[t] = s.h[t];
+    store_digest(digests + (size_t)inst * 32u, d);
 }
 
 // ============================================================================
@@ -494,14 +512,41 @@ __global__ __launch_bounds__(256) void decode_prepare_kernel(PrepArgs a) {
         }
         __syncthreads();
     }
-    // D[r][c] = XOR_i M[regen_r][i] * inv[i][c]
+    // D[r][c] = XOR_i M[regen_r][i] * inv[i][c], in the log domain from LDS:
+    // logInvT[c][i] = log inv[i][c], logM[r][i] = log M[regen_r][i] (0xff = zero)
     uint8_t *D = a.dmat + (size_t)inst * a.dmat_stride;
-    for (int e = tid; e < nr * k; e += 256) {
-        const int r = e / k, c = e - r * k;
-        const uint8_t *mrow = a.M + (size_t)s_regen[r] * k;
-        uint32_t acc = 0;
-        for (int i = 0; i < k; ++i) acc ^= gmul(mrow[i], A[i * k2 + k + c]);
-        D[e] = (uint8_t)acc;
+    if (a.stage_lds) {
+        uint8_t *logInvT = A + (size_t)k * k2;
+        uint8_t *logM = logInvT + (size_t)k * k;
+        for (int e = tid; e < k * k; e += 256) {
+            const int c = e / k, i = e - c * k;
+            const uint32_t x = A[i * k2 + k + c];
+            logInvT[e] = x ? s_log[x] : 0xffu;
+        }
+        for (int e = tid; e < nr * k; e += 256) {
+            const int r = e / k, i = e - r * k;
+            const uint32_t x = a.M[(size_t)s_regen[r] * k + i];
+            logM[e] = x ? s_log[x] : 0xffu;
+        }
+        __syncthreads();
+        for (int e = tid; e < nr * k; e += 256) {
+            const int r = e / k, c = e - r * k;
+            const uint8_t *lm = logM + (size_t)r * k, *li = logInvT + (size_t)c * k;
+            uint32_t acc = 0;
+            for (int i = 0; i < k; ++i) {
+                const uint32_t x = lm[i], y = li[i];
+                acc ^= (x != 0xffu && y != 0xffu) ? (uint32_t)s_exp[x + y] : 0u;
+            }
+            D[e] = (uint8_t)acc;
+        }
+    } else {
+        for (int e = tid; e < nr * k; e += 256) {
+            const int r = e / k, c = e - r * k;
+            const uint8_t *mrow = a.M + (size_t)s_regen[r] * k;
+            uint32_t acc = 0;
+            for (int i = 0; i < k; ++i) acc ^= gmul(mrow[i], A[i * k2 + k + c]);
+            D[e] = (uint8_t)acc;
+        }
     }
     if (tid == 0) a.status[inst] = 0;
 }
@@ -627,10 +672,22 @@ hipError_t rbc_launch_merkle(const MerkleArgs &a, bool check, hipStream_t st) {
     return hipGetLastError();
 }
 
+hipError_t rbc_launch_digest(const uint8_t *leaves, uint64_t leaves_inst_pitch, int k, const int32_t *status,
+                             uint8_t *digests, int count, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(digest_kernel, dim3((count + 63) / 64), dim3(64), 0, st, leaves, leaves_inst_pitch, k, status,
+                       digests, count);
+    return hipGetLastError();
+}
+
 hipError_t rbc_launch_decode_prepare(const PrepArgs &a, hipStream_t st) {
     if (a.count <= 0) return hipSuccess;
-    const size_t lds = 1552 + (size_t)a.k * 2 * a.k;
-    hipLaunchKernelGGL(decode_prepare_kernel, dim3(a.count), dim3(256), lds, st, a);
+    PrepArgs b = a;
+    const size_t base = 1552 + (size_t)a.k * 2 * a.k;
+    const size_t staged = base + (size_t)a.k * a.k + (size_t)(a.n - a.k) * a.k;
+    b.stage_lds = staged <= 96 * 1024;
+    const size_t lds = b.stage_lds ? staged : base;
+    hipLaunchKernelGGL(decode_prepare_kernel, dim3(a.count), dim3(256), lds, st, b);
     return hipGetLastError();
 }
 
