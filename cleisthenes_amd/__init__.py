@@ -8,6 +8,7 @@ C ABI in include/rbc_gpu.h.  This Python package is a thin host binding
 (INTEGRATION.md).
 """
 from .rbc import (  # noqa: F401
+    Batcher,
     Context,
     DeviceBuffer,
     Encoder,
@@ -17,4 +18,4 @@ from .rbc import (  # noqa: F401
     device_count,
 )
 
-__all__ = ["Context", "DeviceBuffer", "Encoder", "RBCError", "Stream", "Event", "device_count"]
+__all__ = ["Batcher", "Context", "DeviceBuffer", "Encoder", "RBCError", "Stream", "Event", "device_count"]

@@ -73,6 +73,17 @@ _SIGS = {
     "rbc_validate_message": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_uint32,
                                      POINTER(c_int)]),
     "rbc_interpolate": (c_int, [c_void_p, c_void_p, c_void_p, szp, c_void_p, c_size_t, szp, c_void_p]),
+    "rbc_batcher_create": (c_int, [c_void_p, c_int, c_int, POINTER(c_void_p)]),
+    "rbc_batcher_destroy": (None, [c_void_p]),
+    "rbc_batcher_shard": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, szp, c_void_p, c_void_p,
+                                  POINTER(c_uint64)]),
+    "rbc_batcher_validate": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_uint32,
+                                     POINTER(c_int), POINTER(c_uint64)]),
+    "rbc_batcher_interpolate": (c_int, [c_void_p, c_void_p, c_void_p, szp, c_void_p, c_size_t, szp, c_void_p,
+                                        POINTER(c_uint64)]),
+    "rbc_batcher_wait": (c_int, [c_void_p, c_uint64]),
+    "rbc_batcher_poll": (c_int, [c_void_p, c_uint64, POINTER(c_int)]),
+    "rbc_batcher_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
     "rbc_rs_new": (c_int, [c_int, c_int, c_int, POINTER(c_void_p)]),
     "rbc_rs_free": (None, [c_void_p]),
     "rbc_rs_encode": (c_int, [c_void_p, c_void_p, szp, c_int]),

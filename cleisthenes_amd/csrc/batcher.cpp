@@ -1,0 +1,350 @@
+// batcher.cpp -- request coalescing for the RBC data path (C++ host runtime).
+//
+// Each RBC instance in the reference runs its own goroutine event loop
+// (rbc/rbc.go:78 run(), channels at rbc/rbc.go:31-33), so shard /
+// validateMessage / interpolate calls arrive one at a time from thousands of
+// goroutines.  The GPU only pays off when many instances share a launch
+// (BASELINE north_star (4)).  A batcher accepts single-instance requests from
+// any number of threads, coalesces them per kind into one batched call
+// (rbc_shard_commit / rbc_validate_batch / rbc_interpolate_batch) when
+// `max_batch` requests are queued or the oldest has waited `max_wait_us`,
+// and completes per-request tickets; callers block in rbc_batcher_wait or
+// poll (no C -> Go callbacks).  Caller buffers must stay valid until their
+// ticket completes (the cgo shim keeps the Go slices alive until then).
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/rbc_gpu.h"
+
+namespace {
+
+enum Kind { K_SHARD = 0, K_VALIDATE = 1, K_INTERP = 2 };
+
+struct Req {
+    uint64_t ticket;
+    Kind kind;
+    std::chrono::steady_clock::time_point t0;
+    // shard
+    const uint8_t *data = nullptr;
+    size_t len = 0;
+    uint8_t *shards_out = nullptr;
+    size_t shards_cap = 0;
+    size_t *shard_len_out = nullptr;
+    uint8_t *root_out = nullptr;
+    uint8_t *branches_out = nullptr;
+    // validate
+    const uint8_t *root = nullptr;
+    const uint8_t *branch = nullptr;
+    size_t branch_len = 0;
+    const uint8_t *shard = nullptr;
+    size_t shard_len = 0;
+    uint32_t index = 0;
+    int *ok_out = nullptr;
+    // interpolate
+    std::vector<const uint8_t *> in_shards;
+    std::vector<size_t> in_lens;
+    uint8_t *value_out = nullptr;
+    size_t value_cap = 0;
+    size_t *value_len = nullptr;
+    uint8_t *digest_out = nullptr;
+};
+
+}  // namespace
+
+struct rbc_batcher {
+    rbc_ctx *ctx = nullptr;
+    int n = 0, k = 0, depth = 0;
+    int max_batch = 256;
+    int max_wait_us = 200;
+    std::mutex mu;
+    std::condition_variable cv_work, cv_done;
+    std::deque<Req> q[3];
+    std::unordered_map<uint64_t, int> done;  // ticket -> status
+    uint64_t next = 1;
+    bool stop = false;
+    uint64_t batches = 0, requests = 0;
+    std::thread worker;
+
+    void run();
+    void process(Kind kind, std::vector<Req> &batch);
+};
+
+namespace {
+
+int check_shards_sizes(const std::vector<size_t> &lens, size_t *S) {
+    size_t size = 0;
+    for (size_t l : lens)
+        if (l) { size = l; break; }
+    if (!size) return RBC_ERR_SHARD_NO_DATA;
+    for (size_t l : lens)
+        if (l && l != size) return RBC_ERR_SHARD_SIZE;
+    *S = size;
+    return RBC_OK;
+}
+
+}  // namespace
+
+void rbc_batcher::process(Kind kind, std::vector<Req> &b) {
+    const int count = (int)b.size();
+    std::vector<int> st(count, RBC_OK);
+    if (kind == K_SHARD) {
+        std::vector<const uint8_t *> vals(count);
+        std::vector<size_t> lens(count);
+        size_t Smax = 1;
+        for (int i = 0; i < count; ++i) {
+            vals[i] = b[i].data;
+            lens[i] = b[i].len;
+            Smax = std::max(Smax, (b[i].len + k - 1) / k);
+        }
+        std::vector<uint8_t> shards((size_t)count * n * Smax), roots((size_t)count * 32),
+            br((size_t)count * n * std::max(depth, 1) * 32);
+        std::vector<uint32_t> slens(count);
+        uint64_t t = 0;
+        const int rc = rbc_shard_commit(ctx, count, vals.data(), lens.data(), shards.data(), Smax, slens.data(),
+                                        roots.data(), br.data(), &t);
+        for (int i = 0; i < count; ++i) {
+            Req &r = b[i];
+            if (rc) { st[i] = rc; continue; }
+            const size_t S = slens[i];
+            if (r.shards_cap < (size_t)n * S) { st[i] = RBC_ERR_INVALID_ARG; continue; }
+            for (int j = 0; j < n; ++j)
+                memcpy(r.shards_out + (size_t)j * S, shards.data() + ((size_t)i * n + j) * Smax, S);
+            if (r.shard_len_out) *r.shard_len_out = S;
+            memcpy(r.root_out, roots.data() + (size_t)i * 32, 32);
+            if (r.branches_out && depth)
+                memcpy(r.branches_out, br.data() + (size_t)i * n * depth * 32, (size_t)n * depth * 32);
+        }
+    } else if (kind == K_VALIDATE) {
+        std::vector<const uint8_t *> sh(count), brs(count), rts(count);
+        std::vector<size_t> sl(count), bl(count);
+        std::vector<uint32_t> ix(count);
+        std::vector<uint8_t> ok(count, 0);
+        for (int i = 0; i < count; ++i) {
+            sh[i] = b[i].shard;
+            sl[i] = b[i].shard_len;
+            brs[i] = b[i].branch;
+            bl[i] = b[i].branch_len;
+            rts[i] = b[i].root;
+            ix[i] = b[i].index;
+        }
+        uint64_t t = 0;
+        const int rc =
+            rbc_validate_batch(ctx, count, sh.data(), sl.data(), ix.data(), brs.data(), bl.data(), rts.data(),
+                               ok.data(), &t);
+        for (int i = 0; i < count; ++i) {
+            if (rc) st[i] = rc;
+            else *b[i].ok_out = ok[i];
+        }
+    } else {
+        // interpolate: klauspost argument checks per request, then one batch
+        // over the requests that pass them
+        std::vector<int> idx;
+        std::vector<size_t> S(count, 0);
+        for (int i = 0; i < count; ++i) {
+            Req &r = b[i];
+            int present = 0;
+            for (size_t l : r.in_lens) present += l != 0;
+            int rc = check_shards_sizes(r.in_lens, &S[i]);
+            if (!rc && present < k) rc = RBC_ERR_TOO_FEW_SHARDS;
+            if (!rc && r.value_cap < (size_t)k * S[i]) rc = RBC_ERR_INVALID_ARG;
+            if (rc) st[i] = rc;
+            else idx.push_back(i);
+        }
+        const int m = (int)idx.size();
+        if (m) {
+            size_t Smax = 1;
+            for (int i : idx) Smax = std::max(Smax, S[i]);
+            std::vector<uint8_t> shards((size_t)m * n * Smax, 0), present((size_t)m * n, 0), roots((size_t)m * 32),
+                values((size_t)m * k * Smax), digests((size_t)m * 32);
+            std::vector<size_t> lens(m);
+            std::vector<int32_t> status(m, 0);
+            for (int t = 0; t < m; ++t) {
+                Req &r = b[idx[t]];
+                lens[t] = S[idx[t]];
+                for (int j = 0; j < n; ++j)
+                    if (r.in_lens[j]) {
+                        memcpy(shards.data() + ((size_t)t * n + j) * Smax, r.in_shards[j], lens[t]);
+                        present[(size_t)t * n + j] = 1;
+                    }
+                memcpy(roots.data() + (size_t)t * 32, r.root, 32);
+            }
+            uint64_t tk = 0;
+            const int rc = rbc_interpolate_batch(ctx, m, shards.data(), Smax, lens.data(), present.data(), roots.data(),
+                                                 values.data(), (size_t)k * Smax, digests.data(), status.data(), &tk);
+            for (int t = 0; t < m; ++t) {
+                Req &r = b[idx[t]];
+                int s = rc ? rc : status[t];
+                st[idx[t]] = s;
+                if (s) continue;
+                memcpy(r.value_out, values.data() + (size_t)t * k * Smax, (size_t)k * lens[t]);
+                if (r.value_len) *r.value_len = (size_t)k * lens[t];
+                if (r.digest_out) memcpy(r.digest_out, digests.data() + (size_t)t * 32, 32);
+            }
+        }
+    }
+    std::lock_guard<std::mutex> lk(mu);
+    for (int i = 0; i < count; ++i) done[b[i].ticket] = st[i];
+    batches++;
+    requests += count;
+    cv_done.notify_all();
+}
+
+void rbc_batcher::run() {
+    std::unique_lock<std::mutex> lk(mu);
+    while (true) {
+        // pick the kind whose queue is full, or whose oldest request is due
+        const auto now = std::chrono::steady_clock::now();
+        int pick = -1;
+        auto earliest = now + std::chrono::hours(1);
+        for (int kd = 0; kd < 3; ++kd) {
+            if (q[kd].empty()) continue;
+            const auto due = q[kd].front().t0 + std::chrono::microseconds(max_wait_us);
+            if ((int)q[kd].size() >= max_batch || due <= now || stop) { pick = kd; break; }
+            earliest = std::min(earliest, due);
+        }
+        if (pick < 0) {
+            if (stop) return;
+            cv_work.wait_until(lk, earliest);
+            continue;
+        }
+        std::vector<Req> batch;
+        while (!q[pick].empty() && (int)batch.size() < max_batch) {
+            batch.push_back(std::move(q[pick].front()));
+            q[pick].pop_front();
+        }
+        lk.unlock();
+        process((Kind)pick, batch);
+        lk.lock();
+    }
+}
+
+namespace {
+uint64_t enqueue(rbc_batcher *b, Req &&r) {
+    std::lock_guard<std::mutex> lk(b->mu);
+    r.ticket = b->next++;
+    r.t0 = std::chrono::steady_clock::now();
+    const uint64_t t = r.ticket;
+    const Kind kd = r.kind;
+    b->q[kd].push_back(std::move(r));
+    if ((int)b->q[kd].size() >= b->max_batch || b->q[kd].size() == 1) b->cv_work.notify_one();
+    return t;
+}
+}  // namespace
+
+extern "C" {
+
+int rbc_batcher_create(rbc_ctx *ctx, int max_batch, int max_wait_us, rbc_batcher **out) {
+    if (!ctx || !out || max_batch < 1 || max_wait_us < 0) return RBC_ERR_INVALID_ARG;
+    rbc_batcher *b = new rbc_batcher();
+    b->ctx = ctx;
+    int k = 0, p = 0, d = 0;
+    rbc_ctx_params(ctx, &k, &p, &d);
+    b->k = k;
+    b->n = k + p;
+    b->depth = d;
+    b->max_batch = max_batch;
+    b->max_wait_us = max_wait_us;
+    b->worker = std::thread([b] { b->run(); });
+    *out = b;
+    return RBC_OK;
+}
+
+void rbc_batcher_destroy(rbc_batcher *b) {
+    if (!b) return;
+    {
+        std::lock_guard<std::mutex> lk(b->mu);
+        b->stop = true;  // drains every queue before the worker exits
+    }
+    b->cv_work.notify_all();
+    if (b->worker.joinable()) b->worker.join();
+    delete b;
+}
+
+int rbc_batcher_shard(rbc_batcher *b, const uint8_t *data, size_t len, uint8_t *shards_out, size_t shards_cap,
+                      size_t *shard_len_out, uint8_t *root_out, uint8_t *branches_out, uint64_t *ticket) {
+    if (!b || !ticket || !shards_out || !root_out) return RBC_ERR_INVALID_ARG;
+    if (len == 0) return RBC_ERR_SHORT_DATA;
+    if (!data) return RBC_ERR_INVALID_ARG;
+    Req r;
+    r.kind = K_SHARD;
+    r.data = data;
+    r.len = len;
+    r.shards_out = shards_out;
+    r.shards_cap = shards_cap;
+    r.shard_len_out = shard_len_out;
+    r.root_out = root_out;
+    r.branches_out = branches_out;
+    *ticket = enqueue(b, std::move(r));
+    return RBC_OK;
+}
+
+int rbc_batcher_validate(rbc_batcher *b, const uint8_t *root, const uint8_t *branch, size_t branch_len,
+                         const uint8_t *shard, size_t shard_len, uint32_t index, int *ok_out, uint64_t *ticket) {
+    if (!b || !ticket || !ok_out || !root) return RBC_ERR_INVALID_ARG;
+    *ok_out = 0;
+    Req r;
+    r.kind = K_VALIDATE;
+    r.root = root;
+    r.branch = branch;
+    r.branch_len = branch_len;
+    r.shard = shard;
+    r.shard_len = shard_len;
+    r.index = index;
+    r.ok_out = ok_out;
+    *ticket = enqueue(b, std::move(r));
+    return RBC_OK;
+}
+
+int rbc_batcher_interpolate(rbc_batcher *b, const uint8_t *root, const uint8_t *const *shards, const size_t *lens,
+                            uint8_t *value_out, size_t value_cap, size_t *value_len, uint8_t *digest_out,
+                            uint64_t *ticket) {
+    if (!b || !ticket || !root || !shards || !lens || !value_out) return RBC_ERR_INVALID_ARG;
+    Req r;
+    r.kind = K_INTERP;
+    r.root = root;
+    r.in_shards.assign(shards, shards + b->n);
+    r.in_lens.assign(lens, lens + b->n);
+    r.value_out = value_out;
+    r.value_cap = value_cap;
+    r.value_len = value_len;
+    r.digest_out = digest_out;
+    *ticket = enqueue(b, std::move(r));
+    return RBC_OK;
+}
+
+int rbc_batcher_wait(rbc_batcher *b, uint64_t ticket) {
+    if (!b) return RBC_ERR_INVALID_ARG;
+    std::unique_lock<std::mutex> lk(b->mu);
+    if (ticket == 0 || ticket >= b->next) return RBC_ERR_INVALID_ARG;
+    b->cv_work.notify_one();
+    b->cv_done.wait(lk, [&] { return b->done.count(ticket) != 0; });
+    const int s = b->done[ticket];
+    b->done.erase(ticket);
+    return s;
+}
+
+int rbc_batcher_poll(rbc_batcher *b, uint64_t ticket, int *done_out) {
+    if (!b || !done_out) return RBC_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(b->mu);
+    if (ticket == 0 || ticket >= b->next) return RBC_ERR_INVALID_ARG;
+    *done_out = b->done.count(ticket) != 0;
+    return RBC_OK;
+}
+
+int rbc_batcher_stats(rbc_batcher *b, uint64_t *batches, uint64_t *requests) {
+    if (!b) return RBC_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(b->mu);
+    if (batches) *batches = b->batches;
+    if (requests) *requests = b->requests;
+    return RBC_OK;
+}
+
+}  // extern "C"

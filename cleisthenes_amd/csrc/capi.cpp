@@ -84,6 +84,8 @@ struct rbc_ctx {
     uint8_t *d_M = nullptr;        // device copy; parity rows at d_M + k*k
     std::mutex mu;
     hipStream_t stream = nullptr;  // host-API stream
+    hipStream_t aux = nullptr;     // fork stream inside interpolate (join beside the regen hashing)
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // interpolate workspace (device API)
     DevBuf ws_used, ws_regen, ws_dmat, ws_nmiss, ws_flags, ws_list, ws_counter;
     // host-API staging
@@ -121,7 +123,10 @@ int ctx_create_kn(int n, int k, int device, rbc_ctx **out) {
     if (!rbchost::build_matrix(k, n, c->h_M)) { delete c; return RBC_ERR_SINGULAR; }
     if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->d_M, c->h_M.size()) != hipSuccess ||
         hipMemcpy(c->d_M, c->h_M.data(), c->h_M.size(), hipMemcpyHostToDevice) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
         if (c->d_M) (void)hipFree(c->d_M);
         delete c;
         return RBC_ERR_DEVICE;
@@ -331,6 +336,28 @@ int stage_interpolate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, ui
     int rc = stage_regenerate(c, st, count, shards, shard_pitch, shard_lens, uniform_shard_len, valid, status,
                               leaves_verified);
     if (rc) return rc;
+    // fork: value assembly (HBM-bound) runs on the aux stream beside the
+    // regen hashing (latency-bound, under-fills the SIMDs); it needs only the
+    // regenerated rows.  values_out is defined where status == 0.
+    RBC_HIP(hipEventRecord(c->ev_fork, st));
+    RBC_HIP(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+    {
+        JoinArgs j{};
+        j.count = count;
+        j.k = c->k;
+        j.chunks = value_pitch / 16;
+        j.shards = shards;
+        j.inst_pitch = (uint64_t)c->n * shard_pitch;
+        j.row_pitch = shard_pitch;
+        j.inst_bytes = (uint32_t)((uint64_t)c->n * shard_pitch);
+        j.lens = shard_lens;
+        j.uniform_len = uniform_shard_len;
+        j.values = values_out;
+        j.value_pitch = value_pitch;
+        j.status = status;
+        RBC_HIP(rbc_launch_join(j, c->aux));
+    }
+    RBC_HIP(hipEventRecord(c->ev_join, c->aux));
     const int nr = c->n - c->k;
     ShaArgs a{};
     a.count = count;
@@ -367,20 +394,7 @@ int stage_interpolate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, ui
     RBC_HIP(rbc_launch_merkle(m, true, st));
     if (digests)
         RBC_HIP(rbc_launch_digest(leaves, (uint64_t)c->n * 32, c->k, status, digests, count, st));
-    JoinArgs j{};
-    j.count = count;
-    j.k = c->k;
-    j.chunks = value_pitch / 16;
-    j.shards = shards;
-    j.inst_pitch = (uint64_t)c->n * shard_pitch;
-    j.row_pitch = shard_pitch;
-    j.inst_bytes = (uint32_t)((uint64_t)c->n * shard_pitch);
-    j.lens = shard_lens;
-    j.uniform_len = uniform_shard_len;
-    j.values = values_out;
-    j.value_pitch = value_pitch;
-    j.status = status;
-    RBC_HIP(rbc_launch_join(j, st));
+    RBC_HIP(hipStreamWaitEvent(st, c->ev_join, 0));  // join back before returning to the caller's stream
     return RBC_OK;
 }
 
@@ -494,6 +508,9 @@ void rbc_ctx_destroy(rbc_ctx *c) {
         b->release();
     if (c->d_M) (void)hipFree(c->d_M);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->aux) (void)hipStreamDestroy(c->aux);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     delete c;
 }
 

@@ -395,3 +395,77 @@ class Encoder:
         out = np.zeros(max(out_size, 1), dtype=np.uint8)
         check(lib.rbc_rs_join(self._p, ptrs, lens, n, out_size, _ptr(out)), "Join")
         return bytes(out[:out_size])
+
+
+class Batcher:
+    """Request coalescing (include/rbc_gpu.h rbc_batcher_*): single-instance
+    shard / validate / interpolate submissions from any number of threads are
+    merged into batched launches.  ``submit_*`` return a handle that keeps the
+    request's buffers alive; ``wait`` completes it."""
+
+    def __init__(self, ctx: Context, max_batch: int = 256, max_wait_us: int = 200):
+        p = c_void_p()
+        check(lib.rbc_batcher_create(ctx.handle, max_batch, max_wait_us, byref(p)), "rbc_batcher_create")
+        self._p = p
+        self.ctx = ctx
+
+    def close(self) -> None:
+        if getattr(self, "_p", None):
+            lib.rbc_batcher_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def submit_shard(self, data) -> dict:
+        d = _bytes_array(data).copy()
+        k, n = self.ctx.k, self.ctx.n
+        S = (len(d) + k - 1) // k if len(d) else 0
+        h = {"kind": "shard", "data": d, "out": np.zeros(max(n * S, 1), np.uint8), "root": np.zeros(32, np.uint8),
+             "br": np.zeros(max(n * self.ctx.depth * 32, 1), np.uint8), "slen": c_size_t(0), "t": c_uint64(0)}
+        check(lib.rbc_batcher_shard(self._p, _ptr(d) if len(d) else None, len(d), _ptr(h["out"]), h["out"].nbytes,
+                                    byref(h["slen"]), _ptr(h["root"]), _ptr(h["br"]), byref(h["t"])),
+              "rbc_batcher_shard")
+        return h
+
+    def submit_validate(self, root, branch, shard, index) -> dict:
+        r, b, s = _bytes_array(root).copy(), _bytes_array(branch).copy(), _bytes_array(shard).copy()
+        h = {"kind": "validate", "r": r, "b": b, "s": s, "ok": c_int(0), "t": c_uint64(0)}
+        check(lib.rbc_batcher_validate(self._p, _ptr(r), _ptr(b) if len(b) else None, len(b),
+                                       _ptr(s) if len(s) else None, len(s), index, byref(h["ok"]), byref(h["t"])),
+              "rbc_batcher_validate")
+        return h
+
+    def submit_interpolate(self, root, shards) -> dict:
+        n, k = self.ctx.n, self.ctx.k
+        arrs = [_bytes_array(x).copy() for x in shards]
+        S = max(len(a) for a in arrs)
+        lens = (c_size_t * n)(*[len(a) for a in arrs])
+        ptrs = (c_void_p * n)(*[(a.ctypes.data if len(a) else None) for a in arrs])
+        r = _bytes_array(root).copy()
+        h = {"kind": "interp", "arrs": arrs, "lens": lens, "ptrs": ptrs, "r": r,
+             "value": np.zeros(max(k * S, 1), np.uint8), "vlen": c_size_t(0), "dig": np.zeros(32, np.uint8),
+             "t": c_uint64(0)}
+        check(lib.rbc_batcher_interpolate(self._p, _ptr(r), ptrs, lens, _ptr(h["value"]), h["value"].nbytes,
+                                          byref(h["vlen"]), _ptr(h["dig"]), byref(h["t"])), "rbc_batcher_interpolate")
+        return h
+
+    def wait(self, h: dict):
+        st = lib.rbc_batcher_wait(self._p, h["t"].value)
+        if h["kind"] == "validate":
+            check(st, "validate")
+            return bool(h["ok"].value)
+        check(st, h["kind"])
+        if h["kind"] == "shard":
+            S = h["slen"].value
+            return {"shards": [h["out"][j * S:(j + 1) * S].copy() for j in range(self.ctx.n)],
+                    "root": bytes(h["root"]), "shard_len": S}
+        return {"value": bytes(h["value"][: h["vlen"].value]), "digest": bytes(h["dig"])}
+
+    def stats(self):
+        b, r = c_uint64(0), c_uint64(0)
+        check(lib.rbc_batcher_stats(self._p, byref(b), byref(r)))
+        return b.value, r.value

@@ -183,6 +183,30 @@ int rbc_validate_message(rbc_ctx *ctx, const uint8_t *root, const uint8_t *branc
 int rbc_interpolate(rbc_ctx *ctx, const uint8_t *root, const uint8_t *const *shards, const size_t *lens,
                     uint8_t *value_out, size_t value_cap, size_t *value_len, uint8_t *digest_out);
 
+/* ---- request batcher (north_star (4): many RBC instances per launch) -------
+ * Thousands of per-instance RBC event loops (rbc/rbc.go:78, one goroutine
+ * each) submit single requests from any thread; a worker coalesces them per
+ * kind into one batched launch when max_batch are queued or the oldest has
+ * waited max_wait_us.  Caller buffers stay valid until the ticket completes.
+ * rbc_batcher_wait returns the request's own status (RBC_OK, klauspost error,
+ * RBC_ERR_ROOT_MISMATCH, ...) and releases the ticket. */
+typedef struct rbc_batcher rbc_batcher;
+int rbc_batcher_create(rbc_ctx *ctx, int max_batch, int max_wait_us, rbc_batcher **out);
+void rbc_batcher_destroy(rbc_batcher *b); /* drains pending requests first */
+/* shard(): shards_out n*S (shard j at j*S), root 32 B, branches n*d*32 (device form, nullable) */
+int rbc_batcher_shard(rbc_batcher *b, const uint8_t *data, size_t len, uint8_t *shards_out, size_t shards_cap,
+                      size_t *shard_len_out, uint8_t *root_out, uint8_t *branches_out, uint64_t *ticket);
+/* validateMessage(): *ok_out set when the ticket completes */
+int rbc_batcher_validate(rbc_batcher *b, const uint8_t *root, const uint8_t *branch, size_t branch_len,
+                         const uint8_t *shard, size_t shard_len, uint32_t index, int *ok_out, uint64_t *ticket);
+/* interpolate(): shards/lens are n entries (lens[j] == 0: missing) */
+int rbc_batcher_interpolate(rbc_batcher *b, const uint8_t *root, const uint8_t *const *shards, const size_t *lens,
+                            uint8_t *value_out, size_t value_cap, size_t *value_len, uint8_t *digest_out,
+                            uint64_t *ticket);
+int rbc_batcher_wait(rbc_batcher *b, uint64_t ticket);
+int rbc_batcher_poll(rbc_batcher *b, uint64_t ticket, int *done);
+int rbc_batcher_stats(rbc_batcher *b, uint64_t *batches, uint64_t *requests);
+
 /* ---- reedsolomon.Encoder mirror (klauspost v1.9.1 semantics) ---------------
  * Shards are host buffers; lens[i] == 0 marks a missing shard (Go len 0).
  * Reconstruct writes missing shards into the caller's buffers (capacity >= the

@@ -373,3 +373,51 @@ def test_byzantine_noncodeword_rejected_by_every_subset(gpu, golden):
         with pytest.raises(gpu.RBCError) as ei:
             ctx.interpolate(root, [s if j in keep else None for j, s in enumerate(shards)])
         assert ei.value.code == -8
+
+
+def test_batcher_coalesces_concurrent_requests(gpu, ref):
+    """Many threads (the Go goroutines) submit single-instance shard /
+    validate / interpolate requests; the batcher merges them into few
+    launches and every result is bit-exact."""
+    import threading
+
+    n, f = 16, 5
+    ctx = gpu.Context(n, f)
+    bt = gpu.Batcher(ctx, max_batch=64, max_wait_us=2000)
+    rng = np.random.default_rng(42)
+    values = [rng.integers(0, 256, int(rng.integers(1, 5000)), dtype=np.uint8) for _ in range(96)]
+    results = [None] * len(values)
+    errors = []
+
+    def worker(idx):
+        try:
+            h = bt.submit_shard(values[idx])
+            out = bt.wait(h)
+            shards, root, br, _ = ref.encode_commit(n, f, values[idx])
+            assert out["root"] == root
+            assert all(np.array_equal(out["shards"][j], shards[j]) for j in range(n))
+            # validate every shard, then interpolate from a random k subset
+            hs = []
+            com = orc.rbc_commit(shards)
+            for j in range(n):
+                hs.append(bt.submit_validate(root, orc.flat_branch(com["branches"][j]), shards[j], j))
+            assert all(bt.wait(hh) for hh in hs)
+            keep = set(np.random.default_rng(idx).permutation(n)[: ctx.k].tolist())
+            hi = bt.submit_interpolate(root, [shards[j] if j in keep else b"" for j in range(n)])
+            res = bt.wait(hi)
+            assert res["value"][: len(values[idx])] == values[idx].tobytes()
+            results[idx] = True
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=worker, args=(i,)) for i in range(len(values))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=120)
+    assert not errors, errors[:3]
+    assert all(results)
+    batches, requests = bt.stats()
+    assert requests == len(values) * (2 + n)
+    assert batches < requests / 4, (batches, requests)  # actually coalesced
+    bt.close()
