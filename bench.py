@@ -225,9 +225,10 @@ def main():
     # ---- roofline of the dominant kernel --------------------------------
     blocks_per_shard = (S + 9 + 63) // 64
     Ig = bounds[0][1] - bounds[0][0]  # instances per launch (group 0's stream when --streams > 1)
+    enc_kernel = "rs_fft_kernel<encode>" if ctx.codec == "fft" else "gf_rows_kernel<encode>"
     kern = {
         # name: (avg ms, algorithmic HBM bytes per launch, sha compressions per launch)
-        "gf_rows_kernel<encode>": (stage_ms["enc"], Ig * (k * S + n * S), 0),
+        enc_kernel: (stage_ms["enc"], Ig * (k * S + n * S), 0),
         "sha_rows_kernel<leaves>": (stage_ms["leaf"], Ig * (n * S + n * 32), Ig * n * blocks_per_shard),
         "sha_rows_kernel<verify>": (stage_ms["verify"], Ig * (n * S + n * d * 32 + n * 33 + 32 + n),
                                     Ig * n * (blocks_per_shard + 2 * d)),
@@ -274,7 +275,7 @@ def main():
         "config": {"workload": f"{args.config}: {desc}; shard+commit, ECHO verify all N, interpolate from N-f",
                    "n": n, "f": f, "value_bytes": B, "shard_bytes": S, "instances_per_gpu": I,
                    "parallelism": f"instances partitioned over {world} GPU(s), RCCL root all-gather",
-                   "streams_per_gpu": nstreams},
+                   "streams_per_gpu": nstreams, "gf_codec": ctx.codec},
         "stage_ms": {kk: round(v, 4) for kk, v in stage_ms.items()},
         "decoded_ok": n_ok,
         "roofline": roof,

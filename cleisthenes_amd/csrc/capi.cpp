@@ -34,6 +34,15 @@ int gf_rcmax() {
     return v;
 }
 
+// RBC_CODEC=matrix forces the matrix kernel for new contexts (A/B runs)
+int codec_default() {
+    static const int v = [] {
+        const char *e = getenv("RBC_CODEC");
+        return (e && strcmp(e, "matrix") == 0) ? RBC_CODEC_MATRIX : RBC_CODEC_AUTO;
+    }();
+    return v;
+}
+
 int tree_width(int n) {
     int w = 1;
     while (w < n) w <<= 1;
@@ -80,6 +89,7 @@ struct DevBuf {
 
 struct rbc_ctx {
     int n = 0, f = 0, k = 0, p = 0, depth = 0, width = 0, device = 0;
+    bool fft = false;              // additive-FFT codec active (rs_fft.hip)
     std::vector<uint8_t> h_M;      // n x k encode matrix
     uint8_t *d_M = nullptr;        // device copy; parity rows at d_M + k*k
     std::mutex mu;
@@ -87,7 +97,7 @@ struct rbc_ctx {
     hipStream_t aux = nullptr;     // fork stream inside interpolate (join beside the regen hashing)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // interpolate workspace (device API)
-    DevBuf ws_used, ws_regen, ws_dmat, ws_nmiss, ws_flags, ws_list, ws_counter;
+    DevBuf ws_used, ws_regen, ws_dmat, ws_nmiss, ws_flags, ws_list, ws_counter, ws_rcount, ws_cls;
     // host-API staging
     DevBuf d_values, d_shards, d_leaves, d_roots, d_branches, d_valid, d_status, d_digests, d_lens, d_slens,
         d_idx, d_present;
@@ -120,6 +130,7 @@ int ctx_create_kn(int n, int k, int device, rbc_ctx **out) {
     c->width = tree_width(n);
     c->depth = tree_depth(n);
     c->device = device;
+    c->fft = codec_default() != RBC_CODEC_MATRIX && rbc_fft_supported(n, k);
     if (!rbchost::build_matrix(k, n, c->h_M)) { delete c; return RBC_ERR_SINGULAR; }
     if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->d_M, c->h_M.size()) != hipSuccess ||
         hipMemcpy(c->d_M, c->h_M.data(), c->h_M.size(), hipMemcpyHostToDevice) != hipSuccess ||
@@ -149,6 +160,22 @@ int stage_encode(rbc_ctx *c, hipStream_t st, int count, const uint8_t *values, u
     }
     if (value_pitch > 0x7fffffffULL || (uint64_t)c->n * shard_pitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
     if (count == 0) return RBC_OK;
+    if (c->fft) {
+        FftArgs a{};
+        a.count = count;
+        a.n = c->n;
+        a.k = c->k;
+        a.mode = GF_MODE_ENCODE;
+        a.values = values;
+        a.value_pitch = (uint32_t)value_pitch;
+        a.shards = shards;
+        a.inst_pitch = (uint64_t)c->n * shard_pitch;
+        a.row_pitch = shard_pitch;
+        a.lens = value_lens;
+        a.uniform_len = uniform_value_len;
+        RBC_HIP(rbc_launch_rs_fft(a, st));
+        return RBC_OK;
+    }
     GfArgs g{};
     g.count = count;
     g.tiles = (int)((shard_pitch + 4095) / 4096);
@@ -250,6 +277,8 @@ int ensure_ws(rbc_ctx *c, int count) {
     RBC_HIP(c->ws_flags.ensure((size_t)count * c->n * 4));
     RBC_HIP(c->ws_list.ensure((size_t)count * nr * 4));
     RBC_HIP(c->ws_counter.ensure(16));
+    RBC_HIP(c->ws_rcount.ensure((size_t)count * 4));
+    RBC_HIP(c->ws_cls.ensure((size_t)count * round_up(c->n, 4)));
     return RBC_OK;
 }
 
@@ -283,8 +312,62 @@ int stage_regenerate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, uin
         pa.list = c->ws_list.as<uint32_t>();
         pa.counter = c->ws_counter.as<uint32_t>();
     }
+    if (c->fft) {
+        pa.fft = 1;
+        pa.rcount = c->ws_rcount.as<int32_t>();
+        pa.cls = c->ws_cls.as<uint8_t>();
+        pa.cls_stride = (uint32_t)round_up(c->n, 4);
+    }
     RBC_HIP(rbc_launch_decode_prepare(pa, st));
-    if (nr > 0) {
+    if (c->fft && nr > 0) {
+        // 1) missing data rows: D (rcount[i] x k, per instance) times the used rows
+        const int rmax = std::min(c->k, nr);
+        GfArgs g{};
+        g.count = count;
+        g.tiles = (int)((shard_pitch + 4095) / 4096);
+        g.R = rmax;
+        g.K = c->k;
+        g.rc = rbc_gf_pick_rc(rmax, gf_rcmax());
+        g.mode = GF_MODE_DECODE;
+        g.in = shards;
+        g.in_inst_pitch = (uint64_t)c->n * shard_pitch;
+        g.in_row_pitch = shard_pitch;
+        g.in_inst_bytes = (uint32_t)((uint64_t)c->n * shard_pitch);
+        g.out = shards;
+        g.out_inst_pitch = (uint64_t)c->n * shard_pitch;
+        g.out_row_pitch = shard_pitch;
+        g.lens = shard_lens;
+        g.uniform_len = uniform_shard_len;
+        g.coef = pa.dmat;
+        g.coef_inst_stride = pa.dmat_stride;
+        g.in_idx = pa.used;
+        g.out_idx = pa.regen;
+        g.idx_stride = pa.used_stride;
+        g.idx_stride2 = pa.regen_stride;
+        g.status = status;
+        g.rcount = pa.rcount;
+        RBC_HIP(rbc_launch_gf_rows(g, st));
+        // 2) parity positions: additive-FFT re-encode of the completed data half
+        FftArgs a{};
+        a.count = count;
+        a.n = c->n;
+        a.k = c->k;
+        a.mode = GF_MODE_DECODE;
+        a.shards = shards;
+        a.inst_pitch = (uint64_t)c->n * shard_pitch;
+        a.row_pitch = shard_pitch;
+        a.lens = shard_lens;
+        a.uniform_len = uniform_shard_len;
+        a.status = status;
+        a.cls = pa.cls;
+        a.cls_stride = pa.cls_stride;
+        if (compare) {
+            a.flags = pa.flags;
+            a.list = pa.list;
+            a.counter = pa.counter;
+        }
+        RBC_HIP(rbc_launch_rs_fft(a, st));
+    } else if (nr > 0) {
         GfArgs g{};
         g.count = count;
         g.tiles = (int)((shard_pitch + 4095) / 4096);
@@ -502,7 +585,7 @@ void rbc_ctx_destroy(rbc_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     for (DevBuf *b : {&c->ws_used, &c->ws_regen, &c->ws_dmat, &c->ws_nmiss, &c->ws_flags, &c->ws_list,
-                      &c->ws_counter, &c->d_values, &c->d_shards, &c->d_leaves,
+                      &c->ws_counter, &c->ws_rcount, &c->ws_cls, &c->d_values, &c->d_shards, &c->d_leaves,
                       &c->d_roots, &c->d_branches, &c->d_valid, &c->d_status, &c->d_digests, &c->d_lens,
                       &c->d_slens, &c->d_idx, &c->d_present, &c->h_stage, &c->h_small, &c->d_pack})
         b->release();
@@ -519,6 +602,26 @@ int rbc_ctx_params(const rbc_ctx *c, int *k, int *p, int *depth) {
     if (k) *k = c->k;
     if (p) *p = c->p;
     if (depth) *depth = c->depth;
+    return RBC_OK;
+}
+
+int rbc_ctx_set_codec(rbc_ctx *c, int codec) {
+    if (!c) return RBC_ERR_INVALID_ARG;
+    if (codec == RBC_CODEC_MATRIX) {
+        c->fft = false;
+    } else if (codec == RBC_CODEC_AUTO || codec == RBC_CODEC_FFT) {
+        const bool ok = rbc_fft_supported(c->n, c->k);
+        if (codec == RBC_CODEC_FFT && !ok) return RBC_ERR_INVALID_ARG;
+        c->fft = ok;
+    } else {
+        return RBC_ERR_INVALID_ARG;
+    }
+    return RBC_OK;
+}
+
+int rbc_ctx_codec(const rbc_ctx *c, int *codec) {
+    if (!c || !codec) return RBC_ERR_INVALID_ARG;
+    *codec = c->fft ? RBC_CODEC_FFT : RBC_CODEC_MATRIX;
     return RBC_OK;
 }
 

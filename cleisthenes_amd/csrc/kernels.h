@@ -39,6 +39,7 @@ struct GfArgs {
     uint32_t *list;            // (inst << 8 | pos) rows to hash
     uint32_t *counter;
     int n;
+    const int32_t *rcount;     // per-instance output row count (nullable -> R)
 };
 
 struct ShaArgs {
@@ -96,6 +97,12 @@ struct PrepArgs {
     uint32_t *flags;
     uint32_t *list;
     uint32_t *counter;
+    // FFT codec: D covers only the missing data rows (rcount[i] of them, they
+    // lead `regen`); cls[i][pos] = 0 skip / 1 store / 2 compare for pos >= k
+    int fft;
+    int32_t *rcount;
+    uint8_t *cls;
+    uint32_t cls_stride;
     int stage_lds;             // set by the launcher: LDS holds log-domain M rows + inverse
 };
 
@@ -112,6 +119,32 @@ struct JoinArgs {
     uint32_t value_pitch;
     const int32_t *status;
 };
+
+// rs_fft_kernel (rs_fft.hip): additive-FFT systematic encode, one lane per
+// dword column of one instance
+struct FftArgs {
+    int count, n, k;
+    int mode;                  // GF_MODE_ENCODE: values -> data + parity rows;
+                               // GF_MODE_DECODE: data rows -> parity rows by class
+    const uint8_t *values;     // encode: [I][value_pitch]
+    uint32_t value_pitch;
+    uint8_t *shards;           // [I][N][row_pitch]
+    uint64_t inst_pitch;
+    uint32_t row_pitch;
+    const uint32_t *lens;      // encode: B_i, decode: S_i (nullable)
+    uint32_t uniform_len;
+    const int32_t *status;     // nullable
+    // decode: per-position class [I][cls_stride] (0 skip, 1 store, 2 compare);
+    // nullptr -> store every parity position
+    const uint8_t *cls;
+    uint32_t cls_stride;       // multiple of 4
+    uint32_t *flags;           // [I][n]
+    uint32_t *list;
+    uint32_t *counter;
+};
+
+bool rbc_fft_supported(int n, int k);
+hipError_t rbc_launch_rs_fft(const FftArgs &a, hipStream_t st);
 
 int rbc_gf_pick_rc(int R, int rcmax);
 hipError_t rbc_launch_gf_rows(const GfArgs &a, hipStream_t st);

@@ -128,9 +128,11 @@ __global__ __launch_bounds__(256, (RC <= 21 ? 3 : 2)) void gf_rows_kernel(GfArgs
     };
 
     const int cmp_from = a.nmiss ? a.nmiss[inst] : 0x7fffffff;
+    const int rlim = a.rcount ? min(a.rcount[inst], a.R) : a.R;  // block-uniform
+    if (a.R > 0 && c * RC >= rlim) return;
     {
         const int r0 = c * RC;
-        const int rows = min(RC, a.R - r0);
+        const int rows = min(RC, rlim - r0);
         for (int e = tid; e < RC * KP; e += 256) {
             const int r = e / KP, j = e - r * KP;
             uint32_t cf = 0;
@@ -447,6 +449,21 @@ __global__ __launch_bounds__(256) void decode_prepare_kernel(PrepArgs a) {
         int nr = nm;
         for (int j = 0, seen = 0; j < n; ++j)
             if (v[j] && seen++ >= k) s_regen[nr++] = (uint8_t)j;
+        if (a.fft) {
+            // FFT codec: only the missing DATA rows go through D (they lead
+            // regen: missing positions are listed in index order); parity
+            // positions are re-encoded by rs_fft_kernel, by class
+            int md = 0;
+            while (md < nm && s_regen[md] < k) ++md;
+            nr = md;
+            if (a.rcount) a.rcount[inst] = md;
+            uint8_t *cl = a.cls + (size_t)inst * a.cls_stride;
+            for (int j = 0, seen = 0; j < n; ++j) {
+                const bool used = v[j] && seen < k;
+                seen += v[j] ? 1 : 0;
+                cl[j] = (j < k || used) ? 0 : (!v[j] ? 1 : (a.counter ? 2 : 1));
+            }
+        }
         s_misc[0] = nu;
         s_misc[1] = nr;
         s_misc[2] = (a.counter && nu >= k) ? (int)atomicAdd(a.counter, (unsigned)nm) : 0;

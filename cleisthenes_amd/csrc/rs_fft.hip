@@ -1,0 +1,306 @@
+// rs_fft.hip -- Reed-Solomon systematic encode over GF(2^8)/0x11D by additive
+// FFT, for gfx950.  Bit-identical to klauspost/reedsolomon v1.9.1's matrix
+// code (held at rbc/rbc.go:20; shard() at rbc/rbc.go:97-100) because it
+// computes the same linear map:
+//
+//   klauspost's M = V * inv(V[:k]), V[r][c] = r^c, so shard r is P(r) for the
+//   unique P with deg P < k and P(j) = data_j (j < k), evaluated at the field
+//   elements with integer labels 0..N-1.  Those labels form the GF(2)-subspace
+//   V_n = span{1, 2, .., 2^(n-1)}, the domain of the Lin-Chung-Han additive FFT
+//   in the novel polynomial basis X_i = prod_{j in bits(i)} W_j, where
+//   W_j = s_j / s_j(2^j) and s_j is the vanishing polynomial of V_j.  deg P < k
+//   iff the novel coefficients vanish from index k on, so
+//     coeffs  = solve(n, 0, data, k)   (only power-of-two IFFT/FFT blocks)
+//     shards  = FFT(coeffs) at the positions [k, N)
+//   Model and op counts: tools/rs_fft_model.py (checked against the oracle).
+//
+// Every butterfly constant W_j(lambda) is a compile-time constant, so the
+// whole transform unrolls into straight-line VALU code: a constant multiply of
+// 4 packed bytes is three v_perm_b32 lookups into literal 8-entry tables
+// (the CDNA analogue of PSHUFB split-nibble tables), the add is v_bitop3 xor3.
+// One lane owns one dword column of every row of one instance; the rows live
+// in VGPRs for the whole transform (no LDS).  At N=128, k=44: 462 constant
+// multiplies + ~550 xors per column instead of the matrix's 3,696 MACs.
+//
+// Modes: ENCODE reads data row j straight from the value bytes at j*S (Split,
+// zero pad by masking) and writes data + parity rows; DECODE reads the k data
+// rows of an already completed data half (interpolate: the missing data rows
+// are regenerated first by gf_rows_kernel) and writes the parity positions by
+// class: 0 skip (used), 1 store (missing), 2 compare (valid but unused: store,
+// flag and queue for re-hash only if the re-encoding differs).
+#include <utility>
+
+#include "device_common.h"
+#include "kernels.h"
+
+using namespace rbcdev;
+
+namespace lch {
+
+constexpr uint32_t gmul(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+    for (int i = 0; i < 8; ++i) {
+        if (b & 1u) r ^= a;
+        b >>= 1;
+        a <<= 1;
+        if (a & 0x100u) a ^= 0x11du;
+    }
+    return r;
+}
+constexpr uint32_t ginv(uint32_t a) {
+    uint32_t r = 1, e = 254;  // a^254 = a^-1
+    while (e) {
+        if (e & 1u) r = gmul(r, a);
+        a = gmul(a, a);
+        e >>= 1;
+    }
+    return r;
+}
+// s_j(x): vanishing polynomial of V_j = span{1..2^(j-1)}; linearized, so
+// s_{j+1}(x) = s_j(x) * (s_j(x) + s_j(2^j)).
+constexpr uint32_t s_eval(int j, uint32_t x) {
+    if (j == 0) return x;
+    const uint32_t a = s_eval(j - 1, x);
+    return gmul(a, a ^ s_eval(j - 1, 1u << (j - 1)));
+}
+// butterfly constant of layer j on coset lambda: W_j(lambda)
+constexpr uint32_t twiddle(int j, uint32_t lam) { return gmul(s_eval(j, lam), ginv(s_eval(j, 1u << j))); }
+
+struct Tab {
+    uint32_t t0lo, t0hi, t1lo, t1hi, t2;
+};
+constexpr Tab make_tab(uint32_t c) {
+    uint32_t m[8] = {};
+    m[0] = c;
+    for (int i = 1; i < 8; ++i) m[i] = gmul(m[i - 1], 2);
+    Tab t{};
+    t.t0lo = (m[0] << 8) | (m[1] << 16) | ((m[0] ^ m[1]) << 24);
+    t.t0hi = m[2] | ((m[2] ^ m[0]) << 8) | ((m[2] ^ m[1]) << 16) | ((m[2] ^ m[1] ^ m[0]) << 24);
+    t.t1lo = (m[3] << 8) | (m[4] << 16) | ((m[3] ^ m[4]) << 24);
+    t.t1hi = m[5] | ((m[5] ^ m[3]) << 8) | ((m[5] ^ m[4]) << 16) | ((m[5] ^ m[4] ^ m[3]) << 24);
+    t.t2 = (m[6] << 8) | (m[7] << 16) | ((m[6] ^ m[7]) << 24);
+    return t;
+}
+
+// a + C*x for 4 packed bytes (C compile-time)
+template <uint32_t C>
+RBC_DEV uint32_t mac(uint32_t a, uint32_t x) {
+    if constexpr (C == 0) {
+        return a;
+    } else if constexpr (C == 1) {
+        return a ^ x;
+    } else {
+        constexpr Tab t = make_tab(C);
+        const uint32_t p0 = perm(t.t0hi, t.t0lo, x & 0x07070707u);
+        const uint32_t p1 = perm(t.t1hi, t.t1lo, (x >> 3) & 0x07070707u);
+        const uint32_t p2 = perm(t.t2, t.t2, (x >> 6) & 0x03030303u);
+        return xor3(a, p0, p1) ^ p2;
+    }
+}
+
+template <int B, int E, class F>
+RBC_DEV void sfor(F &&f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        sfor<B + 1, E>(f);
+    }
+}
+
+constexpr int cmin(int a, int b) { return a < b ? a : b; }
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
+// Evaluations on coset LAM + V_M of the polynomial whose novel coefficients are
+// v[OFF .. OFF+2^M) (rows >= NZ are zero and never read).  Only the outputs
+// with local index in [LO, HI) are produced, each handed to st(pos, value).
+template <int M, int LAM, int OFF, int NZ, int LO, int HI, int R, class ST>
+RBC_DEV void fft(uint32_t (&v)[R], ST &st) {
+    if constexpr (LO >= HI) {
+        return;
+    } else if constexpr (M == 0) {
+        st(std::integral_constant<int, LAM>{}, NZ > 0 ? v[OFF] : 0u);
+    } else {
+        constexpr int H = 1 << (M - 1);
+        constexpr uint32_t w = twiddle(M - 1, LAM);
+        constexpr int NZA = cmin(NZ, H), NZB = cmax(NZ - H, 0);
+        constexpr bool needA = LO < H, needB = HI > H;
+        sfor<0, H>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            if constexpr (i < NZB) {
+                const uint32_t a = v[OFF + i], b = v[OFF + H + i];
+                if constexpr (needA && needB) {
+                    const uint32_t a2 = mac<w>(a, b);
+                    v[OFF + i] = a2;
+                    v[OFF + H + i] = a2 ^ b;
+                } else if constexpr (needA) {
+                    v[OFF + i] = mac<w>(a, b);
+                } else {
+                    v[OFF + H + i] = mac<w ^ 1u>(a, b);  // a + (w+1) b
+                }
+            } else if constexpr (i < NZA && needB) {
+                v[OFF + H + i] = v[OFF + i];  // b == 0
+            }
+        });
+        if constexpr (needA) fft<M - 1, LAM, OFF, NZA, LO, cmin(HI, H)>(v, st);
+        if constexpr (needB) fft<M - 1, LAM + H, OFF + H, NZA, cmax(LO - H, 0), HI - H>(v, st);
+    }
+}
+
+// Inverse transform on coset LAM + V_M, in place (all 2^M rows known).
+template <int M, int LAM, int OFF, int R>
+RBC_DEV void ifft(uint32_t (&v)[R]) {
+    if constexpr (M > 0) {
+        constexpr int H = 1 << (M - 1);
+        ifft<M - 1, LAM, OFF>(v);
+        ifft<M - 1, LAM + H, OFF + H>(v);
+        constexpr uint32_t w = twiddle(M - 1, LAM);
+        sfor<0, H>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            const uint32_t b = v[OFF + i] ^ v[OFF + H + i];
+            v[OFF + H + i] = b;
+            v[OFF + i] = mac<w>(v[OFF + i], b);
+        });
+    }
+}
+
+// Rows v[OFF .. OFF+T) hold the evaluations at the first T points of
+// LAM + V_M of a polynomial with novel-coefficient support [0, T); on return
+// they hold those coefficients (rows [T, 2^M) are zero by construction).
+template <int M, int LAM, int OFF, int T, int R>
+RBC_DEV void solve(uint32_t (&v)[R]) {
+    constexpr int SZ = 1 << M;
+    if constexpr (T == SZ) {
+        ifft<M, LAM, OFF>(v);
+    } else if constexpr (T <= SZ / 2) {
+        solve<M - 1, LAM, OFF, T>(v);
+    } else {
+        constexpr int H = SZ / 2, TP = T - H;
+        constexpr uint32_t w = twiddle(M - 1, LAM);
+        ifft<M - 1, LAM, OFF>(v);  // g = P0 + w P1
+        // d = vals[H..T) - FFT_{LAM+H}(g)[0..TP) = FFT_{LAM+H}(P1)[0..TP)
+        uint32_t g[H];
+        sfor<0, H>([&](auto I) { g[decltype(I)::value] = v[OFF + decltype(I)::value]; });
+        auto sub = [&](auto P, uint32_t x) {
+            constexpr int p = decltype(P)::value - (LAM + H);
+            v[OFF + H + p] ^= x;
+        };
+        fft<M - 1, LAM + H, 0, H, 0, TP>(g, sub);
+        solve<M - 1, LAM + H, OFF + H, TP>(v);  // P1
+        sfor<0, TP>([&](auto I) {              // P0 = g + w P1
+            constexpr int i = decltype(I)::value;
+            v[OFF + i] = mac<w>(v[OFF + i], v[OFF + H + i]);
+        });
+    }
+}
+
+}  // namespace lch
+
+namespace {
+
+RBC_DEV uint32_t keep_bytes4(int nv) { return nv >= 4 ? 0xffffffffu : (nv <= 0 ? 0u : ((1u << (8 * nv)) - 1u)); }
+
+template <int LOGW, int K, int N>
+__global__ __launch_bounds__(64) void rs_fft_kernel(FftArgs a) {
+    constexpr int W = 1 << LOGW;
+    static_assert(K >= 1 && K <= N && N <= W && 2 * N > W, "geometry");
+    const int col = blockIdx.x * 64 + threadIdx.x;  // dword column inside the row
+    const int inst = blockIdx.y;
+    if (inst >= a.count) return;
+    if (a.status && a.status[inst] != 0) return;
+    const uint32_t off = 4u * (uint32_t)col;
+    if (off >= a.row_pitch) return;
+    uint32_t S, B = 0;
+    if (a.mode == GF_MODE_ENCODE) {
+        B = a.lens ? a.lens[inst] : a.uniform_len;
+        S = (B + K - 1) / K;
+    } else {
+        S = a.lens ? a.lens[inst] : a.uniform_len;
+    }
+    const uint32_t keep = keep_bytes4((int)S - (int)off);  // bytes past S are zero
+    uint8_t *shards = a.shards + (size_t)inst * a.inst_pitch;
+
+    uint32_t v[W];
+    if (a.mode == GF_MODE_ENCODE) {
+        const uint8_t *val = a.values + (size_t)inst * a.value_pitch;
+        const auto rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(val), (short)0, (int)a.value_pitch,
+                                                           0x00020000);
+        lch::sfor<0, K>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            const uint32_t row0 = (uint32_t)j * S;  // Split: data[j*S : (j+1)*S], zero pad
+            const int lim = (int)min(S, B > row0 ? B - row0 : 0u);
+            uint32_t x = 0;
+            if ((int)off < lim) {
+                x = __builtin_amdgcn_raw_buffer_load_b32(rv, (int)(row0 + off), 0, 0);  // unaligned ok (gfx950)
+                x &= keep_bytes4(lim - (int)off);
+            }
+            v[j] = x;
+            *reinterpret_cast<uint32_t *>(shards + (size_t)j * a.row_pitch + off) = x;
+        });
+    } else {
+        lch::sfor<0, K>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            v[j] = *reinterpret_cast<const uint32_t *>(shards + (size_t)j * a.row_pitch + off);
+        });
+    }
+
+    lch::solve<LOGW, 0, 0, K>(v);
+
+    const uint32_t *cls = a.cls ? reinterpret_cast<const uint32_t *>(a.cls + (size_t)inst * a.cls_stride) : nullptr;
+    auto st = [&](auto P, uint32_t x) {
+        constexpr int pos = decltype(P)::value;
+        if constexpr (pos >= K && pos < N) {
+            x &= keep;
+            uint32_t *dst = reinterpret_cast<uint32_t *>(shards + (size_t)pos * a.row_pitch + off);
+            if (!cls) {
+                *dst = x;
+            } else {
+                const uint32_t c = (cls[pos >> 2] >> (8 * (pos & 3))) & 0xffu;  // wave-uniform
+                if (c == 1u) {
+                    *dst = x;
+                } else if (c == 2u) {
+                    if (*dst != x) {
+                        *dst = x;
+                        if (atomicOr(&a.flags[(size_t)inst * N + pos], 1u) == 0u)
+                            a.list[atomicAdd(a.counter, 1u)] = ((uint32_t)inst << 8) | (uint32_t)pos;
+                    }
+                }
+            }
+        }
+    };
+    lch::fft<LOGW, 0, 0, K, K, N>(v, st);
+}
+
+template <int LOGW, int K, int N>
+hipError_t launch_fft(const FftArgs &a, hipStream_t st) {
+    dim3 grid((a.row_pitch / 4 + 63) / 64, (unsigned)a.count);
+    hipLaunchKernelGGL((rs_fft_kernel<LOGW, K, N>), grid, dim3(64), 0, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+// Geometries with a specialised transform: N = 3f+1 (the BFT maximum f) for
+// the benchmark sizes.  Other (N, k) fall back to gf_rows_kernel.
+#define RBC_FFT_GEOMS(X) \
+    X(2, 2, 4)           \
+    X(4, 6, 16)          \
+    X(6, 22, 64)         \
+    X(7, 44, 128)        \
+    X(8, 86, 256)
+
+bool rbc_fft_supported(int n, int k) {
+#define RBC_FFT_SUP(lw, kk, nn) \
+    if (n == nn && k == kk) return true;
+    RBC_FFT_GEOMS(RBC_FFT_SUP)
+#undef RBC_FFT_SUP
+    return false;
+}
+
+hipError_t rbc_launch_rs_fft(const FftArgs &a, hipStream_t st) {
+    if (a.count <= 0) return hipSuccess;
+    if (a.row_pitch % 4) return hipErrorInvalidValue;
+#define RBC_FFT_CASE(lw, kk, nn) \
+    if (a.n == nn && a.k == kk) return launch_fft<lw, kk, nn>(a, st);
+    RBC_FFT_GEOMS(RBC_FFT_CASE)
+#undef RBC_FFT_CASE
+    return hipErrorInvalidValue;
+}

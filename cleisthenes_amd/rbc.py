@@ -159,6 +159,18 @@ class Context:
     def handle(self) -> c_void_p:
         return self._p
 
+    CODEC_AUTO, CODEC_MATRIX, CODEC_FFT = 0, 1, 2
+
+    @property
+    def codec(self) -> str:
+        """Effective GF(2^8) codec: "fft" (additive FFT) or "matrix"."""
+        c = c_int()
+        check(lib.rbc_ctx_codec(self._p, byref(c)))
+        return "fft" if c.value == self.CODEC_FFT else "matrix"
+
+    def set_codec(self, codec: str) -> None:
+        check(lib.rbc_ctx_set_codec(self._p, {"auto": 0, "matrix": 1, "fft": 2}[codec]), "rbc_ctx_set_codec")
+
     def encode_matrix(self) -> np.ndarray:
         m = np.zeros(self.n * self.k, dtype=np.uint8)
         check(lib.rbc_ctx_encode_matrix(self._p, _ptr(m)))

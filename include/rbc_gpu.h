@@ -73,6 +73,15 @@ void rbc_ctx_destroy(rbc_ctx *ctx);
 int rbc_ctx_params(const rbc_ctx *ctx, int *k, int *p, int *depth);
 /* klauspost buildMatrix(k, n) as used by this context: n*k bytes, row-major */
 int rbc_ctx_encode_matrix(const rbc_ctx *ctx, uint8_t *out);
+/* GF(2^8) codec behind encode / interpolate (same bytes either way):
+ * RBC_CODEC_AUTO = additive FFT where this build has a specialised transform
+ * for (n, k) (rbc_ctx_codec reports it), else the matrix kernel;
+ * RBC_CODEC_MATRIX forces klauspost's encode-matrix product on the GPU. */
+#define RBC_CODEC_AUTO 0
+#define RBC_CODEC_MATRIX 1
+#define RBC_CODEC_FFT 2
+int rbc_ctx_set_codec(rbc_ctx *ctx, int codec);
+int rbc_ctx_codec(const rbc_ctx *ctx, int *codec); /* effective: MATRIX or FFT */
 
 /* ---- device memory / streams / events (so a host runtime needs no other
  *      GPU library to drive the rbc_dev_* path) ---------------------------- */

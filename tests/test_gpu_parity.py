@@ -184,9 +184,10 @@ def test_host_batch_ragged_lengths(gpu, ref):
 class Pipeline:
     """Device buffers + the bench's step for `I` instances of (n, f, B)."""
 
-    def __init__(self, gpu, n, f, B, I, seed, corrupt_frac=0.1, present_n=None):
+    def __init__(self, gpu, n, f, B, I, seed, corrupt_frac=0.1, present_n=None, codec="auto"):
         self.ca = gpu
         self.ctx = gpu.Context(n, f)
+        self.ctx.set_codec(codec)
         self.n, self.f, self.B, self.I = n, f, B, I
         k = self.ctx.k
         self.k = k
@@ -421,3 +422,81 @@ def test_batcher_coalesces_concurrent_requests(gpu, ref):
     assert requests == len(values) * (2 + n)
     assert batches < requests / 4, (batches, requests)  # actually coalesced
     bt.close()
+
+
+# ------------------------------------------- FFT codec vs matrix codec
+
+
+FFT_GEOMS = [(4, 1, 1000, 8), (16, 5, 4099, 8), (64, 21, 1 << 20, 4), (128, 42, 1 << 20, 6),
+             (256, 85, 64 << 10, 16)]
+
+
+@pytest.mark.parametrize("n,f,B,I", FFT_GEOMS, ids=[f"n{g[0]}" for g in FFT_GEOMS])
+def test_fft_codec_matches_matrix_codec(gpu, n, f, B, I):
+    """The additive-FFT codec (rs_fft.hip) and the klauspost encode-matrix
+    kernel produce identical shards, statuses, values, digests and re-hash
+    lists on the same inputs, across erasure classes: random N-f present,
+    parity only, data only, exactly k, plus corrupted ECHO shards."""
+    outs = {}
+    for codec in ("matrix", "fft"):
+        pl = Pipeline(gpu, n, f, B, I, seed=n * 7 + B, corrupt_frac=0.3, codec=codec)
+        assert pl.ctx.codec == codec
+        k = pl.k
+        for i in range(I):  # erasure classes on the first instances
+            if i % 4 == 1:
+                pl.present[i] = 0
+                pl.present[i, k:] = 1            # parity only (n-k >= k here)
+                if n - k < k:
+                    pl.present[i, :k - (n - k)] = 1
+            elif i % 4 == 2:
+                pl.present[i] = 0
+                pl.present[i, :k] = 1            # data only
+                pl.corrupt[i] = -1
+            elif i % 4 == 3:
+                pl.present[i] = 0
+                pl.present[i, np.random.default_rng(i).permutation(n)[:k]] = 1
+                pl.corrupt[i] = -1
+        pl.b["present"].upload(pl.present)
+        pl.b["corrupt"].upload(pl.corrupt)
+        pl.commit()
+        enc_shards = pl.shards().copy()
+        pl.receive()
+        outs[codec] = dict(enc=enc_shards, dec=pl.shards(), status=pl.arr("status", np.int32).copy(),
+                           out=pl.arr("out", shape=(I, pl.opitch)).copy(),
+                           digests=pl.arr("digests", shape=(I, 32)).copy(), values=pl.values, B=B)
+    a, b = outs["matrix"], outs["fft"]
+    assert np.array_equal(a["enc"], b["enc"])
+    assert np.array_equal(a["status"], b["status"])
+    ok = a["status"] == 0
+    assert np.array_equal(a["out"][ok], b["out"][ok])
+    assert np.array_equal(a["digests"][ok], b["digests"][ok])
+    for i in np.nonzero(ok)[0]:
+        assert b["out"][i, :B].tobytes() == b["values"][i, :B].tobytes()
+    # the full regenerated codeword is the encoding (both codecs, in place)
+    assert np.array_equal(a["dec"][ok], a["enc"][ok])
+    assert np.array_equal(b["dec"][ok], b["enc"][ok])
+
+
+def test_fft_codec_rejects_noncodeword(gpu):
+    """Byzantine proposer commits to a non-codeword: the FFT codec's compare
+    path must catch it (ROOT_MISMATCH) whatever subset is decoded."""
+    n, f, B, I = 128, 42, 44 * 640, 8
+    pl = Pipeline(gpu, n, f, B, I, seed=11, corrupt_frac=0.0, codec="fft")
+    c, b = pl.ctx, pl.b
+    c.dev_encode(None, I, b["values"], pl.vpitch, None, B, b["shards"], pl.spitch)
+    sh = pl.shards().copy()
+    sh[:, 100, 5] ^= 0x21                       # parity row no longer a codeword row
+    b["shards"].upload(sh)
+    c.dev_leaves(None, I, b["shards"], pl.spitch, None, pl.S, b["leaves"])
+    c.dev_merkle_build(None, I, b["leaves"], b["roots"], b["branches"])
+    rng = np.random.default_rng(1)
+    for i in range(I):
+        pl.present[i] = 0
+        pl.present[i, rng.permutation(n)[: n - f]] = 1
+        pl.present[i, 100] = 1 if i % 2 else 0   # tampered row present (valid) or absent
+    b["present"].upload(pl.present)
+    c.dev_verify(None, I, b["shards"], pl.spitch, None, pl.S, b["branches"], b["roots"], b["present"],
+                 b["valid"], b["leaves_r"])
+    c.dev_interpolate(None, I, b["shards"], pl.spitch, None, pl.S, b["valid"], b["leaves_r"], 1, b["roots"],
+                      b["out"], pl.opitch, b["digests"], b["status"])
+    assert (pl.arr("status", np.int32) == -8).all()
