@@ -109,15 +109,48 @@ RBC_DEV void sfor(F &&f) {
 constexpr int cmin(int a, int b) { return a < b ? a : b; }
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
+template <int V>
+using IC = std::integral_constant<int, V>;
+
+// All 2^M evaluations on coset LAM + V_M, in place, of the polynomial whose
+// novel coefficients are v[OFF .. OFF+2^M) (rows >= NZ are zero, never read).
+template <int M, int LAM, int OFF, int NZ, int R>
+RBC_DEV void fft_full(uint32_t (&v)[R]) {
+    if constexpr (NZ <= 0) {
+        sfor<0, (1 << M)>([&](auto I) { v[OFF + decltype(I)::value] = 0u; });
+    } else if constexpr (M > 0) {
+        constexpr int H = 1 << (M - 1);
+        constexpr uint32_t w = twiddle(M - 1, LAM);
+        constexpr int NZA = cmin(NZ, H), NZB = cmax(NZ - H, 0);
+        sfor<0, H>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            if constexpr (i < NZB) {
+                const uint32_t a = v[OFF + i], b = v[OFF + H + i];
+                const uint32_t a2 = mac<w>(a, b);
+                v[OFF + i] = a2;
+                v[OFF + H + i] = a2 ^ b;
+            } else if constexpr (i < NZA) {
+                v[OFF + H + i] = v[OFF + i];  // b == 0
+            }
+        });
+        fft_full<M - 1, LAM, OFF, NZA>(v);
+        fft_full<M - 1, LAM + H, OFF + H, NZA>(v);
+    }
+}
+
 // Evaluations on coset LAM + V_M of the polynomial whose novel coefficients are
 // v[OFF .. OFF+2^M) (rows >= NZ are zero and never read).  Only the outputs
-// with local index in [LO, HI) are produced, each handed to st(pos, value).
-template <int M, int LAM, int OFF, int NZ, int LO, int HI, int R, class ST>
+// with local index in [LO, HI) are needed.  Sub-transforms of size 2^G are
+// completed in place and handed over as a group, st(IC<lam>, IC<off>, IC<lo>,
+// IC<hi>): outputs v[off + lo .. off + hi) are the evaluations at lam + i --
+// so a sink can batch its memory traffic per group.
+template <int G, int M, int LAM, int OFF, int NZ, int LO, int HI, int R, class ST>
 RBC_DEV void fft(uint32_t (&v)[R], ST &st) {
     if constexpr (LO >= HI) {
         return;
-    } else if constexpr (M == 0) {
-        st(std::integral_constant<int, LAM>{}, NZ > 0 ? v[OFF] : 0u);
+    } else if constexpr (M <= G) {
+        fft_full<M, LAM, OFF, NZ>(v);
+        st(IC<LAM>{}, IC<OFF>{}, IC<LO>{}, IC<HI>{});
     } else {
         constexpr int H = 1 << (M - 1);
         constexpr uint32_t w = twiddle(M - 1, LAM);
@@ -140,8 +173,8 @@ RBC_DEV void fft(uint32_t (&v)[R], ST &st) {
                 v[OFF + H + i] = v[OFF + i];  // b == 0
             }
         });
-        if constexpr (needA) fft<M - 1, LAM, OFF, NZA, LO, cmin(HI, H)>(v, st);
-        if constexpr (needB) fft<M - 1, LAM + H, OFF + H, NZA, cmax(LO - H, 0), HI - H>(v, st);
+        if constexpr (needA) fft<G, M - 1, LAM, OFF, NZA, LO, cmin(HI, H)>(v, st);
+        if constexpr (needB) fft<G, M - 1, LAM + H, OFF + H, NZA, cmax(LO - H, 0), HI - H>(v, st);
     }
 }
 
@@ -179,11 +212,13 @@ RBC_DEV void solve(uint32_t (&v)[R]) {
         // d = vals[H..T) - FFT_{LAM+H}(g)[0..TP) = FFT_{LAM+H}(P1)[0..TP)
         uint32_t g[H];
         sfor<0, H>([&](auto I) { g[decltype(I)::value] = v[OFF + decltype(I)::value]; });
-        auto sub = [&](auto P, uint32_t x) {
-            constexpr int p = decltype(P)::value - (LAM + H);
-            v[OFF + H + p] ^= x;
+        auto sub = [&](auto Lam, auto Off, auto Lo, auto Hi) {
+            sfor<decltype(Lo)::value, decltype(Hi)::value>([&](auto I) {
+                constexpr int i = decltype(I)::value;
+                v[OFF + H + decltype(Lam)::value - (LAM + H) + i] ^= g[decltype(Off)::value + i];
+            });
         };
-        fft<M - 1, LAM + H, 0, H, 0, TP>(g, sub);
+        fft<0, M - 1, LAM + H, 0, H, 0, TP>(g, sub);
         solve<M - 1, LAM + H, OFF + H, TP>(v);  // P1
         sfor<0, TP>([&](auto I) {              // P0 = g + w P1
             constexpr int i = decltype(I)::value;
@@ -198,9 +233,10 @@ namespace {
 
 RBC_DEV uint32_t keep_bytes4(int nv) { return nv >= 4 ? 0xffffffffu : (nv <= 0 ? 0u : ((1u << (8 * nv)) - 1u)); }
 
-template <int LOGW, int K, int N>
+template <int LOGW, int K, int N, int MODE>
 __global__ __launch_bounds__(64) void rs_fft_kernel(FftArgs a) {
     constexpr int W = 1 << LOGW;
+    constexpr int G = 3;  // outputs are stored in groups of 2^G rows
     static_assert(K >= 1 && K <= N && N <= W && 2 * N > W, "geometry");
     const int col = blockIdx.x * 64 + threadIdx.x;  // dword column inside the row
     const int inst = blockIdx.y;
@@ -209,70 +245,94 @@ __global__ __launch_bounds__(64) void rs_fft_kernel(FftArgs a) {
     const uint32_t off = 4u * (uint32_t)col;
     if (off >= a.row_pitch) return;
     uint32_t S, B = 0;
-    if (a.mode == GF_MODE_ENCODE) {
+    if constexpr (MODE == GF_MODE_ENCODE) {
         B = a.lens ? a.lens[inst] : a.uniform_len;
         S = (B + K - 1) / K;
     } else {
         S = a.lens ? a.lens[inst] : a.uniform_len;
     }
     const uint32_t keep = keep_bytes4((int)S - (int)off);  // bytes past S are zero
+    // every row access is base(SGPR) + off(one VGPR) + row*pitch(SGPR): one
+    // VGPR of addressing for all N rows instead of a 64-bit pointer per row
     uint8_t *shards = a.shards + (size_t)inst * a.inst_pitch;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(shards, (short)0, (int)a.inst_pitch, 0x00020000);
+    const int pitch = (int)a.row_pitch;
+    auto row_store = [&](int pos, uint32_t x) { __builtin_amdgcn_raw_buffer_store_b32(x, rs, (int)off, pos * pitch, 0); };
+    auto row_load = [&](int pos) -> uint32_t { return __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, pos * pitch, 0); };
 
     uint32_t v[W];
-    if (a.mode == GF_MODE_ENCODE) {
+    if constexpr (MODE == GF_MODE_ENCODE) {
         const uint8_t *val = a.values + (size_t)inst * a.value_pitch;
         const auto rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(val), (short)0, (int)a.value_pitch,
                                                            0x00020000);
+        // all K loads issued back to back, unconditionally (out-of-range
+        // reads return 0 through the buffer descriptor); the Split zero pad
+        // is applied by masking afterwards.  Unaligned dword reads are fine
+        // on gfx950.
         lch::sfor<0, K>([&](auto J) {
             constexpr int j = decltype(J)::value;
-            const uint32_t row0 = (uint32_t)j * S;  // Split: data[j*S : (j+1)*S], zero pad
+            v[j] = __builtin_amdgcn_raw_buffer_load_b32(rv, (int)off, (int)((uint32_t)j * S), 0);
+        });
+        lch::sfor<0, K>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            const uint32_t row0 = (uint32_t)j * S;  // Split: data[j*S : (j+1)*S]
             const int lim = (int)min(S, B > row0 ? B - row0 : 0u);
-            uint32_t x = 0;
-            if ((int)off < lim) {
-                x = __builtin_amdgcn_raw_buffer_load_b32(rv, (int)(row0 + off), 0, 0);  // unaligned ok (gfx950)
-                x &= keep_bytes4(lim - (int)off);
-            }
-            v[j] = x;
-            *reinterpret_cast<uint32_t *>(shards + (size_t)j * a.row_pitch + off) = x;
+            v[j] &= keep_bytes4(lim - (int)off);
+            row_store(j, v[j]);
         });
     } else {
-        lch::sfor<0, K>([&](auto J) {
-            constexpr int j = decltype(J)::value;
-            v[j] = *reinterpret_cast<const uint32_t *>(shards + (size_t)j * a.row_pitch + off);
-        });
+        lch::sfor<0, K>([&](auto J) { v[decltype(J)::value] = row_load(decltype(J)::value); });
     }
 
     lch::solve<LOGW, 0, 0, K>(v);
 
-    const uint32_t *cls = a.cls ? reinterpret_cast<const uint32_t *>(a.cls + (size_t)inst * a.cls_stride) : nullptr;
-    auto st = [&](auto P, uint32_t x) {
-        constexpr int pos = decltype(P)::value;
-        if constexpr (pos >= K && pos < N) {
-            x &= keep;
-            uint32_t *dst = reinterpret_cast<uint32_t *>(shards + (size_t)pos * a.row_pitch + off);
-            if (!cls) {
-                *dst = x;
-            } else {
-                const uint32_t c = (cls[pos >> 2] >> (8 * (pos & 3))) & 0xffu;  // wave-uniform
-                if (c == 1u) {
-                    *dst = x;
-                } else if (c == 2u) {
-                    if (*dst != x) {
-                        *dst = x;
-                        if (atomicOr(&a.flags[(size_t)inst * N + pos], 1u) == 0u)
+    if constexpr (MODE == GF_MODE_ENCODE) {
+        auto st = [&](auto Lam, auto Off, auto Lo, auto Hi) {
+            lch::sfor<decltype(Lo)::value, decltype(Hi)::value>([&](auto I) {
+                constexpr int i = decltype(I)::value, pos = decltype(Lam)::value + i;
+                if constexpr (pos >= K && pos < N) row_store(pos, v[decltype(Off)::value + i] & keep);
+            });
+        };
+        lch::fft<G, LOGW, 0, 0, K, K, N>(v, st);
+    } else {
+        const uint32_t *cls = reinterpret_cast<const uint32_t *>(a.cls + (size_t)inst * a.cls_stride);
+        auto st = [&](auto Lam, auto Off, auto Lo, auto Hi) {
+            constexpr int lam = decltype(Lam)::value, o = decltype(Off)::value;
+            constexpr int lo = lch::cmax(decltype(Lo)::value, K - lam), hi = lch::cmin(decltype(Hi)::value, N - lam);
+            if constexpr (lo < hi) {
+                uint32_t c[hi - lo], old[hi - lo];
+                // phase 1: class lookups + the compare loads of the whole group
+                lch::sfor<lo, hi>([&](auto I) {
+                    constexpr int i = decltype(I)::value, pos = lam + i;
+                    c[i - lo] = (cls[pos >> 2] >> (8 * (pos & 3))) & 0xffu;  // wave-uniform
+                    old[i - lo] = 0;
+                    if (c[i - lo] == 2u) old[i - lo] = row_load(pos);
+                });
+                // phase 2: store missing rows; store + flag mismatching compare rows
+                lch::sfor<lo, hi>([&](auto I) {
+                    constexpr int i = decltype(I)::value, pos = lam + i;
+                    const uint32_t x = v[o + i] & keep;
+                    if (c[i - lo] == 1u) {
+                        row_store(pos, x);
+                    } else if (c[i - lo] == 2u && old[i - lo] != x) {
+                        row_store(pos, x);
+                        if (a.flags && atomicOr(&a.flags[(size_t)inst * N + pos], 1u) == 0u)
                             a.list[atomicAdd(a.counter, 1u)] = ((uint32_t)inst << 8) | (uint32_t)pos;
                     }
-                }
+                });
             }
-        }
-    };
-    lch::fft<LOGW, 0, 0, K, K, N>(v, st);
+        };
+        lch::fft<G, LOGW, 0, 0, K, K, N>(v, st);
+    }
 }
 
 template <int LOGW, int K, int N>
 hipError_t launch_fft(const FftArgs &a, hipStream_t st) {
     dim3 grid((a.row_pitch / 4 + 63) / 64, (unsigned)a.count);
-    hipLaunchKernelGGL((rs_fft_kernel<LOGW, K, N>), grid, dim3(64), 0, st, a);
+    if (a.mode == GF_MODE_ENCODE)
+        hipLaunchKernelGGL((rs_fft_kernel<LOGW, K, N, GF_MODE_ENCODE>), grid, dim3(64), 0, st, a);
+    else
+        hipLaunchKernelGGL((rs_fft_kernel<LOGW, K, N, GF_MODE_DECODE>), grid, dim3(64), 0, st, a);
     return hipGetLastError();
 }
 
