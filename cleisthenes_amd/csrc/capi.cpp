@@ -43,6 +43,16 @@ int codec_default() {
     return v;
 }
 
+// rows per chunk for the FFT codec's missing-data GF pass (RBC_GF_MDRC)
+int gf_md_rcmax() {
+    static const int v = [] {
+        const char *e = getenv("RBC_GF_MDRC");
+        int x = e ? atoi(e) : 0;
+        return (x >= 1 && x <= 48) ? x : 8;
+    }();
+    return v;
+}
+
 int tree_width(int n) {
     int w = 1;
     while (w < n) w <<= 1;
@@ -132,8 +142,15 @@ int ctx_create_kn(int n, int k, int device, rbc_ctx **out) {
     c->device = device;
     c->fft = codec_default() != RBC_CODEC_MATRIX && rbc_fft_supported(n, k);
     if (!rbchost::build_matrix(k, n, c->h_M)) { delete c; return RBC_ERR_SINGULAR; }
-    if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->d_M, c->h_M.size()) != hipSuccess ||
-        hipMemcpy(c->d_M, c->h_M.data(), c->h_M.size(), hipMemcpyHostToDevice) != hipSuccess ||
+    // d_M = [n x k encode matrix | exp[512] | log[256]] (tables for decode_prepare_fft)
+    std::vector<uint8_t> up(c->h_M);
+    {
+        const rbchost::Gf g;
+        up.insert(up.end(), g.exp, g.exp + 512);
+        up.insert(up.end(), g.log, g.log + 256);
+    }
+    if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->d_M, up.size()) != hipSuccess ||
+        hipMemcpy(c->d_M, up.data(), up.size(), hipMemcpyHostToDevice) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
@@ -317,6 +334,8 @@ int stage_regenerate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, uin
         pa.rcount = c->ws_rcount.as<int32_t>();
         pa.cls = c->ws_cls.as<uint8_t>();
         pa.cls_stride = (uint32_t)round_up(c->n, 4);
+        pa.gf_exp = c->d_M + c->h_M.size();
+        pa.gf_log = pa.gf_exp + 512;
     }
     RBC_HIP(rbc_launch_decode_prepare(pa, st));
     if (c->fft && nr > 0) {
@@ -327,7 +346,7 @@ int stage_regenerate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, uin
         g.tiles = (int)((shard_pitch + 4095) / 4096);
         g.R = rmax;
         g.K = c->k;
-        g.rc = rbc_gf_pick_rc(rmax, gf_rcmax());
+        g.rc = rbc_gf_pick_rc(rmax, gf_md_rcmax());
         g.mode = GF_MODE_DECODE;
         g.in = shards;
         g.in_inst_pitch = (uint64_t)c->n * shard_pitch;

@@ -15,6 +15,8 @@
 //   branches [I][N][d][32]               level-0 slot zero when sibling empty
 //   valid    [I][N] u8 ; status [I] i32 ; digests [I][32]
 // No MFMA: GF(2^8) and SHA-256 are not dense contractions (north_star).
+#include <algorithm>
+
 #include "device_common.h"
 #include "kernels.h"
 
@@ -449,21 +451,6 @@ __global__ __launch_bounds__(256) void decode_prepare_kernel(PrepArgs a) {
         int nr = nm;
         for (int j = 0, seen = 0; j < n; ++j)
             if (v[j] && seen++ >= k) s_regen[nr++] = (uint8_t)j;
-        if (a.fft) {
-            // FFT codec: only the missing DATA rows go through D (they lead
-            // regen: missing positions are listed in index order); parity
-            // positions are re-encoded by rs_fft_kernel, by class
-            int md = 0;
-            while (md < nm && s_regen[md] < k) ++md;
-            nr = md;
-            if (a.rcount) a.rcount[inst] = md;
-            uint8_t *cl = a.cls + (size_t)inst * a.cls_stride;
-            for (int j = 0, seen = 0; j < n; ++j) {
-                const bool used = v[j] && seen < k;
-                seen += v[j] ? 1 : 0;
-                cl[j] = (j < k || used) ? 0 : (!v[j] ? 1 : (a.counter ? 2 : 1));
-            }
-        }
         s_misc[0] = nu;
         s_misc[1] = nr;
         s_misc[2] = (a.counter && nu >= k) ? (int)atomicAdd(a.counter, (unsigned)nm) : 0;
@@ -564,6 +551,132 @@ __global__ __launch_bounds__(256) void decode_prepare_kernel(PrepArgs a) {
             for (int i = 0; i < k; ++i) acc ^= gmul(mrow[i], A[i * k2 + k + c]);
             D[e] = (uint8_t)acc;
         }
+    }
+    if (tid == 0) a.status[inst] = 0;
+}
+
+// ============================================================================
+// decode_prepare_fft: the FFT codec's interpolate plan.  With U = the first k
+// valid positions (klauspost's Reconstruct rule) = every present data row D_p
+// plus the first m valid parity rows P_u (m = #missing data rows D_m), only
+// the m x m block A = M[P_u][D_m] needs inverting:
+//   x_{D_m} = A^-1 (s_{P_u} + M[P_u][D_p] s_{D_p})            (char 2: - = +)
+// so D = [A^-1 M[P_u][D_p] | A^-1] over U in index order, an m x k matrix
+// (m^3 instead of klauspost's k^3 inversion; A is a square sub-matrix of the
+// parity part of a systematic MDS code, hence never singular).  Parity
+// positions are then re-encoded by rs_fft_kernel from the completed data
+// half; cls[pos] tells it what to do per position.
+// ============================================================================
+__global__ __launch_bounds__(256) void decode_prepare_fft_kernel(PrepArgs a, const uint8_t *exp_tab,
+                                                                  const uint8_t *log_tab) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int n = a.n, k = a.k;
+    uint8_t *s_exp = smem;           // 512
+    uint8_t *s_log = smem + 512;     // 256
+    uint8_t *s_used = smem + 768;    // 256: U in index order
+    uint8_t *s_miss = smem + 1024;   // 256: missing positions in index order
+    int *s_misc = reinterpret_cast<int *>(smem + 1280);  // 8 ints
+    uint8_t *s_fac = smem + 1312;    // 256: elimination factors of one pivot step
+    uint8_t *A = smem + 1568;        // m x 2m  [A | I] -> [I | A^-1]
+    const int inst = blockIdx.x, tid = threadIdx.x;
+    for (int t = tid; t < 512; t += 256) s_exp[t] = exp_tab[t];
+    s_log[tid] = log_tab[tid];
+    if (tid == 0) {
+        int nu = 0, nm = 0, md = 0;
+        const uint8_t *v = a.valid + (size_t)inst * a.valid_stride;
+        uint8_t *cl = a.cls + (size_t)inst * a.cls_stride;
+        for (int j = 0; j < n; ++j) {
+            const bool ok = v[j] != 0;
+            const bool used = ok && nu < k;
+            if (used) s_used[nu++] = (uint8_t)j;
+            if (!ok) {
+                s_miss[nm++] = (uint8_t)j;
+                md += j < k;
+            }
+            cl[j] = (j < k || used) ? 0 : (!ok ? 1 : (a.counter ? 2 : 1));
+        }
+        s_misc[0] = nu;
+        s_misc[1] = md;
+        s_misc[2] = (a.counter && nu >= k) ? (int)atomicAdd(a.counter, (unsigned)nm) : 0;
+        s_misc[3] = nm;
+        if (a.nmiss) a.nmiss[inst] = nm;
+        a.rcount[inst] = md;
+    }
+    __syncthreads();
+    const int nu = s_misc[0], m = s_misc[1];
+    if (nu < k) {
+        if (tid == 0) a.status[inst] = RBC_ERR_TOO_FEW_SHARDS;
+        return;
+    }
+    if (a.counter) {
+        const int base = s_misc[2], nm = s_misc[3];
+        for (int t = tid; t < nm; t += 256) a.list[base + t] = ((uint32_t)inst << 8) | s_miss[t];
+        for (int t = tid; t < n; t += 256) a.flags[(size_t)inst * n + t] = 0;
+    }
+    for (int t = tid; t < k; t += 256) a.used[(size_t)inst * a.used_stride + t] = s_used[t];
+    for (int t = tid; t < m; t += 256) a.regen[(size_t)inst * a.regen_stride + t] = s_miss[t];
+    if (m == 0) {
+        if (tid == 0) a.status[inst] = 0;
+        return;
+    }
+    auto gmul = [&](uint32_t x, uint32_t y) -> uint32_t {
+        return (x && y) ? (uint32_t)s_exp[s_log[x] + s_log[y]] : 0u;
+    };
+    const int m2 = 2 * m, kp = k - m;  // U = D_p (kp rows) then P_u (m rows)
+    for (int e = tid; e < m * m2; e += 256) {
+        const int r = e / m2, c = e - r * m2;
+        A[e] = c < m ? a.M[(size_t)s_used[kp + r] * k + s_miss[c]] : (uint8_t)((c - m) == r);
+    }
+    __syncthreads();
+    for (int col = 0; col < m; ++col) {
+        if (tid == 0) {
+            int piv = col;
+            if (A[col * m2 + col] == 0) {
+                piv = -1;
+                for (int b = col + 1; b < m; ++b)
+                    if (A[b * m2 + col]) { piv = b; break; }
+            }
+            s_misc[4] = piv;
+        }
+        __syncthreads();
+        const int piv = s_misc[4];
+        if (piv < 0) {  // impossible for an MDS code; report, don't hang
+            if (tid == 0) a.status[inst] = RBC_ERR_SINGULAR;
+            return;
+        }
+        if (piv != col) {
+            for (int c = tid; c < m2; c += 256) {
+                const uint8_t x = A[col * m2 + c];
+                A[col * m2 + c] = A[piv * m2 + c];
+                A[piv * m2 + c] = x;
+            }
+            __syncthreads();
+        }
+        const uint32_t inv = s_exp[255 - s_log[A[col * m2 + col]]];
+        __syncthreads();
+        for (int c = tid; c < m2; c += 256) A[col * m2 + c] = (uint8_t)gmul(inv, A[col * m2 + c]);
+        for (int r = tid; r < m; r += 256) s_fac[r] = (r == col) ? 0 : A[r * m2 + col];
+        __syncthreads();
+        for (int e = tid; e < m * m2; e += 256) {
+            const int r = e / m2, c = e - r * m2;
+            const uint32_t f = s_fac[r];
+            if (f) A[e] ^= (uint8_t)gmul(f, A[col * m2 + c]);
+        }
+        __syncthreads();
+    }
+    // D[r][u]: u < kp -> sum_i Ainv[r][i] * M[P_u[i]][D_p[u]];  u >= kp -> Ainv[r][u-kp]
+    uint8_t *D = a.dmat + (size_t)inst * a.dmat_stride;
+    for (int e = tid; e < m * k; e += 256) {
+        const int r = e / k, u = e - r * k;
+        uint32_t acc;
+        if (u >= kp) {
+            acc = A[r * m2 + m + (u - kp)];
+        } else {
+            acc = 0;
+            const int dp = s_used[u];
+            for (int i = 0; i < m; ++i) acc ^= gmul(A[r * m2 + m + i], a.M[(size_t)s_used[kp + i] * k + dp]);
+        }
+        D[e] = (uint8_t)acc;
     }
     if (tid == 0) a.status[inst] = 0;
 }
@@ -699,6 +812,12 @@ hipError_t rbc_launch_digest(const uint8_t *leaves, uint64_t leaves_inst_pitch, 
 
 hipError_t rbc_launch_decode_prepare(const PrepArgs &a, hipStream_t st) {
     if (a.count <= 0) return hipSuccess;
+    if (a.fft) {
+        const int mmax = std::min(a.k, a.n - a.k);
+        const size_t lds = 1568 + (size_t)mmax * 2 * mmax;
+        hipLaunchKernelGGL(decode_prepare_fft_kernel, dim3(a.count), dim3(256), lds, st, a, a.gf_exp, a.gf_log);
+        return hipGetLastError();
+    }
     PrepArgs b = a;
     const size_t base = 1552 + (size_t)a.k * 2 * a.k;
     const size_t staged = base + (size_t)a.k * a.k + (size_t)(a.n - a.k) * a.k;

@@ -91,8 +91,16 @@ RBC_DEV uint32_t mac(uint32_t a, uint32_t x) {
         return a ^ x;
     } else {
         constexpr Tab t = make_tab(C);
-        const uint32_t p0 = perm(t.t0hi, t.t0lo, x & 0x07070707u);
-        const uint32_t p1 = perm(t.t1hi, t.t1lo, (x >> 3) & 0x07070707u);
+        // gfx950 VOP3 takes one scalar operand: one table half per lookup is
+        // materialised into a VGPR right here -- the asm nominally reads x, so
+        // it is never CSE'd into a long-lived register (which would cost
+        // occupancy) yet stays free to schedule; the other half and t2 ride
+        // in SGPRs
+        uint32_t lo0, lo1;
+        asm("v_mov_b32 %0, %2 ; %1" : "=v"(lo0) : "v"(x), "i"(t.t0lo));
+        asm("v_mov_b32 %0, %2 ; %1" : "=v"(lo1) : "v"(x), "i"(t.t1lo));
+        const uint32_t p0 = perm(t.t0hi, lo0, x & 0x07070707u);
+        const uint32_t p1 = perm(t.t1hi, lo1, (x >> 3) & 0x07070707u);
         const uint32_t p2 = perm(t.t2, t.t2, (x >> 6) & 0x03030303u);
         return xor3(a, p0, p1) ^ p2;
     }
@@ -111,6 +119,11 @@ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
 template <int V>
 using IC = std::integral_constant<int, V>;
+
+#ifndef RBC_FFT_SB
+#define RBC_FFT_SB 4
+#endif
+constexpr int SB = RBC_FFT_SB;  // sub-transforms of >= 2^SB rows are scheduled one after the other
 
 // All 2^M evaluations on coset LAM + V_M, in place, of the polynomial whose
 // novel coefficients are v[OFF .. OFF+2^M) (rows >= NZ are zero, never read).
@@ -174,6 +187,9 @@ RBC_DEV void fft(uint32_t (&v)[R], ST &st) {
             }
         });
         if constexpr (needA) fft<G, M - 1, LAM, OFF, NZA, LO, cmin(HI, H)>(v, st);
+        // keep the scheduler from interleaving the two independent halves
+        // (that would double the live rows and halve occupancy)
+        if constexpr (needA && needB && M >= SB) __builtin_amdgcn_sched_barrier(0);
         if constexpr (needB) fft<G, M - 1, LAM + H, OFF + H, NZA, cmax(LO - H, 0), HI - H>(v, st);
     }
 }
@@ -236,7 +252,11 @@ RBC_DEV uint32_t keep_bytes4(int nv) { return nv >= 4 ? 0xffffffffu : (nv <= 0 ?
 template <int LOGW, int K, int N, int MODE>
 __global__ __launch_bounds__(64) void rs_fft_kernel(FftArgs a) {
     constexpr int W = 1 << LOGW;
-    constexpr int G = 3;  // outputs are stored in groups of 2^G rows
+    constexpr int G = 3;   // encode: outputs are stored in groups of 2^G rows
+#ifndef RBC_FFT_GD
+#define RBC_FFT_GD 2
+#endif
+    constexpr int GD = RBC_FFT_GD;  // decode: compare-pipeline group (VGPRs: 1 -> 143, 2 -> 157, 3 -> 181)
     static_assert(K >= 1 && K <= N && N <= W && 2 * N > W, "geometry");
     const int col = blockIdx.x * 64 + threadIdx.x;  // dword column inside the row
     const int inst = blockIdx.y;
@@ -278,6 +298,10 @@ __global__ __launch_bounds__(64) void rs_fft_kernel(FftArgs a) {
             const uint32_t row0 = (uint32_t)j * S;  // Split: data[j*S : (j+1)*S]
             const int lim = (int)min(S, B > row0 ? B - row0 : 0u);
             v[j] &= keep_bytes4(lim - (int)off);
+            // materialise the masked row: otherwise the AND is folded into
+            // the first butterfly (v_bitop3) and the raw row plus its mask
+            // stay live through the transform (+44 VGPRs)
+            asm volatile("" : "+v"(v[j]));
             row_store(j, v[j]);
         });
     } else {
@@ -285,6 +309,10 @@ __global__ __launch_bounds__(64) void rs_fft_kernel(FftArgs a) {
     }
 
     lch::solve<LOGW, 0, 0, K>(v);
+    // opaque phase boundary: without it LLVM fuses xor chains of the final
+    // transform with solve's and keeps raw input rows live to the end
+    // (N=128 encode: 191 -> 127 VGPRs, 2 -> 4 waves per SIMD)
+    lch::sfor<0, K>([&v](auto J) { asm volatile("" : "+v"(v[decltype(J)::value])); });
 
     if constexpr (MODE == GF_MODE_ENCODE) {
         auto st = [&](auto Lam, auto Off, auto Lo, auto Hi) {
@@ -296,33 +324,52 @@ __global__ __launch_bounds__(64) void rs_fft_kernel(FftArgs a) {
         lch::fft<G, LOGW, 0, 0, K, K, N>(v, st);
     } else {
         const uint32_t *cls = reinterpret_cast<const uint32_t *>(a.cls + (size_t)inst * a.cls_stride);
+        // Software pipeline over output groups: the compare loads of group g
+        // are in flight while group g-1 is compared and stored, so the HBM
+        // latency of a compare read is paid once per kernel, not per group.
+        constexpr int GS = 1 << GD;
+        uint32_t px[GS], pold[GS], pc[GS];
+        int ppos = 0, pcnt = 0;
+        auto flush = [&]() {
+            lch::sfor<0, GS>([&](auto I) {
+                constexpr int i = decltype(I)::value;
+                if (i < pcnt) {  // wave-uniform
+                    const int pos = ppos + i;
+                    if (pc[i] == 1u) {
+                        row_store(pos, px[i]);
+                    } else if (pc[i] == 2u && pold[i] != px[i]) {
+                        row_store(pos, px[i]);
+                        if (a.flags && atomicOr(&a.flags[(size_t)inst * N + pos], 1u) == 0u)
+                            a.list[atomicAdd(a.counter, 1u)] = ((uint32_t)inst << 8) | (uint32_t)pos;
+                    }
+                }
+            });
+        };
         auto st = [&](auto Lam, auto Off, auto Lo, auto Hi) {
             constexpr int lam = decltype(Lam)::value, o = decltype(Off)::value;
             constexpr int lo = lch::cmax(decltype(Lo)::value, K - lam), hi = lch::cmin(decltype(Hi)::value, N - lam);
             if constexpr (lo < hi) {
                 uint32_t c[hi - lo], old[hi - lo];
-                // phase 1: class lookups + the compare loads of the whole group
+                // class lookups + the compare loads of this group
                 lch::sfor<lo, hi>([&](auto I) {
                     constexpr int i = decltype(I)::value, pos = lam + i;
                     c[i - lo] = (cls[pos >> 2] >> (8 * (pos & 3))) & 0xffu;  // wave-uniform
                     old[i - lo] = 0;
                     if (c[i - lo] == 2u) old[i - lo] = row_load(pos);
                 });
-                // phase 2: store missing rows; store + flag mismatching compare rows
+                flush();  // the previous group, while these loads fly
                 lch::sfor<lo, hi>([&](auto I) {
-                    constexpr int i = decltype(I)::value, pos = lam + i;
-                    const uint32_t x = v[o + i] & keep;
-                    if (c[i - lo] == 1u) {
-                        row_store(pos, x);
-                    } else if (c[i - lo] == 2u && old[i - lo] != x) {
-                        row_store(pos, x);
-                        if (a.flags && atomicOr(&a.flags[(size_t)inst * N + pos], 1u) == 0u)
-                            a.list[atomicAdd(a.counter, 1u)] = ((uint32_t)inst << 8) | (uint32_t)pos;
-                    }
+                    constexpr int i = decltype(I)::value;
+                    px[i - lo] = v[o + i] & keep;
+                    pold[i - lo] = old[i - lo];
+                    pc[i - lo] = c[i - lo];
                 });
+                ppos = lam + lo;
+                pcnt = hi - lo;
             }
         };
-        lch::fft<G, LOGW, 0, 0, K, K, N>(v, st);
+        lch::fft<GD, LOGW, 0, 0, K, K, N>(v, st);
+        flush();
     }
 }
 
