@@ -62,6 +62,8 @@ def main():
     ap.add_argument("--streams", type=int, default=1,
                     help="split the batch over S HIP streams (one context each) so stages of different "
                          "instance groups overlap")
+    ap.add_argument("--shard-align", type=int, default=128,
+                    help="shard row pitch alignment in bytes (multiple of 64; the C ABI needs 64)")
     ap.add_argument("--force-gather", action="store_true",
                     help="run the RCCL all-gather even with one rank (exercises rbc_comm_*)")
     args = ap.parse_args()
@@ -83,7 +85,7 @@ def main():
     ctx = ca.Context(n, f, device=dev)
     k, d = ctx.k, ctx.depth
     S = (B + k - 1) // k
-    spitch = round_up(S, 64)
+    spitch = round_up(S, args.shard_align)  # row starts on whole 128-B lines: full-line HBM writes
     vpitch = round_up(k * S + 32, 64)
     opitch = round_up(k * S, 16)
     I = inst

@@ -151,8 +151,6 @@ int ctx_create_kn(int n, int k, int device, rbc_ctx **out) {
     }
     if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->d_M, up.size()) != hipSuccess ||
         hipMemcpy(c->d_M, up.data(), up.size(), hipMemcpyHostToDevice) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
         if (c->d_M) (void)hipFree(c->d_M);
@@ -164,6 +162,19 @@ int ctx_create_kn(int n, int k, int device, rbc_ctx **out) {
 }
 
 inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+// The context's own streams are created on first use (caller holds c->mu):
+// a device-API caller that brings its own streams never spends hardware
+// queues on them (GPU_MAX_HW_QUEUES is 4; streams beyond that share a queue
+// and serialise).
+hipStream_t host_stream(rbc_ctx *c) {
+    if (!c->stream && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) c->stream = nullptr;
+    return c->stream;
+}
+hipStream_t aux_stream(rbc_ctx *c) {
+    if (!c->aux && hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) c->aux = nullptr;
+    return c->aux;
+}
 
 // ------------------------------------------------------------ stage bodies
 int stage_encode(rbc_ctx *c, hipStream_t st, int count, const uint8_t *values, uint64_t value_pitch,
@@ -304,7 +315,7 @@ int ensure_ws(rbc_ctx *c, int count) {
 // and the rows that need hashing are collected in ws_list
 int stage_regenerate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, uint32_t shard_pitch,
                      const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *valid,
-                     int32_t *status, int compare = 0) {
+                     int32_t *status, int compare = 0, uint8_t *values_out = nullptr, uint32_t value_pitch = 0) {
     int rc = ensure_ws(c, count);
     if (rc) return rc;
     if (compare) RBC_HIP(hipMemsetAsync(c->ws_counter.p, 0, 16, st));
@@ -385,6 +396,8 @@ int stage_regenerate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, uin
             a.list = pa.list;
             a.counter = pa.counter;
         }
+        a.values_out = values_out;  // join fused into the re-encode (it loads every data row anyway)
+        a.value_pitch_out = value_pitch;
         RBC_HIP(rbc_launch_rs_fft(a, st));
     } else if (nr > 0) {
         GfArgs g{};
@@ -435,12 +448,23 @@ int stage_interpolate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, ui
         return RBC_ERR_INVALID_ARG;
     if ((uint64_t)c->n * shard_pitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
     if (count == 0) return RBC_OK;
+    // RBC_FUSE_JOIN=1: rs_fft_kernel<decode> writes the value from the data
+    // rows it loads anyway (saves the join's k*S re-read, but lengthens the
+    // critical path: measured slower at C2 than the join overlapping the
+    // latency-bound regen hashing on the aux stream)
+    static const bool fuse_env = [] {
+        const char *e = getenv("RBC_FUSE_JOIN");
+        return e && atoi(e) != 0;
+    }();
+    const bool fused_join = fuse_env && c->fft && c->n > c->k;
     int rc = stage_regenerate(c, st, count, shards, shard_pitch, shard_lens, uniform_shard_len, valid, status,
-                              leaves_verified);
+                              leaves_verified, fused_join ? values_out : nullptr, value_pitch);
     if (rc) return rc;
-    // fork: value assembly (HBM-bound) runs on the aux stream beside the
-    // regen hashing (latency-bound, under-fills the SIMDs); it needs only the
+    // value assembly (HBM-bound) forks onto the aux stream beside the regen
+    // hashing (latency-bound, under-fills the SIMDs); it needs only the
     // regenerated rows.  values_out is defined where status == 0.
+    if (!fused_join) {
+    if (!aux_stream(c)) return RBC_ERR_DEVICE;
     RBC_HIP(hipEventRecord(c->ev_fork, st));
     RBC_HIP(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
     {
@@ -460,6 +484,7 @@ int stage_interpolate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, ui
         RBC_HIP(rbc_launch_join(j, c->aux));
     }
     RBC_HIP(hipEventRecord(c->ev_join, c->aux));
+    }
     const int nr = c->n - c->k;
     ShaArgs a{};
     a.count = count;
@@ -496,7 +521,7 @@ int stage_interpolate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, ui
     RBC_HIP(rbc_launch_merkle(m, true, st));
     if (digests)
         RBC_HIP(rbc_launch_digest(leaves, (uint64_t)c->n * 32, c->k, status, digests, count, st));
-    RBC_HIP(hipStreamWaitEvent(st, c->ev_join, 0));  // join back before returning to the caller's stream
+    if (!fused_join) RBC_HIP(hipStreamWaitEvent(st, c->ev_join, 0));  // join back before returning
     return RBC_OK;
 }
 
@@ -538,7 +563,8 @@ int host_reconstruct(rbc_ctx *c, uint8_t *const *shards, size_t *lens, int n_sha
         if (lens[i]) memcpy(stage + (size_t)i * pitch, shards[i], S);
         stage[(size_t)c->n * pitch + i] = lens[i] ? 1 : 0;
     }
-    hipStream_t st = c->stream;
+    hipStream_t st = host_stream(c);
+    if (!st) return RBC_ERR_DEVICE;
     RBC_HIP(hipMemcpyAsync(c->d_shards.p, stage, (size_t)c->n * pitch, hipMemcpyHostToDevice, st));
     RBC_HIP(hipMemcpyAsync(c->d_valid.p, stage + (size_t)c->n * pitch, c->n, hipMemcpyHostToDevice, st));
     rc = stage_regenerate(c, st, 1, c->d_shards.as<uint8_t>(), (uint32_t)pitch, nullptr, (uint32_t)S,
@@ -794,7 +820,8 @@ int rbc_shard_commit(rbc_ctx *c, int count, const uint8_t *const *values, const 
     if (vpitch > 0x7fffffffULL || (size_t)c->n * dpitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
     RBC_HIP(hipSetDevice(c->device));
-    hipStream_t st = c->stream;
+    hipStream_t st = host_stream(c);
+    if (!st) return RBC_ERR_DEVICE;
     RBC_HIP(c->d_values.ensure((size_t)count * vpitch));
     RBC_HIP(c->d_shards.ensure((size_t)count * c->n * dpitch));
     RBC_HIP(c->d_leaves.ensure((size_t)count * c->n * 32));
@@ -849,7 +876,8 @@ int rbc_validate_batch(rbc_ctx *c, int count, const uint8_t *const *shards, cons
     const size_t bslot = (size_t)std::max(d, 1) * 32;
     std::lock_guard<std::mutex> lk(c->mu);
     RBC_HIP(hipSetDevice(c->device));
-    hipStream_t st = c->stream;
+    hipStream_t st = host_stream(c);
+    if (!st) return RBC_ERR_DEVICE;
     const size_t stage_bytes = (size_t)count * (pitch + bslot + 32 + 4 + 1);
     RBC_HIP(c->h_stage.ensure(stage_bytes));
     RBC_HIP(c->d_shards.ensure((size_t)count * pitch));
@@ -937,7 +965,8 @@ int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t s
     if ((size_t)c->n * dpitch > 0x7fffffffULL || vpitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
     RBC_HIP(hipSetDevice(c->device));
-    hipStream_t st = c->stream;
+    hipStream_t st = host_stream(c);
+    if (!st) return RBC_ERR_DEVICE;
     RBC_HIP(c->d_shards.ensure((size_t)count * c->n * dpitch));
     RBC_HIP(c->d_valid.ensure((size_t)count * c->n));
     RBC_HIP(c->d_leaves.ensure((size_t)count * c->n * 32));
@@ -954,6 +983,8 @@ int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t s
     RBC_HIP(hipMemcpyAsync(c->d_valid.p, present, (size_t)count * c->n, hipMemcpyHostToDevice, st));
     RBC_HIP(hipMemcpyAsync(c->d_roots.p, roots, (size_t)count * 32, hipMemcpyHostToDevice, st));
     RBC_HIP(hipMemcpyAsync(c->d_slens.p, ln, (size_t)count * 4, hipMemcpyHostToDevice, st));
+    // ragged batch: bytes past k*S_i of a value row are returned as zero
+    RBC_HIP(hipMemsetAsync(c->d_values.p, 0, (size_t)count * vpitch, st));
     int rc = stage_interpolate(c, st, count, c->d_shards.as<uint8_t>(), (uint32_t)dpitch, c->d_slens.as<uint32_t>(),
                                0, c->d_valid.as<uint8_t>(), c->d_leaves.as<uint8_t>(), 0, c->d_roots.as<uint8_t>(),
                                c->d_values.as<uint8_t>(), (uint32_t)vpitch, c->d_digests.as<uint8_t>(),
@@ -1062,7 +1093,8 @@ static int rs_parity(rbc_ctx *c, const uint8_t *const *shards, size_t S, std::ve
     const size_t vpitch = round_up((size_t)c->k * S + 32, kAlign);
     if (vpitch > 0x7fffffffULL || (size_t)c->n * dpitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
     RBC_HIP(hipSetDevice(c->device));
-    hipStream_t st = c->stream;
+    hipStream_t st = host_stream(c);
+    if (!st) return RBC_ERR_DEVICE;
     RBC_HIP(c->h_stage.ensure(std::max(vpitch, (size_t)c->n * dpitch)));
     RBC_HIP(c->d_values.ensure(vpitch));
     RBC_HIP(c->d_shards.ensure((size_t)c->n * dpitch));

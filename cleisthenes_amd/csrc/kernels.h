@@ -143,6 +143,10 @@ struct FftArgs {
     uint32_t *flags;           // [I][n]
     uint32_t *list;
     uint32_t *counter;
+    // decode: interpolate's value (data rows 0..k-1 concatenated, k*S bytes)
+    // written straight from the loaded data rows (nullable)
+    uint8_t *values_out;
+    uint32_t value_pitch_out;
 };
 
 bool rbc_fft_supported(int n, int k);

@@ -82,25 +82,37 @@ constexpr Tab make_tab(uint32_t c) {
     return t;
 }
 
-// a + C*x for 4 packed bytes (C compile-time)
+// Per-group table registers.  gfx950 VOP3 reads one scalar operand, so one
+// half of each 8-entry table must sit in a VGPR; all butterflies of one
+// (layer, coset) group share the constant, so the two halves are
+// materialised once per group (volatile: never CSE'd into a kernel-long
+// register, which would cost occupancy) and the other half plus t2 ride in
+// SGPRs.
+struct TR {
+    uint32_t lo0, lo1;
+};
 template <uint32_t C>
-RBC_DEV uint32_t mac(uint32_t a, uint32_t x) {
+RBC_DEV TR tab_regs() {
+    TR r{0u, 0u};
+    if constexpr (C > 1) {
+        constexpr Tab t = make_tab(C);
+        asm volatile("v_mov_b32 %0, %1" : "=v"(r.lo0) : "i"(t.t0lo));
+        asm volatile("v_mov_b32 %0, %1" : "=v"(r.lo1) : "i"(t.t1lo));
+    }
+    return r;
+}
+
+// a + C*x for 4 packed bytes (C compile-time, tables from tab_regs<C>())
+template <uint32_t C>
+RBC_DEV uint32_t mac(uint32_t a, uint32_t x, const TR &r) {
     if constexpr (C == 0) {
         return a;
     } else if constexpr (C == 1) {
         return a ^ x;
     } else {
         constexpr Tab t = make_tab(C);
-        // gfx950 VOP3 takes one scalar operand: one table half per lookup is
-        // materialised into a VGPR right here -- the asm nominally reads x, so
-        // it is never CSE'd into a long-lived register (which would cost
-        // occupancy) yet stays free to schedule; the other half and t2 ride
-        // in SGPRs
-        uint32_t lo0, lo1;
-        asm("v_mov_b32 %0, %2 ; %1" : "=v"(lo0) : "v"(x), "i"(t.t0lo));
-        asm("v_mov_b32 %0, %2 ; %1" : "=v"(lo1) : "v"(x), "i"(t.t1lo));
-        const uint32_t p0 = perm(t.t0hi, lo0, x & 0x07070707u);
-        const uint32_t p1 = perm(t.t1hi, lo1, (x >> 3) & 0x07070707u);
+        const uint32_t p0 = perm(t.t0hi, r.lo0, x & 0x07070707u);
+        const uint32_t p1 = perm(t.t1hi, r.lo1, (x >> 3) & 0x07070707u);
         const uint32_t p2 = perm(t.t2, t.t2, (x >> 6) & 0x03030303u);
         return xor3(a, p0, p1) ^ p2;
     }
@@ -135,11 +147,12 @@ RBC_DEV void fft_full(uint32_t (&v)[R]) {
         constexpr int H = 1 << (M - 1);
         constexpr uint32_t w = twiddle(M - 1, LAM);
         constexpr int NZA = cmin(NZ, H), NZB = cmax(NZ - H, 0);
+        const TR tr = NZB > 0 ? tab_regs<w>() : TR{0u, 0u};
         sfor<0, H>([&](auto I) {
             constexpr int i = decltype(I)::value;
             if constexpr (i < NZB) {
                 const uint32_t a = v[OFF + i], b = v[OFF + H + i];
-                const uint32_t a2 = mac<w>(a, b);
+                const uint32_t a2 = mac<w>(a, b, tr);
                 v[OFF + i] = a2;
                 v[OFF + H + i] = a2 ^ b;
             } else if constexpr (i < NZA) {
@@ -169,18 +182,20 @@ RBC_DEV void fft(uint32_t (&v)[R], ST &st) {
         constexpr uint32_t w = twiddle(M - 1, LAM);
         constexpr int NZA = cmin(NZ, H), NZB = cmax(NZ - H, 0);
         constexpr bool needA = LO < H, needB = HI > H;
+        constexpr uint32_t wt = needA ? w : (w ^ 1u);  // needB only: b' = a + (w+1) b
+        const TR tr = NZB > 0 ? tab_regs<wt>() : TR{0u, 0u};
         sfor<0, H>([&](auto I) {
             constexpr int i = decltype(I)::value;
             if constexpr (i < NZB) {
                 const uint32_t a = v[OFF + i], b = v[OFF + H + i];
                 if constexpr (needA && needB) {
-                    const uint32_t a2 = mac<w>(a, b);
+                    const uint32_t a2 = mac<wt>(a, b, tr);
                     v[OFF + i] = a2;
                     v[OFF + H + i] = a2 ^ b;
                 } else if constexpr (needA) {
-                    v[OFF + i] = mac<w>(a, b);
+                    v[OFF + i] = mac<wt>(a, b, tr);
                 } else {
-                    v[OFF + H + i] = mac<w ^ 1u>(a, b);  // a + (w+1) b
+                    v[OFF + H + i] = mac<wt>(a, b, tr);  // a + (w+1) b
                 }
             } else if constexpr (i < NZA && needB) {
                 v[OFF + H + i] = v[OFF + i];  // b == 0
@@ -202,11 +217,12 @@ RBC_DEV void ifft(uint32_t (&v)[R]) {
         ifft<M - 1, LAM, OFF>(v);
         ifft<M - 1, LAM + H, OFF + H>(v);
         constexpr uint32_t w = twiddle(M - 1, LAM);
+        const TR tr = tab_regs<w>();
         sfor<0, H>([&](auto I) {
             constexpr int i = decltype(I)::value;
             const uint32_t b = v[OFF + i] ^ v[OFF + H + i];
             v[OFF + H + i] = b;
-            v[OFF + i] = mac<w>(v[OFF + i], b);
+            v[OFF + i] = mac<w>(v[OFF + i], b, tr);
         });
     }
 }
@@ -236,9 +252,10 @@ RBC_DEV void solve(uint32_t (&v)[R]) {
         };
         fft<0, M - 1, LAM + H, 0, H, 0, TP>(g, sub);
         solve<M - 1, LAM + H, OFF + H, TP>(v);  // P1
+        const TR tr = tab_regs<w>();
         sfor<0, TP>([&](auto I) {              // P0 = g + w P1
             constexpr int i = decltype(I)::value;
-            v[OFF + i] = mac<w>(v[OFF + i], v[OFF + H + i]);
+            v[OFF + i] = mac<w>(v[OFF + i], v[OFF + H + i], tr);
         });
     }
 }
@@ -296,8 +313,12 @@ __global__ __launch_bounds__(64) void rs_fft_kernel(FftArgs a) {
         lch::sfor<0, K>([&](auto J) {
             constexpr int j = decltype(J)::value;
             const uint32_t row0 = (uint32_t)j * S;  // Split: data[j*S : (j+1)*S]
-            const int lim = (int)min(S, B > row0 ? B - row0 : 0u);
-            v[j] &= keep_bytes4(lim - (int)off);
+            if (row0 + S <= B) {                    // wave-uniform: a full data row
+                v[j] &= keep;
+            } else {                                // the rows carrying the zero pad
+                const int lim = (int)(B > row0 ? B - row0 : 0u);
+                v[j] &= keep_bytes4(lim - (int)off);
+            }
             // materialise the masked row: otherwise the AND is folded into
             // the first butterfly (v_bitop3) and the raw row plus its mask
             // stay live through the transform (+44 VGPRs)
@@ -306,6 +327,25 @@ __global__ __launch_bounds__(64) void rs_fft_kernel(FftArgs a) {
         });
     } else {
         lch::sfor<0, K>([&](auto J) { v[decltype(J)::value] = row_load(decltype(J)::value); });
+        if (a.values_out) {
+            // interpolate's value = data rows concatenated (k*S bytes, pad
+            // kept): each lane writes its dword of every data row at j*S+off
+            // (unaligned stores are fine on gfx950); the lane holding a
+            // row's last, partial dword writes only the bytes below S
+            uint8_t *val = a.values_out + (size_t)inst * a.value_pitch_out;
+            const auto ro = __builtin_amdgcn_make_buffer_rsrc(val, (short)0, (int)a.value_pitch_out, 0x00020000);
+            const int tail = (int)S - (int)off;  // valid bytes of this lane's dword
+            lch::sfor<0, K>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                const int base = j * (int)S;
+                if (tail >= 4) {
+                    __builtin_amdgcn_raw_buffer_store_b32(v[j], ro, (int)off, base, 0);
+                } else if (tail > 0) {
+                    for (int b = 0; b < tail; ++b)
+                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v[j] >> (8 * b)), ro, (int)off + b, base, 0);
+                }
+            });
+        }
     }
 
     lch::solve<LOGW, 0, 0, K>(v);
@@ -318,7 +358,9 @@ __global__ __launch_bounds__(64) void rs_fft_kernel(FftArgs a) {
         auto st = [&](auto Lam, auto Off, auto Lo, auto Hi) {
             lch::sfor<decltype(Lo)::value, decltype(Hi)::value>([&](auto I) {
                 constexpr int i = decltype(I)::value, pos = decltype(Lam)::value + i;
-                if constexpr (pos >= K && pos < N) row_store(pos, v[decltype(Off)::value + i] & keep);
+                // no `& keep`: every input byte past S was masked to zero on
+                // load, and the transform is column-wise linear
+                if constexpr (pos >= K && pos < N) row_store(pos, v[decltype(Off)::value + i]);
             });
         };
         lch::fft<G, LOGW, 0, 0, K, K, N>(v, st);

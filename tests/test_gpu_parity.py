@@ -468,7 +468,9 @@ def test_fft_codec_matches_matrix_codec(gpu, n, f, B, I):
     assert np.array_equal(a["enc"], b["enc"])
     assert np.array_equal(a["status"], b["status"])
     ok = a["status"] == 0
-    assert np.array_equal(a["out"][ok], b["out"][ok])
+    S = (B + (n - 2 * f) - 1) // (n - 2 * f)
+    kS = (n - 2 * f) * S  # the value is k*S bytes; bytes past it are unspecified
+    assert np.array_equal(a["out"][ok][:, :kS], b["out"][ok][:, :kS])
     assert np.array_equal(a["digests"][ok], b["digests"][ok])
     for i in np.nonzero(ok)[0]:
         assert b["out"][i, :B].tobytes() == b["values"][i, :B].tobytes()

@@ -16,14 +16,30 @@ import sys
 from collections import defaultdict
 
 ROLES = {"gf_rows_kernel": ["encode", "decode"], "sha_rows_kernel<false>": ["leaves", "regen"]}
+# FFT codec (rs_fft.hip): the encode and decode transforms are separate
+# instantiations (last template argument = mode), and gf_rows_kernel only
+# regenerates the missing data rows of interpolate
+FFT_ROLES = {"gf_rows_kernel": ["missing-data"], "sha_rows_kernel<false>": ["leaves", "regen"]}
 
 
 def base(name):
-    return name.split("(")[0].replace("void ", "")
+    return name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
+
+
+def _fft_named(k):
+    if k.startswith("rs_fft_kernel<"):
+        return k + ("[encode]" if k.endswith(", 0>") else "[decode]")
+    return None
+
+
+FFT_MODE = False
 
 
 def role_name(k, ordinal):
-    for prefix, roles in ROLES.items():
+    f = _fft_named(k)
+    if f:
+        return f
+    for prefix, roles in (FFT_ROLES if FFT_MODE else ROLES).items():
         if k.startswith(prefix):
             return f"{k}[{roles[ordinal % len(roles)]}]"
     return k
@@ -69,6 +85,9 @@ def load_trace(d):
 
 
 def summarise(d):
+    global FFT_MODE
+    f = os.path.join(d, "trace", "run_kernel_trace.csv")
+    FFT_MODE = os.path.exists(f) and "rs_fft_kernel" in open(f).read()
     pm, tr = load_pmc(d), load_trace(d)
     rows = {}
     for k in sorted(set(pm) | set(tr)):
@@ -109,6 +128,8 @@ if __name__ == "__main__":
             name = None
             if k.startswith("gf_rows_kernel") and k.endswith("[encode]"):
                 name = "gf_rows_kernel<encode>"
+            elif k.startswith("rs_fft_kernel") and k.endswith("[encode]"):
+                name = "rs_fft_kernel<encode>"
             else:
                 name = bench_names.get(k)
             if name and "hbm_read_bytes" in r and "hbm_write_bytes" in r:
