@@ -235,28 +235,42 @@ def main():
         "sha_rows_kernel<verify>": (stage_ms["verify"], Ig * (n * S + n * d * 32 + n * 33 + 32 + n),
                                     Ig * n * (blocks_per_shard + 2 * d)),
     }
-    dom = max(kern, key=lambda x: kern[x][0])
-    dms, dbytes, dcomp = kern[dom]
-    achieved = dbytes / (dms / 1e3) / 1e9
-    roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-            "algorithmic_bytes_per_launch": int(dbytes), "avg_ms": round(dms, 4)}
-    if dcomp:
-        # SHA-256 compressions/s vs the integer-VALU roof (~1.4k VALU ops per compression)
-        cps = dcomp / (dms / 1e3)
-        roof["sha256_compressions_per_s"] = round(cps / 1e9, 3)
-        roof["sha256_compressions_per_s_unit"] = "G/s"
-        roof["valu_frac_est"] = round(cps * 1470.0 / 64 / VALU_ISSUE_PEAK, 4)  # ~1470 VALU per compression
+    pm = {}
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic_r01.json")
     if os.path.exists(pmc_path):
         try:
             pm = json.load(open(pmc_path))
-            if pm.get("config") == args.config and dom in pm.get("kernels", {}):
-                roof["traffic"] = pm["kernels"][dom]["hbm_bytes_per_launch"]
-                roof["traffic_source"] = os.path.relpath(pmc_path, ROOT)
+            if pm.get("config") != args.config:
+                pm = {}
         except Exception:
-            pass
+            pm = {}
 
+    def roofline(name):
+        ms, nbytes, ncomp = kern[name]
+        ach = nbytes / (ms / 1e3) / 1e9
+        r = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "algorithmic_bytes_per_launch": int(nbytes),
+             "avg_ms": round(ms, 4)}
+        pk = pm.get("kernels", {}).get(name)
+        if pk:
+            r["traffic"] = pk["hbm_bytes_per_launch"]
+            r["traffic_source"] = os.path.relpath(pmc_path, ROOT)
+        if ncomp:
+            # SHA-256 is integer-VALU bound (north_star: hashes/s against the VALU
+            # peak): compressions/s, and VALU issue = compressions x the kernel's
+            # VALU wave-instructions per compression (rocprof SQ_INSTS_VALU, in
+            # the PMC file) over 1024 SIMDs x 2.4 GHz / 4 clk
+            cps = ncomp / (ms / 1e3)
+            r["sha256_compressions_per_s"] = round(cps / 1e9, 3)
+            r["sha256_compressions_per_s_unit"] = "G/s"
+            vpc = (pk or {}).get("valu_per_compression", 1418.0 / 64)
+            r["valu"] = {"achieved": round(cps * vpc / 1e9, 2), "peak": round(VALU_ISSUE_PEAK / 1e9, 1),
+                         "unit": "G wave-instr/s", "frac": round(cps * vpc / VALU_ISSUE_PEAK, 4)}
+        return r
+
+    dom = max(kern, key=lambda x: kern[x][0])
+    roof = roofline(dom)
+    codec_roof = roofline(enc_kernel)  # north_star: encode against the HBM peak
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(n, f, B, args.cpu_instances, args.cpu_threads)
@@ -281,6 +295,7 @@ def main():
         "stage_ms": {kk: round(v, 4) for kk, v in stage_ms.items()},
         "decoded_ok": n_ok,
         "roofline": roof,
+        "roofline_encode": codec_roof,
         "cpu_baseline": cpu,
     }
     if rank == 0:

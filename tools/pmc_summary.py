@@ -19,6 +19,10 @@ ROLES = {"gf_rows_kernel": ["encode", "decode"], "sha_rows_kernel<false>": ["lea
 # FFT codec (rs_fft.hip): the encode and decode transforms are separate
 # instantiations (last template argument = mode), and gf_rows_kernel only
 # regenerates the missing data rows of interpolate
+# SHA-256 compressions per launch of the bench's c2 step (I=1024, N=128,
+# S=23832: 373 blocks per shard; verify adds 2 per branch level, d=7)
+COMPRESSIONS = {("c2", "sha_rows_kernel<leaves>"): 1024 * 128 * 373,
+                ("c2", "sha_rows_kernel<verify>"): 1024 * 128 * (373 + 14)}
 FFT_ROLES = {"gf_rows_kernel": ["missing-data"], "sha_rows_kernel<false>": ["leaves", "regen"]}
 
 
@@ -135,5 +139,9 @@ if __name__ == "__main__":
             if name and "hbm_read_bytes" in r and "hbm_write_bytes" in r:
                 out["kernels"][name] = {"hbm_bytes_per_launch": r["hbm_read_bytes"] + r["hbm_write_bytes"],
                                         "hbm_read_bytes": r["hbm_read_bytes"], "hbm_write_bytes": r["hbm_write_bytes"],
-                                        "avg_us_profiled": r["avg_us"]}
+                                        "avg_us_profiled": r["avg_us"], "SQ_INSTS_VALU": r.get("SQ_INSTS_VALU")}
+                comp = COMPRESSIONS.get((cfg, name))
+                if comp and r.get("SQ_INSTS_VALU"):
+                    out["kernels"][name]["compressions_per_launch"] = comp
+                    out["kernels"][name]["valu_per_compression"] = round(r["SQ_INSTS_VALU"] / comp, 3)
         json.dump(out, open(sys.argv[sys.argv.index("--traffic") + 1], "w"), indent=1)
