@@ -12,7 +12,8 @@
 //   iff the novel coefficients vanish from index k on, so
 //     coeffs  = solve(n, 0, data, k)   (only power-of-two IFFT/FFT blocks)
 //     shards  = FFT(coeffs) at the positions [k, N)
-//   Model and op counts: tools/rs_fft_model.py (checked against the oracle).
+//   Model and op counts: tests/fft_model.py (checked against the oracle by
+//   tests/test_fft_model.py).
 //
 // Every butterfly constant W_j(lambda) is a compile-time constant, so the
 // whole transform unrolls into straight-line VALU code: a constant multiply of

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Python model of the additive-FFT Reed-Solomon encoder used by the gfx950
-`rs_fft_kernel` (design validation; not product code, not the oracle).
+`rs_fft_kernel` (test infrastructure: pins the transform's math against the
+oracle on the CPU; not product code).
 
 klauspost/reedsolomon v1.9.1's code (oracle/rbc_oracle.py build_matrix) is
 M = V * inv(V[:k]), V[r][c] = r^c over GF(2^8)/0x11D: shard r of the codeword
@@ -21,7 +22,7 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "oracle"))
-import rbc_oracle as orc  # noqa: E402
+import rbc_oracle as orc  # noqa: E402  (tests/ may use the oracle as the checker)
 
 MUL = orc.MUL
 
