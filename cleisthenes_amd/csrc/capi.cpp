@@ -354,10 +354,12 @@ int stage_regenerate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, uin
         const int rmax = std::min(c->k, nr);
         GfArgs g{};
         g.count = count;
-        g.tiles = (int)((shard_pitch + 4095) / 4096);
         g.R = rmax;
         g.K = c->k;
         g.rc = rbc_gf_pick_rc(rmax, gf_md_rcmax());
+        // short rows (C4: 763 B) would leave most of a 4 KiB tile idle
+        g.tpb = (g.rc == 8 && shard_pitch <= 2048) ? 64 : 256;
+        g.tiles = (int)((shard_pitch + 16 * g.tpb - 1) / (16 * g.tpb));
         g.mode = GF_MODE_DECODE;
         g.in = shards;
         g.in_inst_pitch = (uint64_t)c->n * shard_pitch;

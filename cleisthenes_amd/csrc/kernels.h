@@ -10,8 +10,9 @@ enum { GF_MODE_ENCODE = 0, GF_MODE_DECODE = 1 };
 
 struct GfArgs {
     int count;                 // instances
-    int tiles;                 // 4 KiB column tiles per instance (ceil(out_row_pitch / 4096))
+    int tiles;                 // column tiles per instance (ceil(out_row_pitch / (16 * tpb)))
     int rc;                    // rows per chunk (template)
+    int tpb;                   // threads per block (template): 256 (4 KiB tiles) or 64 (1 KiB, rc 8 only); 0 = 256
     int R, K;                  // output rows, input rows per instance
     int mode;                  // GF_MODE_*
     const uint8_t *in;         // encode: values [I][value_pitch]; decode: shards [I][N][pitch]

@@ -64,14 +64,14 @@ RBC_DEV uint4 mask16(uint4 v, int nvalid) {
 // (Split), funnel-shifting unaligned rows, masks the zero pad, and writes the
 // data rows through to shards[0..k) on the first chunk.
 // ============================================================================
-template <int RC>
-__global__ __launch_bounds__(256, (RC <= 21 ? 3 : 2)) void gf_rows_kernel(GfArgs a) {
+template <int RC, int TPB>
+__global__ __launch_bounds__(TPB, (RC <= 21 ? 3 : 2)) void gf_rows_kernel(GfArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int KP = (a.K + 1) & ~1;
     uint4 *s_t01 = reinterpret_cast<uint4 *>(smem);
     uint32_t *s_t2 = reinterpret_cast<uint32_t *>(smem + (size_t)16 * RC * KP);
     uint8_t *s_in = reinterpret_cast<uint8_t *>(smem + (size_t)20 * RC * KP);
-    uint8_t *s_out = s_in + 256;
+    uint8_t *s_out = s_in + 256;  // 256 = max positions
 
     // block -> (work item = instance x column tile, row chunk c).  The chunks
     // of one item are 8 block ids apart, i.e. dispatched to the same XCD under
@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256, (RC <= 21 ? 3 : 2)) void gf_rows_kernel(GfArgs
     } else {
         S = inst_len(a.lens, a.uniform_len, inst);
     }
-    const uint32_t tile_byte0 = (uint32_t)tile * 4096u;
+    const uint32_t tile_byte0 = (uint32_t)tile * (16u * TPB);  // TPB threads x 16 B
     if (tile_byte0 >= a.out_row_pitch) return;
     const uint32_t my_off = tile_byte0 + 16u * tid;      // byte offset inside a row
     const bool my_store = my_off < a.out_row_pitch;
@@ -106,8 +106,8 @@ __global__ __launch_bounds__(256, (RC <= 21 ? 3 : 2)) void gf_rows_kernel(GfArgs
     const rsrc_t rin = make_rsrc(in_inst, a.in_inst_bytes);
 
     if (a.mode == GF_MODE_DECODE) {
-        for (int t = tid; t < a.K; t += 256) s_in[t] = a.in_idx[(size_t)inst * a.idx_stride + t];
-        for (int t = tid; t < a.R; t += 256) s_out[t] = a.out_idx[(size_t)inst * a.idx_stride2 + t];
+        for (int t = tid; t < a.K; t += TPB) s_in[t] = a.in_idx[(size_t)inst * a.idx_stride + t];
+        for (int t = tid; t < a.R; t += TPB) s_out[t] = a.out_idx[(size_t)inst * a.idx_stride2 + t];
     }
 
     // load 16 bytes of input row j for this thread (masked to the row)
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256, (RC <= 21 ? 3 : 2)) void gf_rows_kernel(GfArgs
     {
         const int r0 = c * RC;
         const int rows = min(RC, rlim - r0);
-        for (int e = tid; e < RC * KP; e += 256) {
+        for (int e = tid; e < RC * KP; e += TPB) {
             const int r = e / KP, j = e - r * KP;
             uint32_t cf = 0;
             if (r < rows && j < a.K)
@@ -577,30 +577,52 @@ __global__ __launch_bounds__(256) void decode_prepare_fft_kernel(PrepArgs a, con
     uint8_t *s_miss = smem + 1024;   // 256: missing positions in index order
     int *s_misc = reinterpret_cast<int *>(smem + 1280);  // 8 ints
     uint8_t *s_fac = smem + 1312;    // 256: elimination factors of one pivot step
-    uint8_t *A = smem + 1568;        // m x 2m  [A | I] -> [I | A^-1]
+    int *s_wcnt = reinterpret_cast<int *>(smem + 1568);  // 12 ints: per-wave counts
+    uint8_t *A = smem + 1616;        // m x 2m  [A | I] -> [I | A^-1]
     const int inst = blockIdx.x, tid = threadIdx.x;
     for (int t = tid; t < 512; t += 256) s_exp[t] = exp_tab[t];
     s_log[tid] = log_tab[tid];
-    if (tid == 0) {
-        int nu = 0, nm = 0, md = 0;
-        const uint8_t *v = a.valid + (size_t)inst * a.valid_stride;
-        uint8_t *cl = a.cls + (size_t)inst * a.cls_stride;
-        for (int j = 0; j < n; ++j) {
-            const bool ok = v[j] != 0;
-            const bool used = ok && nu < k;
-            if (used) s_used[nu++] = (uint8_t)j;
-            if (!ok) {
-                s_miss[nm++] = (uint8_t)j;
-                md += j < k;
-            }
-            cl[j] = (j < k || used) ? 0 : (!ok ? 1 : (a.counter ? 2 : 1));
+    // used = the first k valid positions, missing = the invalid ones, both in
+    // index order: block-wide ranks from wave ballots (n <= 256 = blockDim)
+    {
+        const int lane = tid & 63, w = tid >> 6;
+        const bool in = tid < n;
+        const bool ok = in && a.valid[(size_t)inst * a.valid_stride + tid] != 0;
+        const bool miss = in && !ok;
+        const uint64_t bo = __ballot(ok), bm = __ballot(miss), bd = __ballot(miss && tid < k);
+        const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+        if (lane == 0) {
+            s_wcnt[w] = __popcll(bo);
+            s_wcnt[4 + w] = __popcll(bm);
+            s_wcnt[8 + w] = __popcll(bd);
         }
-        s_misc[0] = nu;
-        s_misc[1] = md;
-        s_misc[2] = (a.counter && nu >= k) ? (int)atomicAdd(a.counter, (unsigned)nm) : 0;
-        s_misc[3] = nm;
-        if (a.nmiss) a.nmiss[inst] = nm;
-        a.rcount[inst] = md;
+        __syncthreads();
+        int rok = __popcll(bo & below), rmiss = __popcll(bm & below);
+        int tok = 0, tmiss = 0, tmd = 0;
+        for (int q = 0; q < 4; ++q) {
+            if (q < w) {
+                rok += s_wcnt[q];
+                rmiss += s_wcnt[4 + q];
+            }
+            tok += s_wcnt[q];
+            tmiss += s_wcnt[4 + q];
+            tmd += s_wcnt[8 + q];
+        }
+        const bool used = ok && rok < k;
+        if (used) s_used[rok] = (uint8_t)tid;
+        if (miss) s_miss[rmiss] = (uint8_t)tid;
+        if (in)
+            a.cls[(size_t)inst * a.cls_stride + tid] =
+                (tid < k || used) ? 0 : (miss ? 1 : (a.counter ? 2 : 1));
+        if (tid == 0) {
+            const int nu = tok < k ? tok : k;
+            s_misc[0] = nu;
+            s_misc[1] = tmd;
+            s_misc[2] = (a.counter && nu >= k) ? (int)atomicAdd(a.counter, (unsigned)tmiss) : 0;
+            s_misc[3] = tmiss;
+            if (a.nmiss) a.nmiss[inst] = tmiss;
+            a.rcount[inst] = tmd;
+        }
     }
     __syncthreads();
     const int nu = s_misc[0], m = s_misc[1];
@@ -744,14 +766,14 @@ __global__ void inject_faults_kernel(uint8_t *shards, uint64_t inst_pitch, uint3
 // ============================================================================
 // launchers
 // ============================================================================
-template <int RC>
+template <int RC, int TPB = 256>
 static hipError_t launch_gf_rc(const GfArgs &a, hipStream_t st) {
     const int KP = (a.K + 1) & ~1;
     const size_t lds = (size_t)20 * RC * KP + 512;
     const int chunks = a.R > 0 ? (a.R + RC - 1) / RC : 1;
     const long items = (long)a.count * a.tiles;
     dim3 grid((unsigned)(((items + 7) / 8) * 8 * chunks));
-    hipLaunchKernelGGL(gf_rows_kernel<RC>, grid, dim3(256), lds, st, a);
+    hipLaunchKernelGGL((gf_rows_kernel<RC, TPB>), grid, dim3(TPB), lds, st, a);
     return hipGetLastError();
 }
 
@@ -772,6 +794,11 @@ int rbc_gf_pick_rc(int R, int rcmax) {
 
 hipError_t rbc_launch_gf_rows(const GfArgs &a, hipStream_t st) {
     if (a.count <= 0 || (a.R <= 0 && !a.copy)) return hipSuccess;
+    if (a.tpb == 64) {  // short rows: 1 KiB column tiles (one wave per block)
+        if (a.rc == 8) return launch_gf_rc<8, 64>(a, st);
+        return hipErrorInvalidValue;
+    }
+    if (a.tpb != 0 && a.tpb != 256) return hipErrorInvalidValue;
     switch (a.rc) {
 #define RBC_RC_CASE(x) case x: return launch_gf_rc<x>(a, st);
         RBC_RC_CASE(1) RBC_RC_CASE(2) RBC_RC_CASE(3) RBC_RC_CASE(4) RBC_RC_CASE(5) RBC_RC_CASE(6)
@@ -814,7 +841,7 @@ hipError_t rbc_launch_decode_prepare(const PrepArgs &a, hipStream_t st) {
     if (a.count <= 0) return hipSuccess;
     if (a.fft) {
         const int mmax = std::min(a.k, a.n - a.k);
-        const size_t lds = 1568 + (size_t)mmax * 2 * mmax;
+        const size_t lds = 1616 + (size_t)mmax * 2 * mmax;
         hipLaunchKernelGGL(decode_prepare_fft_kernel, dim3(a.count), dim3(256), lds, st, a, a.gf_exp, a.gf_log);
         return hipGetLastError();
     }

@@ -353,7 +353,10 @@ __global__ __launch_bounds__(64) void rs_fft_kernel(FftArgs a) {
     // opaque phase boundary: without it LLVM fuses xor chains of the final
     // transform with solve's and keeps raw input rows live to the end
     // (N=128 encode: 191 -> 127 VGPRs, 2 -> 4 waves per SIMD)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wunused-lambda-capture"  // the capture is needed (asm operand)
     lch::sfor<0, K>([&v](auto J) { asm volatile("" : "+v"(v[decltype(J)::value])); });
+#pragma clang diagnostic pop
 
     if constexpr (MODE == GF_MODE_ENCODE) {
         auto st = [&](auto Lam, auto Off, auto Lo, auto Hi) {
