@@ -11,12 +11,15 @@
 // and completes per-request tickets; callers block in rbc_batcher_wait or
 // poll (no C -> Go callbacks).  Caller buffers must stay valid until their
 // ticket completes (the cgo shim keeps the Go slices alive until then).
+// Launches are submitted asynchronously (the context's host-API slots), so
+// while batch t runs on the GPU the worker already stages batch t+1.
 #include <string.h>
 
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <unordered_map>
@@ -74,7 +77,8 @@ struct rbc_batcher {
     std::thread worker;
 
     void run();
-    void process(Kind kind, std::vector<Req> &batch);
+    std::unique_ptr<struct Pending> submit(Kind kind, std::vector<Req> &&batch);
+    void finish(struct Pending &p);
 };
 
 namespace {
@@ -92,41 +96,48 @@ int check_shards_sizes(const std::vector<size_t> &lens, size_t *S) {
 
 }  // namespace
 
-void rbc_batcher::process(Kind kind, std::vector<Req> &b) {
-    const int count = (int)b.size();
-    std::vector<int> st(count, RBC_OK);
+// One coalesced launch in flight: the requests it serves, the batch-shaped
+// buffers the C API reads at submit and fills at completion, its ticket.
+struct Pending {
+    Kind kind;
+    std::vector<Req> reqs;
+    std::vector<int> st;         // per-request status (argument checks at submit)
+    uint64_t ticket = 0;
+    int rc = RBC_OK;             // submit status
+    size_t Smax = 1;
+    std::vector<int> idx;        // interpolate: requests in the batch
+    std::vector<size_t> lens;
+    std::vector<uint8_t> shards, roots, br, ok, present, values, digests;
+    std::vector<uint32_t> slens;
+    std::vector<int32_t> status;
+};
+
+std::unique_ptr<Pending> rbc_batcher::submit(Kind kind, std::vector<Req> &&batch) {
+    auto P = std::make_unique<Pending>();
+    P->kind = kind;
+    P->reqs = std::move(batch);
+    const int count = (int)P->reqs.size();
+    P->st.assign(count, RBC_OK);
+    std::vector<Req> &b = P->reqs;
     if (kind == K_SHARD) {
         std::vector<const uint8_t *> vals(count);
-        std::vector<size_t> lens(count);
-        size_t Smax = 1;
+        P->lens.resize(count);
         for (int i = 0; i < count; ++i) {
             vals[i] = b[i].data;
-            lens[i] = b[i].len;
-            Smax = std::max(Smax, (b[i].len + k - 1) / k);
+            P->lens[i] = b[i].len;
+            P->Smax = std::max(P->Smax, (b[i].len + k - 1) / k);
         }
-        std::vector<uint8_t> shards((size_t)count * n * Smax), roots((size_t)count * 32),
-            br((size_t)count * n * std::max(depth, 1) * 32);
-        std::vector<uint32_t> slens(count);
-        uint64_t t = 0;
-        const int rc = rbc_shard_commit(ctx, count, vals.data(), lens.data(), shards.data(), Smax, slens.data(),
-                                        roots.data(), br.data(), &t);
-        for (int i = 0; i < count; ++i) {
-            Req &r = b[i];
-            if (rc) { st[i] = rc; continue; }
-            const size_t S = slens[i];
-            if (r.shards_cap < (size_t)n * S) { st[i] = RBC_ERR_INVALID_ARG; continue; }
-            for (int j = 0; j < n; ++j)
-                memcpy(r.shards_out + (size_t)j * S, shards.data() + ((size_t)i * n + j) * Smax, S);
-            if (r.shard_len_out) *r.shard_len_out = S;
-            memcpy(r.root_out, roots.data() + (size_t)i * 32, 32);
-            if (r.branches_out && depth)
-                memcpy(r.branches_out, br.data() + (size_t)i * n * depth * 32, (size_t)n * depth * 32);
-        }
+        P->shards.resize((size_t)count * n * P->Smax);
+        P->roots.resize((size_t)count * 32);
+        P->br.resize((size_t)count * n * std::max(depth, 1) * 32);
+        P->slens.resize(count);
+        P->rc = rbc_shard_commit(ctx, count, vals.data(), P->lens.data(), P->shards.data(), P->Smax, P->slens.data(),
+                                 P->roots.data(), P->br.data(), &P->ticket);
     } else if (kind == K_VALIDATE) {
         std::vector<const uint8_t *> sh(count), brs(count), rts(count);
         std::vector<size_t> sl(count), bl(count);
         std::vector<uint32_t> ix(count);
-        std::vector<uint8_t> ok(count, 0);
+        P->ok.assign(count, 0);
         for (int i = 0; i < count; ++i) {
             sh[i] = b[i].shard;
             sl[i] = b[i].shard_len;
@@ -135,18 +146,11 @@ void rbc_batcher::process(Kind kind, std::vector<Req> &b) {
             rts[i] = b[i].root;
             ix[i] = b[i].index;
         }
-        uint64_t t = 0;
-        const int rc =
-            rbc_validate_batch(ctx, count, sh.data(), sl.data(), ix.data(), brs.data(), bl.data(), rts.data(),
-                               ok.data(), &t);
-        for (int i = 0; i < count; ++i) {
-            if (rc) st[i] = rc;
-            else *b[i].ok_out = ok[i];
-        }
+        P->rc = rbc_validate_batch(ctx, count, sh.data(), sl.data(), ix.data(), brs.data(), bl.data(), rts.data(),
+                                   P->ok.data(), &P->ticket);
     } else {
         // interpolate: klauspost argument checks per request, then one batch
         // over the requests that pass them
-        std::vector<int> idx;
         std::vector<size_t> S(count, 0);
         for (int i = 0; i < count; ++i) {
             Req &r = b[i];
@@ -155,49 +159,85 @@ void rbc_batcher::process(Kind kind, std::vector<Req> &b) {
             int rc = check_shards_sizes(r.in_lens, &S[i]);
             if (!rc && present < k) rc = RBC_ERR_TOO_FEW_SHARDS;
             if (!rc && r.value_cap < (size_t)k * S[i]) rc = RBC_ERR_INVALID_ARG;
-            if (rc) st[i] = rc;
-            else idx.push_back(i);
+            if (rc) P->st[i] = rc;
+            else P->idx.push_back(i);
         }
-        const int m = (int)idx.size();
+        const int m = (int)P->idx.size();
         if (m) {
-            size_t Smax = 1;
-            for (int i : idx) Smax = std::max(Smax, S[i]);
-            std::vector<uint8_t> shards((size_t)m * n * Smax, 0), present((size_t)m * n, 0), roots((size_t)m * 32),
-                values((size_t)m * k * Smax), digests((size_t)m * 32);
-            std::vector<size_t> lens(m);
-            std::vector<int32_t> status(m, 0);
+            for (int i : P->idx) P->Smax = std::max(P->Smax, S[i]);
+            const size_t Smax = P->Smax;
+            P->shards.assign((size_t)m * n * Smax, 0);
+            P->present.assign((size_t)m * n, 0);
+            P->roots.resize((size_t)m * 32);
+            P->values.resize((size_t)m * k * Smax);
+            P->digests.resize((size_t)m * 32);
+            P->lens.resize(m);
+            P->status.assign(m, 0);
             for (int t = 0; t < m; ++t) {
-                Req &r = b[idx[t]];
-                lens[t] = S[idx[t]];
+                Req &r = b[P->idx[t]];
+                P->lens[t] = S[P->idx[t]];
                 for (int j = 0; j < n; ++j)
                     if (r.in_lens[j]) {
-                        memcpy(shards.data() + ((size_t)t * n + j) * Smax, r.in_shards[j], lens[t]);
-                        present[(size_t)t * n + j] = 1;
+                        memcpy(P->shards.data() + ((size_t)t * n + j) * Smax, r.in_shards[j], P->lens[t]);
+                        P->present[(size_t)t * n + j] = 1;
                     }
-                memcpy(roots.data() + (size_t)t * 32, r.root, 32);
+                memcpy(P->roots.data() + (size_t)t * 32, r.root, 32);
             }
-            uint64_t tk = 0;
-            const int rc = rbc_interpolate_batch(ctx, m, shards.data(), Smax, lens.data(), present.data(), roots.data(),
-                                                 values.data(), (size_t)k * Smax, digests.data(), status.data(), &tk);
-            for (int t = 0; t < m; ++t) {
-                Req &r = b[idx[t]];
-                int s = rc ? rc : status[t];
-                st[idx[t]] = s;
-                if (s) continue;
-                memcpy(r.value_out, values.data() + (size_t)t * k * Smax, (size_t)k * lens[t]);
-                if (r.value_len) *r.value_len = (size_t)k * lens[t];
-                if (r.digest_out) memcpy(r.digest_out, digests.data() + (size_t)t * 32, 32);
-            }
+            P->rc = rbc_interpolate_batch(ctx, m, P->shards.data(), Smax, P->lens.data(), P->present.data(),
+                                          P->roots.data(), P->values.data(), (size_t)k * Smax, P->digests.data(),
+                                          P->status.data(), &P->ticket);
+        }
+    }
+    return P;
+}
+
+void rbc_batcher::finish(Pending &P) {
+    int rc = P.rc;
+    if (!rc && P.ticket) rc = rbc_wait(ctx, P.ticket);
+    const int count = (int)P.reqs.size();
+    std::vector<Req> &b = P.reqs;
+    if (P.kind == K_SHARD) {
+        for (int i = 0; i < count; ++i) {
+            Req &r = b[i];
+            if (rc) { P.st[i] = rc; continue; }
+            const size_t S = P.slens[i];
+            if (r.shards_cap < (size_t)n * S) { P.st[i] = RBC_ERR_INVALID_ARG; continue; }
+            for (int j = 0; j < n; ++j)
+                memcpy(r.shards_out + (size_t)j * S, P.shards.data() + ((size_t)i * n + j) * P.Smax, S);
+            if (r.shard_len_out) *r.shard_len_out = S;
+            memcpy(r.root_out, P.roots.data() + (size_t)i * 32, 32);
+            if (r.branches_out && depth)
+                memcpy(r.branches_out, P.br.data() + (size_t)i * n * depth * 32, (size_t)n * depth * 32);
+        }
+    } else if (P.kind == K_VALIDATE) {
+        for (int i = 0; i < count; ++i) {
+            if (rc) P.st[i] = rc;
+            else *b[i].ok_out = P.ok[i];
+        }
+    } else {
+        for (int t = 0; t < (int)P.idx.size(); ++t) {
+            Req &r = b[P.idx[t]];
+            const int s = rc ? rc : P.status[t];
+            P.st[P.idx[t]] = s;
+            if (s) continue;
+            memcpy(r.value_out, P.values.data() + (size_t)t * k * P.Smax, (size_t)k * P.lens[t]);
+            if (r.value_len) *r.value_len = (size_t)k * P.lens[t];
+            if (r.digest_out) memcpy(r.digest_out, P.digests.data() + (size_t)t * 32, 32);
         }
     }
     std::lock_guard<std::mutex> lk(mu);
-    for (int i = 0; i < count; ++i) done[b[i].ticket] = st[i];
+    for (int i = 0; i < count; ++i) done[b[i].ticket] = P.st[i];
     batches++;
     requests += count;
     cv_done.notify_all();
 }
 
+// Worker: coalesce, submit asynchronously, and complete launches in order.
+// Up to `depth` launches are in flight, so the host-side staging of batch
+// t+1 overlaps the GPU work (and copies) of batch t.
 void rbc_batcher::run() {
+    std::deque<std::unique_ptr<Pending>> inflight;
+    const size_t depth_max = 2;
     std::unique_lock<std::mutex> lk(mu);
     while (true) {
         // pick the kind whose queue is full, or whose oldest request is due
@@ -211,6 +251,13 @@ void rbc_batcher::run() {
             earliest = std::min(earliest, due);
         }
         if (pick < 0) {
+            if (!inflight.empty()) {  // nothing new is due: complete what runs
+                lk.unlock();
+                finish(*inflight.front());
+                inflight.pop_front();
+                lk.lock();
+                continue;
+            }
             if (stop) return;
             cv_work.wait_until(lk, earliest);
             continue;
@@ -221,7 +268,11 @@ void rbc_batcher::run() {
             q[pick].pop_front();
         }
         lk.unlock();
-        process((Kind)pick, batch);
+        inflight.push_back(submit((Kind)pick, std::move(batch)));
+        if (inflight.size() >= depth_max) {
+            finish(*inflight.front());
+            inflight.pop_front();
+        }
         lk.lock();
     }
 }

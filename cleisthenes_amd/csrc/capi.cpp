@@ -12,7 +12,10 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <functional>
+#include <memory>
 #include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/rbc_gpu.h"
@@ -95,6 +98,63 @@ struct DevBuf {
     template <class T> T *as() const { return reinterpret_cast<T *>(p); }
 };
 
+// Interpolate's decode workspace and its fork resources (aux stream for the
+// value assembly beside the regen hashing).  One per independent stream of
+// work: the context's device API has one, every host-API slot has its own.
+struct Ws {
+    DevBuf used, regen, dmat, nmiss, flags, list, counter, rcount, cls;
+    hipStream_t aux = nullptr;  // created on first use
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    bool init() {
+        return hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) == hipSuccess &&
+               hipEventCreateWithFlags(&ev_join, hipEventDisableTiming) == hipSuccess;
+    }
+    void release() {
+        for (DevBuf *b : {&used, &regen, &dmat, &nmiss, &flags, &list, &counter, &rcount, &cls}) b->release();
+        if (aux) (void)hipStreamDestroy(aux);
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
+        if (ev_join) (void)hipEventDestroy(ev_join);
+        aux = nullptr;
+        ev_fork = ev_join = nullptr;
+    }
+};
+
+// One in-flight host-API submission (the Go batcher's entry points): its own
+// stream, device buffers, pinned staging both ways and decode workspace, so
+// consecutive batches pipeline -- batch t+1 is staged and its H2D runs while
+// batch t computes.  `finish` copies the pinned results into the caller's
+// buffers at completion (rbc_wait / rbc_poll / slot reuse).
+struct Slot {
+    DevBuf d_values, d_shards, d_leaves, d_roots, d_branches, d_valid, d_status, d_digests, d_lens, d_slens, d_idx;
+    DevBuf h_in{nullptr, 0, true}, h_out{nullptr, 0, true};
+    Ws ws;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    uint64_t ticket = 0;
+    bool busy = false;
+    std::function<int()> finish;
+    void release() {
+        for (DevBuf *b : {&d_values, &d_shards, &d_leaves, &d_roots, &d_branches, &d_valid, &d_status, &d_digests,
+                          &d_lens, &d_slens, &d_idx, &h_in, &h_out})
+            b->release();
+        ws.release();
+        if (stream) (void)hipStreamDestroy(stream);
+        if (done) (void)hipEventDestroy(done);
+        stream = nullptr;
+        done = nullptr;
+    }
+};
+
+// host-API submissions in flight per context (RBC_HOST_SLOTS, default 2)
+int host_slots() {
+    static const int v = [] {
+        const char *e = getenv("RBC_HOST_SLOTS");
+        int x = e ? atoi(e) : 0;
+        return (x >= 1 && x <= 8) ? x : 2;
+    }();
+    return v;
+}
+
 }  // namespace
 
 struct rbc_ctx {
@@ -103,16 +163,15 @@ struct rbc_ctx {
     std::vector<uint8_t> h_M;      // n x k encode matrix
     uint8_t *d_M = nullptr;        // device copy; parity rows at d_M + k*k
     std::mutex mu;
-    hipStream_t stream = nullptr;  // host-API stream
-    hipStream_t aux = nullptr;     // fork stream inside interpolate (join beside the regen hashing)
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    // interpolate workspace (device API)
-    DevBuf ws_used, ws_regen, ws_dmat, ws_nmiss, ws_flags, ws_list, ws_counter, ws_rcount, ws_cls;
+    hipStream_t stream = nullptr;  // Encoder-mirror stream (created on first use)
+    Ws ws;                         // interpolate workspace of the device API
     // host-API staging
     DevBuf d_values, d_shards, d_leaves, d_roots, d_branches, d_valid, d_status, d_digests, d_lens, d_slens,
         d_idx, d_present;
     DevBuf h_stage{nullptr, 0, true}, h_small{nullptr, 0, true};
     uint64_t next_ticket = 1;
+    std::vector<std::unique_ptr<Slot>> slots;        // host-API pipeline
+    std::unordered_map<uint64_t, int> retired;       // completed tickets not yet waited on
     // RCCL
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -151,8 +210,7 @@ int ctx_create_kn(int n, int k, int device, rbc_ctx **out) {
     }
     if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->d_M, up.size()) != hipSuccess ||
         hipMemcpy(c->d_M, up.data(), up.size(), hipMemcpyHostToDevice) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+        !c->ws.init()) {
         if (c->d_M) (void)hipFree(c->d_M);
         delete c;
         return RBC_ERR_DEVICE;
@@ -171,9 +229,9 @@ hipStream_t host_stream(rbc_ctx *c) {
     if (!c->stream && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) c->stream = nullptr;
     return c->stream;
 }
-hipStream_t aux_stream(rbc_ctx *c) {
-    if (!c->aux && hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) c->aux = nullptr;
-    return c->aux;
+hipStream_t aux_stream(Ws &w) {
+    if (!w.aux && hipStreamCreateWithFlags(&w.aux, hipStreamNonBlocking) != hipSuccess) w.aux = nullptr;
+    return w.aux;
 }
 
 // ------------------------------------------------------------ stage bodies
@@ -296,29 +354,29 @@ int stage_verify(rbc_ctx *c, hipStream_t st, int count, const uint8_t *shards, u
     return RBC_OK;
 }
 
-int ensure_ws(rbc_ctx *c, int count) {
+int ensure_ws(rbc_ctx *c, Ws &w, int count) {
     const size_t nr = (size_t)std::max(c->n - c->k, 1);
-    RBC_HIP(c->ws_used.ensure((size_t)count * c->k));
-    RBC_HIP(c->ws_regen.ensure((size_t)count * nr));
-    RBC_HIP(c->ws_dmat.ensure((size_t)count * nr * c->k));
-    RBC_HIP(c->ws_nmiss.ensure((size_t)count * 4));
-    RBC_HIP(c->ws_flags.ensure((size_t)count * c->n * 4));
-    RBC_HIP(c->ws_list.ensure((size_t)count * nr * 4));
-    RBC_HIP(c->ws_counter.ensure(16));
-    RBC_HIP(c->ws_rcount.ensure((size_t)count * 4));
-    RBC_HIP(c->ws_cls.ensure((size_t)count * round_up(c->n, 4)));
+    RBC_HIP(w.used.ensure((size_t)count * c->k));
+    RBC_HIP(w.regen.ensure((size_t)count * nr));
+    RBC_HIP(w.dmat.ensure((size_t)count * nr * c->k));
+    RBC_HIP(w.nmiss.ensure((size_t)count * 4));
+    RBC_HIP(w.flags.ensure((size_t)count * c->n * 4));
+    RBC_HIP(w.list.ensure((size_t)count * nr * 4));
+    RBC_HIP(w.counter.ensure(16));
+    RBC_HIP(w.rcount.ensure((size_t)count * 4));
+    RBC_HIP(w.cls.ensure((size_t)count * round_up(c->n, 4)));
     return RBC_OK;
 }
 
 // decode_prepare + GF regeneration (in place), no hashing
 // compare != 0: valid-but-unused rows are compared, not blindly rewritten,
 // and the rows that need hashing are collected in ws_list
-int stage_regenerate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, uint32_t shard_pitch,
+int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shards, uint32_t shard_pitch,
                      const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *valid,
                      int32_t *status, int compare = 0, uint8_t *values_out = nullptr, uint32_t value_pitch = 0) {
-    int rc = ensure_ws(c, count);
+    int rc = ensure_ws(c, w, count);
     if (rc) return rc;
-    if (compare) RBC_HIP(hipMemsetAsync(c->ws_counter.p, 0, 16, st));
+    if (compare) RBC_HIP(hipMemsetAsync(w.counter.p, 0, 16, st));
     const int nr = c->n - c->k;
     PrepArgs pa{};
     pa.count = count;
@@ -327,23 +385,23 @@ int stage_regenerate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, uin
     pa.valid = valid;
     pa.valid_stride = (uint32_t)c->n;
     pa.M = c->d_M;
-    pa.used = c->ws_used.as<uint8_t>();
+    pa.used = w.used.as<uint8_t>();
     pa.used_stride = (uint32_t)c->k;
-    pa.regen = c->ws_regen.as<uint8_t>();
+    pa.regen = w.regen.as<uint8_t>();
     pa.regen_stride = (uint32_t)std::max(nr, 1);
-    pa.dmat = c->ws_dmat.as<uint8_t>();
+    pa.dmat = w.dmat.as<uint8_t>();
     pa.dmat_stride = (uint64_t)std::max(nr, 1) * c->k;
     pa.status = status;
     if (compare) {
-        pa.nmiss = c->ws_nmiss.as<int32_t>();
-        pa.flags = c->ws_flags.as<uint32_t>();
-        pa.list = c->ws_list.as<uint32_t>();
-        pa.counter = c->ws_counter.as<uint32_t>();
+        pa.nmiss = w.nmiss.as<int32_t>();
+        pa.flags = w.flags.as<uint32_t>();
+        pa.list = w.list.as<uint32_t>();
+        pa.counter = w.counter.as<uint32_t>();
     }
     if (c->fft) {
         pa.fft = 1;
-        pa.rcount = c->ws_rcount.as<int32_t>();
-        pa.cls = c->ws_cls.as<uint8_t>();
+        pa.rcount = w.rcount.as<int32_t>();
+        pa.cls = w.cls.as<uint8_t>();
         pa.cls_stride = (uint32_t)round_up(c->n, 4);
         pa.gf_exp = c->d_M + c->h_M.size();
         pa.gf_log = pa.gf_exp + 512;
@@ -438,7 +496,7 @@ int stage_regenerate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, uin
     return RBC_OK;
 }
 
-int stage_interpolate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, uint32_t shard_pitch,
+int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shards, uint32_t shard_pitch,
                       const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *valid, uint8_t *leaves,
                       int leaves_verified, const uint8_t *roots, uint8_t *values_out, uint32_t value_pitch,
                       uint8_t *digests, int32_t *status) {
@@ -459,16 +517,16 @@ int stage_interpolate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, ui
         return e && atoi(e) != 0;
     }();
     const bool fused_join = fuse_env && c->fft && c->n > c->k;
-    int rc = stage_regenerate(c, st, count, shards, shard_pitch, shard_lens, uniform_shard_len, valid, status,
+    int rc = stage_regenerate(c, w, st, count, shards, shard_pitch, shard_lens, uniform_shard_len, valid, status,
                               leaves_verified, fused_join ? values_out : nullptr, value_pitch);
     if (rc) return rc;
     // value assembly (HBM-bound) forks onto the aux stream beside the regen
     // hashing (latency-bound, under-fills the SIMDs); it needs only the
     // regenerated rows.  values_out is defined where status == 0.
     if (!fused_join) {
-    if (!aux_stream(c)) return RBC_ERR_DEVICE;
-    RBC_HIP(hipEventRecord(c->ev_fork, st));
-    RBC_HIP(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+    if (!aux_stream(w)) return RBC_ERR_DEVICE;
+    RBC_HIP(hipEventRecord(w.ev_fork, st));
+    RBC_HIP(hipStreamWaitEvent(w.aux, w.ev_fork, 0));
     {
         JoinArgs j{};
         j.count = count;
@@ -483,9 +541,9 @@ int stage_interpolate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, ui
         j.values = values_out;
         j.value_pitch = value_pitch;
         j.status = status;
-        RBC_HIP(rbc_launch_join(j, c->aux));
+        RBC_HIP(rbc_launch_join(j, w.aux));
     }
-    RBC_HIP(hipEventRecord(c->ev_join, c->aux));
+    RBC_HIP(hipEventRecord(w.ev_join, w.aux));
     }
     const int nr = c->n - c->k;
     ShaArgs a{};
@@ -504,8 +562,8 @@ int stage_interpolate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, ui
         // hash only the rows in the device-built list: every missing position
         // plus any valid-but-unused shard the re-encoding disagreed with
         a.rows_per_inst = nr;  // grid bound (count * nr entries at most)
-        a.list = c->ws_list.as<uint32_t>();
-        a.list_count = c->ws_counter.as<uint32_t>();
+        a.list = w.list.as<uint32_t>();
+        a.list_count = w.counter.as<uint32_t>();
     } else {
         a.rows_per_inst = c->n;
     }
@@ -523,7 +581,7 @@ int stage_interpolate(rbc_ctx *c, hipStream_t st, int count, uint8_t *shards, ui
     RBC_HIP(rbc_launch_merkle(m, true, st));
     if (digests)
         RBC_HIP(rbc_launch_digest(leaves, (uint64_t)c->n * 32, c->k, status, digests, count, st));
-    if (!fused_join) RBC_HIP(hipStreamWaitEvent(st, c->ev_join, 0));  // join back before returning
+    if (!fused_join) RBC_HIP(hipStreamWaitEvent(st, w.ev_join, 0));  // join back before returning
     return RBC_OK;
 }
 
@@ -569,7 +627,7 @@ int host_reconstruct(rbc_ctx *c, uint8_t *const *shards, size_t *lens, int n_sha
     if (!st) return RBC_ERR_DEVICE;
     RBC_HIP(hipMemcpyAsync(c->d_shards.p, stage, (size_t)c->n * pitch, hipMemcpyHostToDevice, st));
     RBC_HIP(hipMemcpyAsync(c->d_valid.p, stage + (size_t)c->n * pitch, c->n, hipMemcpyHostToDevice, st));
-    rc = stage_regenerate(c, st, 1, c->d_shards.as<uint8_t>(), (uint32_t)pitch, nullptr, (uint32_t)S,
+    rc = stage_regenerate(c, c->ws, st, 1, c->d_shards.as<uint8_t>(), (uint32_t)pitch, nullptr, (uint32_t)S,
                           c->d_valid.as<uint8_t>(), c->d_status.as<int32_t>());
     if (rc) return rc;
     RBC_HIP(hipMemcpyAsync(stage, c->d_shards.p, (size_t)c->n * pitch, hipMemcpyDeviceToHost, st));
@@ -631,16 +689,17 @@ void rbc_ctx_destroy(rbc_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->comm) (void)ncclCommDestroy(c->comm);
-    for (DevBuf *b : {&c->ws_used, &c->ws_regen, &c->ws_dmat, &c->ws_nmiss, &c->ws_flags, &c->ws_list,
-                      &c->ws_counter, &c->ws_rcount, &c->ws_cls, &c->d_values, &c->d_shards, &c->d_leaves,
+    for (auto &sl : c->slots) {
+        if (sl->busy) (void)hipEventSynchronize(sl->done);
+        sl->release();
+    }
+    c->ws.release();
+    for (DevBuf *b : {&c->d_values, &c->d_shards, &c->d_leaves,
                       &c->d_roots, &c->d_branches, &c->d_valid, &c->d_status, &c->d_digests, &c->d_lens,
                       &c->d_slens, &c->d_idx, &c->d_present, &c->h_stage, &c->h_small, &c->d_pack})
         b->release();
     if (c->d_M) (void)hipFree(c->d_M);
     if (c->stream) (void)hipStreamDestroy(c->stream);
-    if (c->aux) (void)hipStreamDestroy(c->aux);
-    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     delete c;
 }
 
@@ -790,7 +849,7 @@ int rbc_dev_interpolate(rbc_ctx *c, void *stream, int count, uint8_t *shards, ui
     if (!c) return RBC_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(c->mu);  // shared decode workspace
     RBC_HIP(hipSetDevice(c->device));
-    return stage_interpolate(c, as_stream(stream), count, shards, shard_pitch, shard_lens, uniform_shard_len, valid,
+    return stage_interpolate(c, c->ws, as_stream(stream), count, shards, shard_pitch, shard_lens, uniform_shard_len, valid,
                              leaves, leaves_verified, roots, values_out, value_pitch, digests, status);
 }
 
@@ -803,7 +862,58 @@ int rbc_dev_inject_faults(rbc_ctx *c, void *stream, int count, uint8_t *shards, 
     return RBC_OK;
 }
 
-// ---- host-memory batch API
+// ---- host-memory batch API (pipelined through per-context slots)
+namespace {
+
+// Free slot for the next submission: create one while fewer than
+// host_slots() exist, else reuse an idle one, else retire the oldest
+// in-flight submission (its status is kept until the caller waits on it).
+int retire(rbc_ctx *c, Slot &s) {
+    int st = RBC_OK;
+    if (hipEventSynchronize(s.done) != hipSuccess) st = RBC_ERR_DEVICE;
+    if (st == RBC_OK && s.finish) st = s.finish();
+    s.finish = nullptr;
+    s.busy = false;
+    return st;
+}
+
+Slot *acquire_slot(rbc_ctx *c) {
+    for (auto &sl : c->slots)
+        if (!sl->busy) return sl.get();
+    if ((int)c->slots.size() < host_slots()) {
+        auto sl = std::make_unique<Slot>();
+        if (hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&sl->done, hipEventDisableTiming) != hipSuccess || !sl->ws.init()) {
+            sl->release();
+            return nullptr;
+        }
+        c->slots.push_back(std::move(sl));
+        return c->slots.back().get();
+    }
+    Slot *old = nullptr;
+    for (auto &sl : c->slots)
+        if (!old || sl->ticket < old->ticket) old = sl.get();
+    c->retired[old->ticket] = retire(c, *old);
+    return old;
+}
+
+// Seal a submission: record its completion event and hand out a ticket, or
+// (ticket == NULL) complete it before returning.
+int submit(rbc_ctx *c, Slot &s, uint64_t *ticket, std::function<int()> finish) {
+    s.finish = std::move(finish);
+    if (hipEventRecord(s.done, s.stream) != hipSuccess) {
+        s.finish = nullptr;
+        return RBC_ERR_DEVICE;
+    }
+    s.ticket = c->next_ticket++;
+    s.busy = true;
+    if (!ticket) return retire(c, s);
+    *ticket = s.ticket;
+    return RBC_OK;
+}
+
+}  // namespace
+
 int rbc_shard_commit(rbc_ctx *c, int count, const uint8_t *const *values, const size_t *value_lens,
                      uint8_t *shards_out, size_t shard_pitch, uint32_t *shard_lens_out, uint8_t *roots_out,
                      uint8_t *branches_out, uint64_t *ticket) {
@@ -817,51 +927,58 @@ int rbc_shard_commit(rbc_ctx *c, int count, const uint8_t *const *values, const 
         Smax = std::max(Smax, (value_lens[i] + c->k - 1) / c->k);
     }
     if (shard_pitch < Smax) return RBC_ERR_INVALID_ARG;
-    const size_t dpitch = round_up(Smax, kAlign);
+    const size_t dpitch = round_up(Smax, 128);  // whole HBM lines per row
     const size_t vpitch = round_up((size_t)c->k * Smax + 32, kAlign);
     if (vpitch > 0x7fffffffULL || (size_t)c->n * dpitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
+    const int d = c->depth, n = c->n;
+    const size_t sh_bytes = (size_t)count * n * dpitch, br_bytes = (size_t)count * n * std::max(d, 1) * 32;
     std::lock_guard<std::mutex> lk(c->mu);
     RBC_HIP(hipSetDevice(c->device));
-    hipStream_t st = host_stream(c);
-    if (!st) return RBC_ERR_DEVICE;
-    RBC_HIP(c->d_values.ensure((size_t)count * vpitch));
-    RBC_HIP(c->d_shards.ensure((size_t)count * c->n * dpitch));
-    RBC_HIP(c->d_leaves.ensure((size_t)count * c->n * 32));
-    RBC_HIP(c->d_roots.ensure((size_t)count * 32));
-    RBC_HIP(c->d_branches.ensure((size_t)count * c->n * std::max(c->depth, 1) * 32));
-    RBC_HIP(c->d_lens.ensure((size_t)count * 4));
-    RBC_HIP(c->d_slens.ensure((size_t)count * 4));
-    RBC_HIP(c->h_stage.ensure((size_t)count * vpitch));
-    RBC_HIP(c->h_small.ensure((size_t)count * 8));
-    uint8_t *stage = c->h_stage.as<uint8_t>();
-    uint32_t *lens = c->h_small.as<uint32_t>();
+    Slot *sp = acquire_slot(c);
+    if (!sp) return RBC_ERR_DEVICE;
+    Slot &s = *sp;
+    hipStream_t st = s.stream;
+    RBC_HIP(s.d_values.ensure((size_t)count * vpitch));
+    RBC_HIP(s.d_shards.ensure(sh_bytes));
+    RBC_HIP(s.d_leaves.ensure((size_t)count * n * 32));
+    RBC_HIP(s.d_roots.ensure((size_t)count * 32));
+    RBC_HIP(s.d_branches.ensure(br_bytes));
+    RBC_HIP(s.d_lens.ensure((size_t)count * 8));
+    RBC_HIP(s.h_in.ensure((size_t)count * vpitch + (size_t)count * 8));
+    RBC_HIP(s.h_out.ensure(sh_bytes + (size_t)count * 32 + br_bytes));
+    uint8_t *stage = s.h_in.as<uint8_t>();
+    uint32_t *lens = reinterpret_cast<uint32_t *>(stage + (size_t)count * vpitch);
     for (int i = 0; i < count; ++i) {
         memcpy(stage + (size_t)i * vpitch, values[i], value_lens[i]);
         memset(stage + (size_t)i * vpitch + value_lens[i], 0, vpitch - value_lens[i]);
         lens[i] = (uint32_t)value_lens[i];
         lens[count + i] = (uint32_t)((value_lens[i] + c->k - 1) / c->k);
     }
-    RBC_HIP(hipMemcpyAsync(c->d_values.p, stage, (size_t)count * vpitch, hipMemcpyHostToDevice, st));
-    RBC_HIP(hipMemcpyAsync(c->d_lens.p, lens, (size_t)count * 4, hipMemcpyHostToDevice, st));
-    RBC_HIP(hipMemcpyAsync(c->d_slens.p, lens + count, (size_t)count * 4, hipMemcpyHostToDevice, st));
-    int rc = stage_encode(c, st, count, c->d_values.as<uint8_t>(), vpitch, c->d_lens.as<uint32_t>(), 0,
-                          c->d_shards.as<uint8_t>(), (uint32_t)dpitch);
-    if (!rc) rc = stage_leaves(c, st, count, c->d_shards.as<uint8_t>(), (uint32_t)dpitch, c->d_slens.as<uint32_t>(),
-                               0, c->d_leaves.as<uint8_t>());
-    if (!rc) rc = stage_merkle_build(c, st, count, c->d_leaves.as<uint8_t>(), c->d_roots.as<uint8_t>(),
-                                     c->d_branches.as<uint8_t>());
+    RBC_HIP(hipMemcpyAsync(s.d_values.p, stage, (size_t)count * vpitch, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(s.d_lens.p, lens, (size_t)count * 8, hipMemcpyHostToDevice, st));
+    const uint32_t *d_vlens = s.d_lens.as<uint32_t>(), *d_slens = d_vlens + count;
+    int rc = stage_encode(c, st, count, s.d_values.as<uint8_t>(), vpitch, d_vlens, 0, s.d_shards.as<uint8_t>(),
+                          (uint32_t)dpitch);
+    if (!rc) rc = stage_leaves(c, st, count, s.d_shards.as<uint8_t>(), (uint32_t)dpitch, d_slens, 0,
+                               s.d_leaves.as<uint8_t>());
+    if (!rc) rc = stage_merkle_build(c, st, count, s.d_leaves.as<uint8_t>(), s.d_roots.as<uint8_t>(),
+                                     s.d_branches.as<uint8_t>());
     if (rc) return rc;
-    RBC_HIP(hipMemcpy2DAsync(shards_out, shard_pitch, c->d_shards.p, dpitch, Smax, (size_t)count * c->n,
-                             hipMemcpyDeviceToHost, st));
-    RBC_HIP(hipMemcpyAsync(roots_out, c->d_roots.p, (size_t)count * 32, hipMemcpyDeviceToHost, st));
-    if (branches_out && c->depth > 0)
-        RBC_HIP(hipMemcpyAsync(branches_out, c->d_branches.p, (size_t)count * c->n * c->depth * 32,
-                               hipMemcpyDeviceToHost, st));
-    RBC_HIP(hipStreamSynchronize(st));
-    if (shard_lens_out)
-        for (int i = 0; i < count; ++i) shard_lens_out[i] = lens[count + i];
-    if (ticket) *ticket = c->next_ticket++;
-    return RBC_OK;
+    uint8_t *o_sh = s.h_out.as<uint8_t>(), *o_rt = o_sh + sh_bytes, *o_br = o_rt + (size_t)count * 32;
+    RBC_HIP(hipMemcpyAsync(o_sh, s.d_shards.p, sh_bytes, hipMemcpyDeviceToHost, st));
+    RBC_HIP(hipMemcpyAsync(o_rt, s.d_roots.p, (size_t)count * 32, hipMemcpyDeviceToHost, st));
+    if (branches_out && d > 0) RBC_HIP(hipMemcpyAsync(o_br, s.d_branches.p, br_bytes, hipMemcpyDeviceToHost, st));
+    return submit(c, s, ticket, [=]() {
+        for (int i = 0; i < count; ++i) {
+            const size_t S = lens[count + i];
+            for (int j = 0; j < n; ++j)  // Smax bytes per row: the device rows are zero past S_i
+                memcpy(shards_out + ((size_t)i * n + j) * shard_pitch, o_sh + ((size_t)i * n + j) * dpitch, Smax);
+            if (shard_lens_out) shard_lens_out[i] = (uint32_t)S;
+        }
+        memcpy(roots_out, o_rt, (size_t)count * 32);
+        if (branches_out && d > 0) memcpy(branches_out, o_br, (size_t)count * n * d * 32);
+        return RBC_OK;
+    });
 }
 
 int rbc_validate_batch(rbc_ctx *c, int count, const uint8_t *const *shards, const size_t *shard_lens,
@@ -876,30 +993,35 @@ int rbc_validate_batch(rbc_ctx *c, int count, const uint8_t *const *shards, cons
     for (int i = 0; i < count; ++i) Smax = std::max(Smax, shard_lens[i]);
     const size_t pitch = round_up(Smax, kAlign);
     const size_t bslot = (size_t)std::max(d, 1) * 32;
+    if ((size_t)count * pitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
     RBC_HIP(hipSetDevice(c->device));
-    hipStream_t st = host_stream(c);
-    if (!st) return RBC_ERR_DEVICE;
+    Slot *sp = acquire_slot(c);
+    if (!sp) return RBC_ERR_DEVICE;
+    Slot &s = *sp;
+    hipStream_t st = s.stream;
     const size_t stage_bytes = (size_t)count * (pitch + bslot + 32 + 4 + 1);
-    RBC_HIP(c->h_stage.ensure(stage_bytes));
-    RBC_HIP(c->d_shards.ensure((size_t)count * pitch));
-    RBC_HIP(c->d_branches.ensure((size_t)count * bslot));
-    RBC_HIP(c->d_roots.ensure((size_t)count * 32));
-    RBC_HIP(c->d_slens.ensure((size_t)count * 4));
-    RBC_HIP(c->d_idx.ensure((size_t)count));
-    RBC_HIP(c->d_valid.ensure((size_t)count));
-    uint8_t *sh = c->h_stage.as<uint8_t>();
+    RBC_HIP(s.h_in.ensure(stage_bytes));
+    RBC_HIP(s.h_out.ensure((size_t)count * 2));
+    RBC_HIP(s.d_shards.ensure((size_t)count * pitch));
+    RBC_HIP(s.d_branches.ensure((size_t)count * bslot));
+    RBC_HIP(s.d_roots.ensure((size_t)count * 32));
+    RBC_HIP(s.d_slens.ensure((size_t)count * 4));
+    RBC_HIP(s.d_idx.ensure((size_t)count));
+    RBC_HIP(s.d_valid.ensure((size_t)count));
+    uint8_t *sh = s.h_in.as<uint8_t>();
     uint8_t *br = sh + (size_t)count * pitch;
     uint8_t *rt = br + (size_t)count * bslot;
     uint32_t *ln = reinterpret_cast<uint32_t *>(rt + (size_t)count * 32);
     uint8_t *ix = reinterpret_cast<uint8_t *>(ln + count);
-    std::vector<uint8_t> shape_ok(count, 1);
+    uint8_t *shape_ok = s.h_out.as<uint8_t>() + count;  // host-side shape verdicts
     memset(sh, 0, stage_bytes);
     for (int i = 0; i < count; ++i) {
         const uint32_t j = indices[i];
         // unflatten the Go-form branch (the empty level-0 sibling is omitted)
         const bool empty0 = d > 0 && (int)(j ^ 1u) >= c->n;
         const size_t want = (size_t)32 * (d - (empty0 ? 1 : 0));
+        shape_ok[i] = 1;
         if ((int)j >= c->n || branch_lens[i] != want || shard_lens[i] == 0 || !shards[i] || !roots[i] ||
             (want && !branches[i])) {
             shape_ok[i] = 0;
@@ -918,34 +1040,34 @@ int rbc_validate_batch(rbc_ctx *c, int count, const uint8_t *const *shards, cons
         ln[i] = (uint32_t)shard_lens[i];
         ix[i] = (uint8_t)j;
     }
-    RBC_HIP(hipMemcpyAsync(c->d_shards.p, sh, (size_t)count * pitch, hipMemcpyHostToDevice, st));
-    RBC_HIP(hipMemcpyAsync(c->d_branches.p, br, (size_t)count * bslot, hipMemcpyHostToDevice, st));
-    RBC_HIP(hipMemcpyAsync(c->d_roots.p, rt, (size_t)count * 32, hipMemcpyHostToDevice, st));
-    RBC_HIP(hipMemcpyAsync(c->d_slens.p, ln, (size_t)count * 4, hipMemcpyHostToDevice, st));
-    RBC_HIP(hipMemcpyAsync(c->d_idx.p, ix, (size_t)count, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(s.d_shards.p, sh, (size_t)count * pitch, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(s.d_branches.p, br, (size_t)count * bslot, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(s.d_roots.p, rt, (size_t)count * 32, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(s.d_slens.p, ln, (size_t)count * 4, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(s.d_idx.p, ix, (size_t)count, hipMemcpyHostToDevice, st));
     ShaArgs a{};
     a.count = count;
     a.rows_per_inst = 1;
-    a.rows = c->d_shards.as<uint8_t>();
+    a.rows = s.d_shards.as<uint8_t>();
     a.inst_pitch = pitch;
     a.row_pitch = 0;
-    a.lens = c->d_slens.as<uint32_t>();
-    a.idx = c->d_idx.as<uint8_t>();
+    a.lens = s.d_slens.as<uint32_t>();
+    a.idx = s.d_idx.as<uint8_t>();
     a.idx_stride = 1;
     a.per_message = 1;
     a.n = c->n;
     a.depth = d;
-    a.branches = c->d_branches.as<uint8_t>();
+    a.branches = s.d_branches.as<uint8_t>();
     a.br_inst_pitch = bslot;
-    a.roots = c->d_roots.as<uint8_t>();
-    a.valid = c->d_valid.as<uint8_t>();
+    a.roots = s.d_roots.as<uint8_t>();
+    a.valid = s.d_valid.as<uint8_t>();
     RBC_HIP(rbc_launch_sha_rows(a, true, st));
-    RBC_HIP(hipMemcpyAsync(ok_out, c->d_valid.p, (size_t)count, hipMemcpyDeviceToHost, st));
-    RBC_HIP(hipStreamSynchronize(st));
-    for (int i = 0; i < count; ++i)
-        if (!shape_ok[i]) ok_out[i] = 0;
-    if (ticket) *ticket = c->next_ticket++;
-    return RBC_OK;
+    uint8_t *o_ok = s.h_out.as<uint8_t>();
+    RBC_HIP(hipMemcpyAsync(o_ok, s.d_valid.p, (size_t)count, hipMemcpyDeviceToHost, st));
+    return submit(c, s, ticket, [=]() {
+        for (int i = 0; i < count; ++i) ok_out[i] = shape_ok[i] ? o_ok[i] : 0;
+        return RBC_OK;
+    });
 }
 
 int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t shard_pitch,
@@ -962,55 +1084,96 @@ int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t s
         Smax = std::max(Smax, shard_lens[i]);
     }
     if (value_pitch < (size_t)c->k * Smax) return RBC_ERR_INVALID_ARG;
-    const size_t dpitch = round_up(Smax, kAlign);
+    const size_t dpitch = round_up(Smax, 128);
     const size_t vpitch = round_up((size_t)c->k * Smax, 16);
     if ((size_t)c->n * dpitch > 0x7fffffffULL || vpitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
+    const int n = c->n, k = c->k;
+    const size_t sh_bytes = (size_t)count * n * dpitch;
     std::lock_guard<std::mutex> lk(c->mu);
     RBC_HIP(hipSetDevice(c->device));
-    hipStream_t st = host_stream(c);
-    if (!st) return RBC_ERR_DEVICE;
-    RBC_HIP(c->d_shards.ensure((size_t)count * c->n * dpitch));
-    RBC_HIP(c->d_valid.ensure((size_t)count * c->n));
-    RBC_HIP(c->d_leaves.ensure((size_t)count * c->n * 32));
-    RBC_HIP(c->d_roots.ensure((size_t)count * 32));
-    RBC_HIP(c->d_values.ensure((size_t)count * vpitch));
-    RBC_HIP(c->d_digests.ensure((size_t)count * 32));
-    RBC_HIP(c->d_status.ensure((size_t)count * 4));
-    RBC_HIP(c->d_slens.ensure((size_t)count * 4));
-    RBC_HIP(c->h_small.ensure((size_t)count * 4));
-    uint32_t *ln = c->h_small.as<uint32_t>();
-    for (int i = 0; i < count; ++i) ln[i] = (uint32_t)shard_lens[i];
-    RBC_HIP(hipMemcpy2DAsync(c->d_shards.p, dpitch, shards, shard_pitch, Smax, (size_t)count * c->n,
-                             hipMemcpyHostToDevice, st));
-    RBC_HIP(hipMemcpyAsync(c->d_valid.p, present, (size_t)count * c->n, hipMemcpyHostToDevice, st));
-    RBC_HIP(hipMemcpyAsync(c->d_roots.p, roots, (size_t)count * 32, hipMemcpyHostToDevice, st));
-    RBC_HIP(hipMemcpyAsync(c->d_slens.p, ln, (size_t)count * 4, hipMemcpyHostToDevice, st));
+    Slot *sp = acquire_slot(c);
+    if (!sp) return RBC_ERR_DEVICE;
+    Slot &s = *sp;
+    hipStream_t st = s.stream;
+    RBC_HIP(s.d_shards.ensure(sh_bytes));
+    RBC_HIP(s.d_valid.ensure((size_t)count * n));
+    RBC_HIP(s.d_leaves.ensure((size_t)count * n * 32));
+    RBC_HIP(s.d_roots.ensure((size_t)count * 32));
+    RBC_HIP(s.d_values.ensure((size_t)count * vpitch));
+    RBC_HIP(s.d_digests.ensure((size_t)count * 32));
+    RBC_HIP(s.d_status.ensure((size_t)count * 4));
+    RBC_HIP(s.d_slens.ensure((size_t)count * 4));
+    RBC_HIP(s.h_in.ensure(sh_bytes + (size_t)count * (n + 32 + 4)));
+    RBC_HIP(s.h_out.ensure((size_t)count * (vpitch + 32 + 4)));
+    uint8_t *i_sh = s.h_in.as<uint8_t>(), *i_pr = i_sh + sh_bytes, *i_rt = i_pr + (size_t)count * n;
+    uint32_t *ln = reinterpret_cast<uint32_t *>(i_rt + (size_t)count * 32);
+    for (int i = 0; i < count; ++i) {
+        ln[i] = (uint32_t)shard_lens[i];
+        for (int j = 0; j < n; ++j) {
+            uint8_t *dst = i_sh + ((size_t)i * n + j) * dpitch;
+            const uint8_t *src = shards + ((size_t)i * n + j) * shard_pitch;
+            memcpy(dst, src, shard_lens[i]);
+            memset(dst + shard_lens[i], 0, dpitch - shard_lens[i]);
+        }
+    }
+    memcpy(i_pr, present, (size_t)count * n);
+    memcpy(i_rt, roots, (size_t)count * 32);
+    RBC_HIP(hipMemcpyAsync(s.d_shards.p, i_sh, sh_bytes, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(s.d_valid.p, i_pr, (size_t)count * n, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(s.d_roots.p, i_rt, (size_t)count * 32, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(s.d_slens.p, ln, (size_t)count * 4, hipMemcpyHostToDevice, st));
     // ragged batch: bytes past k*S_i of a value row are returned as zero
-    RBC_HIP(hipMemsetAsync(c->d_values.p, 0, (size_t)count * vpitch, st));
-    int rc = stage_interpolate(c, st, count, c->d_shards.as<uint8_t>(), (uint32_t)dpitch, c->d_slens.as<uint32_t>(),
-                               0, c->d_valid.as<uint8_t>(), c->d_leaves.as<uint8_t>(), 0, c->d_roots.as<uint8_t>(),
-                               c->d_values.as<uint8_t>(), (uint32_t)vpitch, c->d_digests.as<uint8_t>(),
-                               c->d_status.as<int32_t>());
+    RBC_HIP(hipMemsetAsync(s.d_values.p, 0, (size_t)count * vpitch, st));
+    int rc = stage_interpolate(c, s.ws, st, count, s.d_shards.as<uint8_t>(), (uint32_t)dpitch,
+                               s.d_slens.as<uint32_t>(), 0, s.d_valid.as<uint8_t>(), s.d_leaves.as<uint8_t>(), 0,
+                               s.d_roots.as<uint8_t>(), s.d_values.as<uint8_t>(), (uint32_t)vpitch,
+                               s.d_digests.as<uint8_t>(), s.d_status.as<int32_t>());
     if (rc) return rc;
-    RBC_HIP(hipMemcpyAsync(status_out, c->d_status.p, (size_t)count * 4, hipMemcpyDeviceToHost, st));
-    RBC_HIP(hipMemcpy2DAsync(values_out, value_pitch, c->d_values.p, vpitch, (size_t)c->k * Smax, count,
-                             hipMemcpyDeviceToHost, st));
-    if (digests_out)
-        RBC_HIP(hipMemcpyAsync(digests_out, c->d_digests.p, (size_t)count * 32, hipMemcpyDeviceToHost, st));
-    RBC_HIP(hipStreamSynchronize(st));
-    if (ticket) *ticket = c->next_ticket++;
-    return RBC_OK;
+    uint8_t *o_val = s.h_out.as<uint8_t>(), *o_dig = o_val + (size_t)count * vpitch;
+    int32_t *o_st = reinterpret_cast<int32_t *>(o_dig + (size_t)count * 32);
+    RBC_HIP(hipMemcpyAsync(o_val, s.d_values.p, (size_t)count * vpitch, hipMemcpyDeviceToHost, st));
+    RBC_HIP(hipMemcpyAsync(o_dig, s.d_digests.p, (size_t)count * 32, hipMemcpyDeviceToHost, st));
+    RBC_HIP(hipMemcpyAsync(o_st, s.d_status.p, (size_t)count * 4, hipMemcpyDeviceToHost, st));
+    return submit(c, s, ticket, [=]() {
+        memcpy(status_out, o_st, (size_t)count * 4);
+        for (int i = 0; i < count; ++i)
+            memcpy(values_out + (size_t)i * value_pitch, o_val + (size_t)i * vpitch, (size_t)k * Smax);
+        if (digests_out) memcpy(digests_out, o_dig, (size_t)count * 32);
+        return RBC_OK;
+    });
 }
 
-// Round 1: host-API submissions complete before returning (tickets are
-// already done); rbc_wait/rbc_poll keep the Go batcher's contract stable.
+// A ticket completes (its outputs land in the caller's buffers) in rbc_wait,
+// in an rbc_poll that finds it done, or when its slot is needed again.
 int rbc_wait(rbc_ctx *c, uint64_t ticket) {
-    if (!c || ticket >= c->next_ticket) return RBC_ERR_INVALID_ARG;
-    return RBC_OK;
+    if (!c || ticket == 0) return RBC_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (ticket >= c->next_ticket) return RBC_ERR_INVALID_ARG;
+    (void)hipSetDevice(c->device);
+    for (auto &sl : c->slots)
+        if (sl->busy && sl->ticket == ticket) return retire(c, *sl);
+    auto it = c->retired.find(ticket);
+    if (it == c->retired.end()) return RBC_OK;  // completed and already collected
+    const int st = it->second;
+    c->retired.erase(it);
+    return st;
 }
+
 int rbc_poll(rbc_ctx *c, uint64_t ticket, int *done) {
-    if (!c || !done || ticket >= c->next_ticket) return RBC_ERR_INVALID_ARG;
+    if (!c || !done || ticket == 0) return RBC_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (ticket >= c->next_ticket) return RBC_ERR_INVALID_ARG;
     *done = 1;
+    for (auto &sl : c->slots)
+        if (sl->busy && sl->ticket == ticket) {
+            const hipError_t q = hipEventQuery(sl->done);
+            if (q == hipErrorNotReady) {
+                *done = 0;
+                return RBC_OK;
+            }
+            c->retired[ticket] = retire(c, *sl);  // outputs are in place; status kept for rbc_wait
+            return RBC_OK;
+        }
     return RBC_OK;
 }
 
@@ -1023,8 +1186,7 @@ int rbc_shard(rbc_ctx *c, const uint8_t *data, size_t len, uint8_t *shards_out, 
     const size_t S = (len + c->k - 1) / c->k;
     if (shards_cap < (size_t)c->n * S) return RBC_ERR_INVALID_ARG;
     uint32_t slen = 0;
-    uint64_t t = 0;
-    int rc = rbc_shard_commit(c, 1, &data, &len, shards_out, S, &slen, root_out, branches_out, &t);
+    int rc = rbc_shard_commit(c, 1, &data, &len, shards_out, S, &slen, root_out, branches_out, nullptr);
     if (rc) return rc;
     if (shard_len_out) *shard_len_out = slen;
     return RBC_OK;
@@ -1036,8 +1198,7 @@ int rbc_validate_message(rbc_ctx *c, const uint8_t *root, const uint8_t *branch,
     *ok = 0;
     if (!shard || shard_len == 0) return RBC_OK;
     uint8_t r = 0;
-    uint64_t t = 0;
-    int rc = rbc_validate_batch(c, 1, &shard, &shard_len, &index, &branch, &branch_len, &root, &r, &t);
+    int rc = rbc_validate_batch(c, 1, &shard, &shard_len, &index, &branch, &branch_len, &root, &r, nullptr);
     if (rc) return rc;
     *ok = r;
     return RBC_OK;
@@ -1061,9 +1222,8 @@ int rbc_interpolate(rbc_ctx *c, const uint8_t *root, const uint8_t *const *shard
             pres[i] = 1;
         }
     int32_t status = 0;
-    uint64_t t = 0;
     rc = rbc_interpolate_batch(c, 1, buf.data(), S, &S, pres.data(), root, value_out, value_cap, digest_out, &status,
-                               &t);
+                               nullptr);
     if (rc) return rc;
     if (status) return status;
     if (value_len) *value_len = (size_t)c->k * S;

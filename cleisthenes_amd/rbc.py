@@ -132,6 +132,25 @@ def _dv(x) -> Optional[c_void_p]:
     return x
 
 
+class HostTicket:
+    """An in-flight host-API submission; the caller's arrays stay referenced
+    until wait() completes it."""
+
+    def __init__(self, ctx, ticket, result, keep=()):
+        self.ctx, self.ticket, self.result, self._keep = ctx, ticket, result, keep
+
+    def done(self) -> bool:
+        d = c_int(0)
+        check(lib.rbc_poll(self.ctx._p, self.ticket, byref(d)), "rbc_poll")
+        return bool(d.value)
+
+    def wait(self) -> dict:
+        if self._keep is not None:
+            check(lib.rbc_wait(self.ctx._p, self.ticket), "rbc_wait")
+            self._keep = None
+        return self.result
+
+
 class Context:
     """One (N, f) RBC geometry on one GPU (rbc/rbc.go:9-20)."""
 
@@ -229,6 +248,11 @@ class Context:
 
     # ---- host batch API ---------------------------------------------------
     def shard_commit_batch(self, values: Sequence[bytes]) -> dict:
+        return self.shard_commit_submit(values).wait()
+
+    def shard_commit_submit(self, values: Sequence[bytes]) -> "HostTicket":
+        """Asynchronous rbc_shard_commit: returns at once; .wait() completes
+        it (the context pipelines consecutive submissions through its slots)."""
         count = len(values)
         arrs = [_bytes_array(v) for v in values]
         Smax = max((len(a) + self.k - 1) // self.k for a in arrs)
@@ -243,8 +267,8 @@ class Context:
         check(lib.rbc_shard_commit(self._p, count, vptrs, vlens, _ptr(shards), pitch,
                                    slens.ctypes.data_as(_lib.u32p), _ptr(roots), _ptr(br), byref(t)),
               "rbc_shard_commit")
-        check(lib.rbc_wait(self._p, t.value))
-        return {"shards": shards, "shard_lens": slens, "roots": roots, "branches": br[:, :, : self.depth]}
+        out = {"shards": shards, "shard_lens": slens, "roots": roots, "branches": br[:, :, : self.depth]}
+        return HostTicket(self, t.value, out, keep=(arrs, vlens, vptrs, br))
 
     def validate_batch(self, shards, indices, branches, roots) -> np.ndarray:
         count = len(shards)
@@ -261,6 +285,7 @@ class Context:
         t = c_uint64(0)
         check(lib.rbc_validate_batch(self._p, count, sp, slens, idx, bp, blens, rp, _ptr(ok), byref(t)),
               "rbc_validate_batch")
+        check(lib.rbc_wait(self._p, t.value))
         return ok.astype(bool)
 
     def interpolate_batch(self, shards: np.ndarray, shard_lens, present: np.ndarray, roots: np.ndarray) -> dict:
@@ -279,6 +304,7 @@ class Context:
         check(lib.rbc_interpolate_batch(self._p, count, _ptr(shards), pitch, sl, _ptr(present), _ptr(roots),
                                         _ptr(values), values.shape[1], _ptr(digests),
                                         status.ctypes.data_as(_lib.i32p), byref(t)), "rbc_interpolate_batch")
+        check(lib.rbc_wait(self._p, t.value))
         return {"values": values, "digests": digests, "status": status}
 
     # ---- device-resident stages --------------------------------------------

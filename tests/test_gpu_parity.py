@@ -502,3 +502,27 @@ def test_fft_codec_rejects_noncodeword(gpu):
     c.dev_interpolate(None, I, b["shards"], pl.spitch, None, pl.S, b["valid"], b["leaves_r"], 1, b["roots"],
                       b["out"], pl.opitch, b["digests"], b["status"])
     assert (pl.arr("status", np.int32) == -8).all()
+
+
+def test_host_api_pipelined_submissions(gpu, ref):
+    """Host batch API tickets are asynchronous: several submissions are in
+    flight at once (more than the context's slots, so slot reuse retires the
+    oldest), completion order is the caller's, and every result is bit-exact."""
+    n, f = 16, 5
+    ctx = gpu.Context(n, f)
+    rng = np.random.default_rng(123)
+    batches = [[rng.integers(0, 256, int(rng.integers(1, 9000)), dtype=np.uint8) for _ in range(7)]
+               for _ in range(5)]
+    tickets = [ctx.shard_commit_submit(b) for b in batches]
+    polled = [t.done() for t in tickets]  # any mix of done / not yet
+    assert len(polled) == 5
+    for t, b in zip(reversed(tickets), reversed(batches)):
+        out = t.wait()
+        for i, v in enumerate(b):
+            shards, root, br, _ = ref.encode_commit(n, f, v)
+            S = shards.shape[1]
+            assert out["shard_lens"][i] == S
+            assert np.array_equal(out["shards"][i, :, :S], shards)
+            assert bytes(out["roots"][i]) == root
+            assert np.array_equal(out["branches"][i], br)
+    assert tickets[0].wait() is tickets[0].result  # waiting twice is harmless
