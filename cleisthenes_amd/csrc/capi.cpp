@@ -15,6 +15,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -863,7 +864,29 @@ int rbc_dev_inject_faults(rbc_ctx *c, void *stream, int count, uint8_t *shards, 
 }
 
 // ---- host-memory batch API (pipelined through per-context slots)
+extern "C++" {
 namespace {
+
+// Host-side staging copies run on several threads: one thread's memcpy
+// (~10 GB/s) would otherwise bound the host path well below PCIe.
+template <class F>
+void parallel_for(int count, size_t bytes_per_item, F &&f) {
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    int nt = (int)std::min<size_t>(std::min<unsigned>(hw, 16u), (size_t)count * bytes_per_item / (4u << 20));
+    nt = std::max(1, std::min(nt, count));
+    if (nt == 1) {
+        for (int i = 0; i < count; ++i) f(i);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve(nt - 1);
+    auto body = [&](int t) {
+        for (int i = t; i < count; i += nt) f(i);
+    };
+    for (int t = 1; t < nt; ++t) th.emplace_back(body, t);
+    body(0);
+    for (auto &x : th) x.join();
+}
 
 // Free slot for the next submission: create one while fewer than
 // host_slots() exist, else reuse an idle one, else retire the oldest
@@ -913,6 +936,7 @@ int submit(rbc_ctx *c, Slot &s, uint64_t *ticket, std::function<int()> finish) {
 }
 
 }  // namespace
+}  // extern "C++"
 
 int rbc_shard_commit(rbc_ctx *c, int count, const uint8_t *const *values, const size_t *value_lens,
                      uint8_t *shards_out, size_t shard_pitch, uint32_t *shard_lens_out, uint8_t *roots_out,
@@ -948,12 +972,12 @@ int rbc_shard_commit(rbc_ctx *c, int count, const uint8_t *const *values, const 
     RBC_HIP(s.h_out.ensure(sh_bytes + (size_t)count * 32 + br_bytes));
     uint8_t *stage = s.h_in.as<uint8_t>();
     uint32_t *lens = reinterpret_cast<uint32_t *>(stage + (size_t)count * vpitch);
-    for (int i = 0; i < count; ++i) {
+    parallel_for(count, vpitch, [&](int i) {
         memcpy(stage + (size_t)i * vpitch, values[i], value_lens[i]);
         memset(stage + (size_t)i * vpitch + value_lens[i], 0, vpitch - value_lens[i]);
         lens[i] = (uint32_t)value_lens[i];
         lens[count + i] = (uint32_t)((value_lens[i] + c->k - 1) / c->k);
-    }
+    });
     RBC_HIP(hipMemcpyAsync(s.d_values.p, stage, (size_t)count * vpitch, hipMemcpyHostToDevice, st));
     RBC_HIP(hipMemcpyAsync(s.d_lens.p, lens, (size_t)count * 8, hipMemcpyHostToDevice, st));
     const uint32_t *d_vlens = s.d_lens.as<uint32_t>(), *d_slens = d_vlens + count;
@@ -969,12 +993,12 @@ int rbc_shard_commit(rbc_ctx *c, int count, const uint8_t *const *values, const 
     RBC_HIP(hipMemcpyAsync(o_rt, s.d_roots.p, (size_t)count * 32, hipMemcpyDeviceToHost, st));
     if (branches_out && d > 0) RBC_HIP(hipMemcpyAsync(o_br, s.d_branches.p, br_bytes, hipMemcpyDeviceToHost, st));
     return submit(c, s, ticket, [=]() {
-        for (int i = 0; i < count; ++i) {
+        parallel_for(count, (size_t)n * Smax, [&](int i) {
             const size_t S = lens[count + i];
             for (int j = 0; j < n; ++j)  // Smax bytes per row: the device rows are zero past S_i
                 memcpy(shards_out + ((size_t)i * n + j) * shard_pitch, o_sh + ((size_t)i * n + j) * dpitch, Smax);
             if (shard_lens_out) shard_lens_out[i] = (uint32_t)S;
-        }
+        });
         memcpy(roots_out, o_rt, (size_t)count * 32);
         if (branches_out && d > 0) memcpy(branches_out, o_br, (size_t)count * n * d * 32);
         return RBC_OK;
@@ -1107,7 +1131,7 @@ int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t s
     RBC_HIP(s.h_out.ensure((size_t)count * (vpitch + 32 + 4)));
     uint8_t *i_sh = s.h_in.as<uint8_t>(), *i_pr = i_sh + sh_bytes, *i_rt = i_pr + (size_t)count * n;
     uint32_t *ln = reinterpret_cast<uint32_t *>(i_rt + (size_t)count * 32);
-    for (int i = 0; i < count; ++i) {
+    parallel_for(count, (size_t)n * dpitch, [&](int i) {
         ln[i] = (uint32_t)shard_lens[i];
         for (int j = 0; j < n; ++j) {
             uint8_t *dst = i_sh + ((size_t)i * n + j) * dpitch;
@@ -1115,7 +1139,7 @@ int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t s
             memcpy(dst, src, shard_lens[i]);
             memset(dst + shard_lens[i], 0, dpitch - shard_lens[i]);
         }
-    }
+    });
     memcpy(i_pr, present, (size_t)count * n);
     memcpy(i_rt, roots, (size_t)count * 32);
     RBC_HIP(hipMemcpyAsync(s.d_shards.p, i_sh, sh_bytes, hipMemcpyHostToDevice, st));
@@ -1136,8 +1160,9 @@ int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t s
     RBC_HIP(hipMemcpyAsync(o_st, s.d_status.p, (size_t)count * 4, hipMemcpyDeviceToHost, st));
     return submit(c, s, ticket, [=]() {
         memcpy(status_out, o_st, (size_t)count * 4);
-        for (int i = 0; i < count; ++i)
+        parallel_for(count, (size_t)k * Smax, [&](int i) {
             memcpy(values_out + (size_t)i * value_pitch, o_val + (size_t)i * vpitch, (size_t)k * Smax);
+        });
         if (digests_out) memcpy(digests_out, o_dig, (size_t)count * 32);
         return RBC_OK;
     });

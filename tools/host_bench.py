@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""Host-path (PCIe-inclusive) throughput of the C ABI's batch entry points.
+
+The bench.py metric keeps inputs resident in HBM.  This measures what the Go
+batcher would see: values in host memory -> rbc_shard_commit (pinned staging,
+H2D, encode + leaves + tree, D2H of shards/roots/branches) and the ECHO side
+rbc_interpolate_batch (shards H2D, decode + recheck, values D2H), with
+`--inflight` submissions pipelined through the context's slots.
+
+usage: python tools/host_bench.py [--config c2] [--batch 64] [--batches 8] [--inflight 2]
+Prints one JSON line; GB/s counts committed shard bytes (N*S per instance).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+CFG = {"c1": (64, 21, 1 << 20), "c2": (128, 42, 1 << 20), "c3": (128, 42, 4 << 20), "c4": (256, 85, 64 << 10)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2", choices=sorted(CFG))
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--batches", type=int, default=8)
+    ap.add_argument("--inflight", type=int, default=2)
+    args = ap.parse_args()
+    import cleisthenes_amd as ca
+
+    n, f, B = CFG[args.config]
+    ctx = ca.Context(n, f)
+    k = ctx.k
+    S = (B + k - 1) // k
+    rng = np.random.default_rng(1)
+    pool = [[rng.integers(0, 256, B, dtype=np.uint8) for _ in range(args.batch)] for _ in range(2)]
+
+    # shard + commit (proposer side)
+    warm = [ctx.shard_commit_submit(pool[i % 2]) for i in range(args.inflight)]  # warm every slot's buffers
+    for w in warm:
+        w.wait()
+    t0 = time.perf_counter()
+    live, outs = [], []
+    for b in range(args.batches):
+        live.append(ctx.shard_commit_submit(pool[b % 2]))
+        if len(live) >= args.inflight:
+            outs.append(live.pop(0).wait())
+    while live:
+        outs.append(live.pop(0).wait())
+    t_enc = time.perf_counter() - t0
+
+    # interpolate (receiver side) from N-f present shards of the last commit
+    sh = outs[-1]["shards"]
+    present = np.zeros((args.batch, n), np.uint8)
+    for i in range(args.batch):
+        present[i, rng.permutation(n)[: n - f]] = 1
+    rx = sh * present[:, :, None]
+    lens = outs[-1]["shard_lens"]
+    roots = outs[-1]["roots"]
+    ctx.interpolate_batch(rx, lens, present, roots)  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(args.batches):
+        res = ctx.interpolate_batch(rx, lens, present, roots)
+    t_dec = time.perf_counter() - t0
+    assert (res["status"] == 0).all()
+    shard_bytes = args.batch * n * S * args.batches
+    print(json.dumps({
+        "metric": "host-path RBC shard GB/s (PCIe-inclusive, host buffers in and out)",
+        "config": {"workload": args.config, "n": n, "f": f, "value_bytes": B, "batch": args.batch,
+                   "batches": args.batches, "inflight": args.inflight},
+        "shard_commit_GBps": round(shard_bytes / t_enc / 1e9, 2),
+        "interpolate_GBps": round(shard_bytes / t_dec / 1e9, 2),
+        "shard_commit_ms_per_batch": round(t_enc * 1e3 / args.batches, 3),
+        "interpolate_ms_per_batch": round(t_dec * 1e3 / args.batches, 3),
+    }))
+
+
+if __name__ == "__main__":
+    main()
