@@ -12,7 +12,8 @@ from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_size_t, c_uint8
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "librbc_gpu.so")
-HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "rbc_gpu.h")
+INCLUDE_DIR = os.path.join(os.path.dirname(_HERE), "include")
+HEADER_PATH = os.path.join(INCLUDE_DIR, "rbc_gpu.h")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(
@@ -98,6 +99,23 @@ _SIGS = {
     "rbc_comm_init": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "rbc_comm_destroy": (c_int, [c_void_p]),
     "rbc_dev_allgather_roots": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    # include/rbc_protocol.h
+    "rbc_pb_encode_rbc": (c_size_t, [c_int, c_void_p, c_size_t, c_void_p, c_size_t]),
+    "rbc_pb_decode_rbc": (c_int, [c_void_p, c_size_t, POINTER(c_int), POINTER(c_void_p), szp]),
+    "rbc_json_encode_val": (c_size_t, [c_void_p, c_size_t, c_void_p, c_size_t, c_void_p, c_size_t, c_void_p,
+                                       c_size_t]),
+    "rbc_json_encode_ready": (c_size_t, [c_void_p, c_size_t, c_void_p, c_size_t]),
+    "rbc_json_decode_val": (c_int, [c_void_p, c_size_t, c_void_p, c_void_p, c_size_t, szp, c_void_p, c_size_t,
+                                    szp]),
+    "rbc_json_decode_ready": (c_int, [c_void_p, c_size_t, c_void_p]),
+    "rbc_node_create": (c_int, [c_void_p, c_int, c_int, c_int, c_int, POINTER(c_void_p)]),
+    "rbc_node_destroy": (None, [c_void_p]),
+    "rbc_node_propose": (c_int, [c_void_p, c_void_p, c_size_t]),
+    "rbc_node_handle_message": (c_int, [c_void_p, c_int, c_void_p, c_size_t]),
+    "rbc_node_progress": (c_int, [c_void_p, c_int, POINTER(c_int)]),
+    "rbc_node_next_message": (c_int, [c_void_p, POINTER(c_int), c_void_p, c_size_t, szp]),
+    "rbc_node_value": (c_int, [c_void_p, c_void_p, c_size_t, szp, POINTER(c_int)]),
+    "rbc_node_stats": (c_int, [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_int), POINTER(c_int)]),
 }
 
 for _name, (_res, _args) in _SIGS.items():
@@ -106,12 +124,17 @@ for _name, (_res, _args) in _SIGS.items():
     _fn.argtypes = _args
 
 
-def header_functions(path: str = HEADER_PATH):
-    """Every function the C-ABI header declares (for the export test)."""
-    text = open(path).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    names = re.findall(r"\b(rbc_[a-z0-9_]+)\s*\(", text)
-    return sorted(set(names))
+def header_functions(path: str = None):
+    """Every function the C-ABI headers declare (all of include/*.h, or one
+    header), for the export test."""
+    paths = [path] if path else sorted(os.path.join(INCLUDE_DIR, f) for f in os.listdir(INCLUDE_DIR)
+                                       if f.endswith(".h"))
+    names = set()
+    for p in paths:
+        text = open(p).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        names.update(re.findall(r"\b(rbc_[a-z0-9_]+)\s*\(", text))
+    return sorted(names)
 
 
 # status codes (include/rbc_gpu.h)
@@ -128,6 +151,10 @@ RBC_ERR_DEVICE = -9
 RBC_ERR_INVALID_ARG = -10
 RBC_ERR_SINGULAR = -11
 RBC_ERR_NO_COMM = -12
+RBC_ERR_PROTOCOL = -20  # include/rbc_protocol.h
+
+# pb.RBC type (pb/message.proto:30-34)
+RBC_MSG_VAL, RBC_MSG_ECHO, RBC_MSG_READY = 0, 1, 2
 
 
 class RBCError(Exception):

@@ -667,6 +667,7 @@ const char *rbc_strerror(int s) {
         case RBC_ERR_INVALID_ARG: return "invalid argument";
         case RBC_ERR_SINGULAR: return "matrix is singular";
         case RBC_ERR_NO_COMM: return "multi-GPU communicator not initialised";
+        case -20: return "malformed or out-of-protocol RBC message"; /* RBC_ERR_PROTOCOL */
         default: return "unknown rbc status";
     }
 }
