@@ -40,9 +40,17 @@ CONFIGS = {
     "c4": (256, 85, 64 << 10, 16384, "N=256 f=85 64KiB x16384"),
 }
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
-# integer VOP3 (alignbit/bitop3/perm/add3): one wave64 instruction per 4 clk per SIMD
-# (16 lanes/clk), measured (profiles/r01_pmc_summary.json); 1024 SIMDs at 2.4 GHz
-VALU_ISSUE_PEAK = 1024 * 2.4e9 / 4      # wave-instructions/s
+# SHA-256 VALU roof.  Issue cost per wave64 instruction on one SIMD, measured
+# (profiles/r01_valu_probe.txt): v_alignbit / v_add3 / v_perm / v_bfi 4 clk,
+# v_bitop3 / v_add / v_xor / v_and / shifts 2 clk (with >= 4 waves per SIMD).
+# The compression loop of sha_rows_kernel (ISA) issues
+# 833 four-clock + 576 two-clock instructions = 4484 SIMD clocks per
+# wave-compression (64 rows): peak = 1024 SIMDs x 2.4 GHz / 4484 x 64.
+SHA_CLK_PER_WAVE_COMPRESSION = 833 * 4 + 576 * 2
+SHA_PEAK_CPS = 1024 * 2.4e9 / SHA_CLK_PER_WAVE_COMPRESSION * 64
+# attainable: the same compression register-resident at 8 waves/SIMD
+# (profiles/r01_sha_probe.txt, 5782 clk at the nominal 2.4 GHz)
+SHA_PROBE_CPS = 1024 * 2.4e9 / 5782 * 64
 
 
 def round_up(x, a):
@@ -257,15 +265,19 @@ def main():
             r["traffic_source"] = os.path.relpath(pmc_path, ROOT)
         if ncomp:
             # SHA-256 is integer-VALU bound (north_star: hashes/s against the VALU
-            # peak): compressions/s, and VALU issue = compressions x the kernel's
-            # VALU wave-instructions per compression (rocprof SQ_INSTS_VALU, in
-            # the PMC file) over 1024 SIMDs x 2.4 GHz / 4 clk
+            # peak): compressions/s against the issue-cost-weighted VALU peak, and
+            # against the register-resident probe (what the instruction mix attains)
             cps = ncomp / (ms / 1e3)
             r["sha256_compressions_per_s"] = round(cps / 1e9, 3)
             r["sha256_compressions_per_s_unit"] = "G/s"
-            vpc = (pk or {}).get("valu_per_compression", 1418.0 / 64)
-            r["valu"] = {"achieved": round(cps * vpc / 1e9, 2), "peak": round(VALU_ISSUE_PEAK / 1e9, 1),
-                         "unit": "G wave-instr/s", "frac": round(cps * vpc / VALU_ISSUE_PEAK, 4)}
+            r["valu"] = {"achieved": round(cps / 1e9, 3), "peak": round(SHA_PEAK_CPS / 1e9, 2),
+                         "unit": "G compressions/s", "frac": round(cps / SHA_PEAK_CPS, 4),
+                         "attainable_probe": round(SHA_PROBE_CPS / 1e9, 2),
+                         "frac_of_attainable": round(cps / SHA_PROBE_CPS, 4),
+                         "model": "4 clk alignbit/add3/perm, 2 clk bitop3/add/shift per wave64 instr; "
+                                  "4484 SIMD clk per wave-compression @2.4 GHz"}
+            if pk and pk.get("valu_per_compression"):
+                r["valu"]["valu_instr_per_compression_pmc"] = pk["valu_per_compression"]
         return r
 
     dom = max(kern, key=lambda x: kern[x][0])
