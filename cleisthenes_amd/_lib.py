@@ -108,6 +108,9 @@ _SIGS = {
     "rbc_json_decode_val": (c_int, [c_void_p, c_size_t, c_void_p, c_void_p, c_size_t, szp, c_void_p, c_size_t,
                                     szp]),
     "rbc_json_decode_ready": (c_int, [c_void_p, c_size_t, c_void_p]),
+    "rbc_dev_marshal_val": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_uint32, c_void_p, c_uint32,
+                                    c_void_p, c_void_p, c_void_p, c_uint64, c_void_p]),
+    "rbc_val_message_size": (c_size_t, [c_int, c_uint32, c_uint32, c_int]),
     "rbc_node_create": (c_int, [c_void_p, c_int, c_int, c_int, c_int, POINTER(c_void_p)]),
     "rbc_node_destroy": (None, [c_void_p]),
     "rbc_node_propose": (c_int, [c_void_p, c_void_p, c_size_t]),

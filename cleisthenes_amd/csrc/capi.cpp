@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/rbc_gpu.h"
+#include "../../include/rbc_protocol.h"
 #include "gf_host.h"
 #include "kernels.h"
 
@@ -853,6 +854,43 @@ int rbc_dev_interpolate(rbc_ctx *c, void *stream, int count, uint8_t *shards, ui
     RBC_HIP(hipSetDevice(c->device));
     return stage_interpolate(c, c->ws, as_stream(stream), count, shards, shard_pitch, shard_lens, uniform_shard_len, valid,
                              leaves, leaves_verified, roots, values_out, value_pitch, digests, status);
+}
+
+size_t rbc_val_message_size(int n, uint32_t shard_len, uint32_t index, int type) {
+    if (n < 1) return 0;
+    int d = 0;
+    while ((1 << d) < n) ++d;
+    return rbc_val_message_bytes(n, d, shard_len, index, type);
+}
+
+int rbc_dev_marshal_val(rbc_ctx *c, void *stream, int count, int type, const uint8_t *shards,
+                        uint32_t shard_pitch, const uint32_t *shard_lens, uint32_t uniform_shard_len,
+                        const uint8_t *branches, const uint8_t *roots, uint8_t *out, uint64_t out_pitch,
+                        uint32_t *out_lens) {
+    if (!c || count < 0 || (type != 0 && type != 1) || out_pitch % 16 || shard_pitch % 4) return RBC_ERR_INVALID_ARG;
+    if (count == 0) return RBC_OK;
+    if (!shards || !roots || !out || (c->depth && !branches)) return RBC_ERR_INVALID_ARG;
+    if (!shard_lens && (uniform_shard_len == 0 || uniform_shard_len > shard_pitch ||
+                        out_pitch < rbc_val_message_bytes(c->n, c->depth, uniform_shard_len, 0, type)))
+        return RBC_ERR_INVALID_ARG;
+    RBC_HIP(hipSetDevice(c->device));
+    WireArgs a{};
+    a.count = count;
+    a.n = c->n;
+    a.depth = c->depth;
+    a.type = type;
+    a.shards = shards;
+    a.inst_pitch = (uint64_t)c->n * shard_pitch;
+    a.row_pitch = shard_pitch;
+    a.lens = shard_lens;
+    a.uniform_len = uniform_shard_len;
+    a.branches = branches;
+    a.roots = roots;
+    a.out = out;
+    a.out_pitch = out_pitch;
+    a.out_lens = out_lens;
+    RBC_HIP(rbc_launch_marshal_val(a, as_stream(stream)));
+    return RBC_OK;
 }
 
 int rbc_dev_inject_faults(rbc_ctx *c, void *stream, int count, uint8_t *shards, uint32_t shard_pitch,

@@ -151,6 +151,24 @@ struct FftArgs {
 };
 
 bool rbc_fft_supported(int n, int k);
+// VAL / ECHO marshaling (wire.hip): message (i, j) = pb.Message bytes of
+// the request for shard j of instance i, at out + (i*n + j)*out_pitch.
+struct WireArgs {
+    int count, n, depth, type;
+    const uint8_t *shards;
+    uint64_t inst_pitch;
+    uint32_t row_pitch;
+    const uint32_t *lens;  // per instance, or NULL: uniform_len
+    uint32_t uniform_len;
+    const uint8_t *branches;  // [count][n][depth][32]
+    const uint8_t *roots;     // [count][32]
+    uint8_t *out;
+    uint64_t out_pitch;  // % 16 == 0
+    uint32_t *out_lens;  // [count*n], nullable
+};
+hipError_t rbc_launch_marshal_val(const WireArgs &a, hipStream_t st);
+size_t rbc_val_message_bytes(int n, int depth, uint32_t S, uint32_t index, int type);
+
 hipError_t rbc_launch_rs_fft(const FftArgs &a, hipStream_t st);
 
 int rbc_gf_pick_rc(int R, int rcmax);

@@ -339,6 +339,16 @@ class Context:
                                       _dv(values_out), value_pitch, _dv(digests), _dv(status)),
               "rbc_dev_interpolate")
 
+    def dev_marshal_val(self, stream, count, msg_type, shards, shard_pitch, shard_lens, uniform_len, branches,
+                        roots, out, out_pitch, out_lens):
+        """Per-recipient VAL / ECHO pb.Message bytes in HBM (include/rbc_protocol.h)."""
+        check(lib.rbc_dev_marshal_val(self._p, _dv(stream), count, msg_type, _dv(shards), shard_pitch,
+                                      _dv(shard_lens), uniform_len, _dv(branches), _dv(roots), _dv(out), out_pitch,
+                                      _dv(out_lens)), "rbc_dev_marshal_val")
+
+    def val_message_size(self, shard_len: int, index: int = 0, msg_type: int = 0) -> int:
+        return lib.rbc_val_message_size(self.n, shard_len, index, msg_type)
+
     def dev_inject_faults(self, stream, count, shards, shard_pitch, corrupt):
         check(lib.rbc_dev_inject_faults(self._p, _dv(stream), count, _dv(shards), shard_pitch, _dv(corrupt)),
               "rbc_dev_inject_faults")

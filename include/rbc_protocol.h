@@ -62,6 +62,22 @@ int rbc_json_decode_val(const uint8_t *json, size_t len, uint8_t *root_out, uint
                         size_t *branch_len, uint8_t *block_out, size_t block_cap, size_t *block_len);
 int rbc_json_decode_ready(const uint8_t *json, size_t len, uint8_t *root_out);
 
+/* ---- device-side marshaling (the proposer's per-recipient VAL send path) --
+ * For every instance i and row j, writes the pb.Message bytes of VAL / ECHO
+ * (type) carrying (roots[i], flat branch j, shard j) -- byte-identical to
+ * rbc_pb_encode_rbc(type, rbc_json_encode_val(...)) -- to
+ * out + (i*n + j)*out_pitch, and out_lens[i*n + j] = its size (nullable).
+ * Inputs in the rbc_dev_* layout (rbc_gpu.h): shards [count][n][shard_pitch],
+ * branches [count][n][d][32], roots [count][32].  out_pitch % 16 == 0 and
+ * >= round_up(rbc_val_message_size(n, S_max, 0, type), 16); bytes past a
+ * message up to the next 16 are zeroed. */
+int rbc_dev_marshal_val(rbc_ctx *ctx, void *stream, int count, int type, const uint8_t *shards,
+                        uint32_t shard_pitch, const uint32_t *shard_lens, uint32_t uniform_shard_len,
+                        const uint8_t *branches, const uint8_t *roots, uint8_t *out, uint64_t out_pitch,
+                        uint32_t *out_lens);
+/* Size of that message for shard length S at leaf `index` of an n-node tree. */
+size_t rbc_val_message_size(int n, uint32_t shard_len, uint32_t index, int type);
+
 /* ---- RBC instance (one proposer's broadcast, seen at one node) ----------- */
 typedef struct rbc_node rbc_node;
 /* NewRBC (rbc/rbc.go:38). */
