@@ -70,6 +70,9 @@ def main():
     ap.add_argument("--streams", type=int, default=1,
                     help="split the batch over S HIP streams (one context each) so stages of different "
                          "instance groups overlap")
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="1: overlap batch t's commit (proposer stream) with batch t-1's verify + "
+                         "interpolate (receiver stream), two shard buffer sets")
     ap.add_argument("--shard-align", type=int, default=128,
                     help="shard row pitch alignment in bytes (multiple of 64; the C ABI needs 64)")
     ap.add_argument("--force-gather", action="store_true",
@@ -113,10 +116,13 @@ def main():
     d_values = mb(I * vpitch)
     d_values.upload(values_h)
     del values_h
-    d_shards = mb(I * n * spitch)
-    d_leaves_p = mb(I * n * 32)
-    d_roots = mb(I * 32)
-    d_branches = mb(I * n * max(d, 1) * 32)
+    pipe = bool(args.pipeline)
+    if pipe and args.streams > 1:
+        raise SystemExit("--pipeline and --streams > 1 are exclusive")
+    nsets = 2 if pipe else 1
+    sets = [dict(shards=mb(I * n * spitch), leaves=mb(I * n * 32), roots=mb(I * 32),
+                 branches=mb(I * n * max(d, 1) * 32)) for _ in range(nsets)]
+    d_shards, d_leaves_p, d_roots, d_branches = (sets[0][x] for x in ("shards", "leaves", "roots", "branches"))
     d_present = mb(I * n)
     d_present.upload(present_h)
     d_corrupt = mb(I * 4)
@@ -185,15 +191,56 @@ def main():
         if timed:
             ev["gather"].record(stream)
 
+    # --pipeline: proposer stream P commits batch t into set t%2 while the
+    # receiver stream R verifies + interpolates batch t-1 from the other set.
+    # A set is reused only after R has finished with it (evR), and R starts a
+    # batch only after P committed it (evP): K timed steps = K commits + K
+    # decodes, all inside the timed region.
+    rstream = ca.Stream(dev) if pipe else None
+    evP = [ca.Event() for _ in range(nsets)]
+    evR = [ca.Event() for _ in range(nsets)]
+    for e in evP + evR:
+        e.record(stream)  # recorded once, so every wait below is well defined
+
+    def pstep(t):
+        P, R = stream, rstream
+        sp = sets[t % 2]
+        P.wait(evR[t % 2])
+        ctx.dev_encode(P.ptr, I, d_values.value, vpitch, None, B, sp["shards"].value, spitch)
+        ctx.dev_leaves(P.ptr, I, sp["shards"].value, spitch, None, S, sp["leaves"].value)
+        ctx.dev_merkle_build(P.ptr, I, sp["leaves"].value, sp["roots"].value, sp["branches"].value)
+        ctx.dev_inject_faults(P.ptr, I, sp["shards"].value, spitch, d_corrupt.value)
+        evP[t % 2].record(P)
+        if t == 0:
+            return
+        sr = sets[(t - 1) % 2]
+        R.wait(evP[(t - 1) % 2])
+        ctx.dev_verify(R.ptr, I, sr["shards"].value, spitch, None, S, sr["branches"].value, sr["roots"].value,
+                       d_present.value, d_valid.value, d_leaves_r.value)
+        ctx.dev_interpolate(R.ptr, I, sr["shards"].value, spitch, None, S, d_valid.value, d_leaves_r.value, 1,
+                            sr["roots"].value, d_out.value, opitch, d_digests.value, d_status.value)
+        if gather:
+            ctx.dev_allgather_roots(R.ptr, I, sr["roots"].value, d_digests.value, d_gather)
+        evR[(t - 1) % 2].record(R)
+
     def barrier():
+        if rstream is not None:
+            rstream.sync()
         for s_ in streams:
             s_.sync()
         ca.rbc.lib.rbc_device_sync(dev)
         if dist is not None:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        step(False)
+    if pipe:
+        args.warmup = max(args.warmup, 2)  # fill the pipeline: at least one decode before the guard
+        for t in range(args.warmup):
+            pstep(t)
+        last_set = sets[(args.warmup - 2) % 2]
+        d_roots = last_set["roots"]  # the set the last decode (and gather) read
+    else:
+        for _ in range(args.warmup):
+            step(False)
     barrier()
     # correctness guard on the warmed-up state: every instance must decode
     status = np.frombuffer(d_status.download().tobytes(), dtype=np.int32)
@@ -209,14 +256,29 @@ def main():
     order = ["t0", "enc", "leaf", "tree", "fault", "verify", "interp", "gather"]
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
-        for s_ in streams:
-            s_.sync()
-        for a, b in zip(order[:-1], order[1:]):
-            stage_ms[b] += ev[a].elapsed_ms(ev[b])
+    if pipe:
+        for t in range(args.warmup, args.warmup + args.steps):
+            pstep(t)
+    else:
+        for _ in range(args.steps):
+            step(True)
+            for s_ in streams:
+                s_.sync()
+            for a, b in zip(order[:-1], order[1:]):
+                stage_ms[b] += ev[a].elapsed_ms(ev[b])
     barrier()
     elapsed = time.perf_counter() - t0
+    if pipe:
+        # per-stage (and roofline) timings from an isolated serial pass: under
+        # the overlap, one kernel's event span includes the other stream's work
+        d_shards, d_leaves_p, d_roots, d_branches = (sets[0][x] for x in ("shards", "leaves", "roots", "branches"))
+        iso = 3
+        for _ in range(iso):
+            step(True)
+            stream.sync()
+            for a, b in zip(order[:-1], order[1:]):
+                stage_ms[b] += ev[a].elapsed_ms(ev[b]) * args.steps / iso
+        barrier()
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -303,7 +365,8 @@ def main():
         "config": {"workload": f"{args.config}: {desc}; shard+commit, ECHO verify all N, interpolate from N-f",
                    "n": n, "f": f, "value_bytes": B, "shard_bytes": S, "instances_per_gpu": I,
                    "parallelism": f"instances partitioned over {world} GPU(s), RCCL root all-gather",
-                   "streams_per_gpu": nstreams, "gf_codec": ctx.codec},
+                   "streams_per_gpu": nstreams, "gf_codec": ctx.codec,
+                   "pipeline": "commit(t) || verify+interpolate(t-1) on two streams" if pipe else "serial"},
         "stage_ms": {kk: round(v, 4) for kk, v in stage_ms.items()},
         "decoded_ok": n_ok,
         "roofline": roof,

@@ -52,6 +52,7 @@ _SIGS = {
     "rbc_event_destroy": (c_int, [c_void_p]),
     "rbc_event_record": (c_int, [c_void_p, c_void_p]),
     "rbc_event_elapsed_ms": (c_int, [c_void_p, c_void_p, POINTER(c_float)]),
+    "rbc_stream_wait_event": (c_int, [c_void_p, c_void_p]),
     "rbc_device_sync": (c_int, [c_int]),
     "rbc_dev_encode": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_uint64, c_void_p, c_uint32, c_void_p,
                                c_uint32]),

@@ -791,6 +791,11 @@ int rbc_event_elapsed_ms(void *start, void *stop, float *ms) {
     RBC_HIP(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
     return RBC_OK;
 }
+int rbc_stream_wait_event(void *stream, void *event) {
+    if (!event) return RBC_ERR_INVALID_ARG;
+    RBC_HIP(hipStreamWaitEvent(as_stream(stream), (hipEvent_t)event, 0));
+    return RBC_OK;
+}
 int rbc_device_sync(int device) {
     RBC_HIP(hipSetDevice(device));
     RBC_HIP(hipDeviceSynchronize());

@@ -76,6 +76,50 @@ RBC_DEV void sha256_compress(Sha256State &s, uint32_t (&w)[16]) {
     s.h[4] += e; s.h[5] += f; s.h[6] += g; s.h[7] += h;
 }
 
+// R independent compressions interleaved round by round.  One wave alone
+// issues a dependent VALU chain at ~8.7 clk per instruction
+// (profiles/r01_valu_probe.txt); R chains per lane hide that latency without
+// needing more waves per SIMD (profiles/r01_sha_probe.txt: rows/lane=2).
+// Rotating registers: at round i, a..h live in v[(0-i)&7] .. v[(7-i)&7].
+template <int R>
+RBC_DEV void sha256_compress_n(Sha256State (&s)[R], uint32_t (&w)[R][16]) {
+    uint32_t v[R][8];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[r][q] = s[r].h[q];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            uint32_t wi;
+            if (i < 16) {
+                wi = w[r][i];
+            } else {
+                const uint32_t w15 = w[r][(i - 15) & 15], w2 = w[r][(i - 2) & 15];
+                const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+                const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+                wi = w[r][i & 15] + s0 + w[r][(i - 7) & 15] + s1;
+                w[r][i & 15] = wi;
+            }
+            uint32_t &a = v[r][(0 - i) & 7], &b = v[r][(1 - i) & 7], &c = v[r][(2 - i) & 7];
+            uint32_t &d = v[r][(3 - i) & 7], &e = v[r][(4 - i) & 7], &f = v[r][(5 - i) & 7];
+            uint32_t &g = v[r][(6 - i) & 7], &h = v[r][(7 - i) & 7];
+            const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+            const uint32_t ch = (e & f) ^ (~e & g);
+            const uint32_t t1 = h + S1 + ch + kSHA_K[i] + wi;
+            const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+            const uint32_t mj = __builtin_amdgcn_bitop3_b32(a, b, c, 0xe8);
+            d = d + t1;        // becomes e of round i+1
+            h = t1 + S0 + mj;  // becomes a of round i+1
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s[r].h[q] += v[r][q];
+}
+
 // Load 64 bytes (16-byte aligned) and decode to big-endian words.
 RBC_DEV void load_block_be(const uint8_t *p, uint32_t (&w)[16]) {
     const uint4 *q = reinterpret_cast<const uint4 *>(p);
@@ -154,6 +198,91 @@ RBC_DEV void sha256_row(const uint8_t *row, uint32_t len, Sha256State &s) {
         w[15] = (uint32_t)bits;
         sha256_compress(s, w);
     }
+}
+
+// Last data block of a `len`-byte message (tail words already in w): keep
+// the len % 64 message bytes, append 0x80, zero the rest.
+RBC_DEV void sha256_pad_tail(uint32_t (&w)[16], uint32_t len) {
+    const uint32_t rem = len & 63u;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+        const int nb = (int)rem - 4 * t;
+        uint32_t v = w[t];
+        if (nb >= 4) {
+        } else if (nb <= 0) {
+            v = (nb == 0) ? 0x80000000u : 0u;
+        } else {
+            const uint32_t keep = 0xffffffffu << (32 - 8 * nb);
+            v = (v & keep) | (0x80u << (24 - 8 * nb));
+        }
+        w[t] = v;
+    }
+}
+
+// Two rows of the same length hashed by one lane, compressions interleaved.
+RBC_DEV void sha256_row2(const uint8_t *row0, const uint8_t *row1, uint32_t len, Sha256State (&s)[2]) {
+    sha256_init(s[0]);
+    sha256_init(s[1]);
+    const uint32_t nfull = len >> 6;
+    uint32_t w[2][16];
+    uint4 q0[4], q1[4];
+    if (nfull) {
+        load_block_raw(row0, q0);
+        load_block_raw(row1, q1);
+    }
+    for (uint32_t b = 0; b < nfull; ++b) {
+        bswap_block(q0, w[0]);
+        bswap_block(q1, w[1]);
+        if (b + 1 < nfull) {
+            load_block_raw(row0 + 64u * (b + 1), q0);
+            load_block_raw(row1 + 64u * (b + 1), q1);
+        }
+        sha256_compress_n<2>(s, w);
+    }
+    const uint32_t rem = len & 63u;
+    if (rem) {
+        load_block_be(row0 + 64u * nfull, w[0]);
+        load_block_be(row1 + 64u * nfull, w[1]);
+    } else {
+#pragma unroll
+        for (int t = 0; t < 16; ++t) w[0][t] = w[1][t] = 0;
+    }
+    sha256_pad_tail(w[0], len);
+    sha256_pad_tail(w[1], len);
+    const uint64_t bits = (uint64_t)len * 8u;
+    if (rem > 55u) {
+        sha256_compress_n<2>(s, w);
+#pragma unroll
+        for (int t = 0; t < 14; ++t) w[0][t] = w[1][t] = 0;
+    }
+    w[0][14] = w[1][14] = (uint32_t)(bits >> 32);
+    w[0][15] = w[1][15] = (uint32_t)bits;
+    sha256_compress_n<2>(s, w);
+}
+
+// Two Merkle nodes H(l_r || r_r) at once (second block's schedule constant).
+RBC_DEV void sha256_node64x2(const uint32_t (&l)[2][8], const uint32_t (&rr)[2][8], uint32_t (&out)[2][8]) {
+    Sha256State s[2];
+    sha256_init(s[0]);
+    sha256_init(s[1]);
+    uint32_t w[2][16];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) { w[r][t] = l[r][t]; w[r][8 + t] = rr[r][t]; }
+    sha256_compress_n<2>(s, w);
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+#pragma unroll
+        for (int t = 0; t < 16; ++t) w[r][t] = 0;
+        w[r][0] = 0x80000000u;
+        w[r][15] = 512u;
+    }
+    sha256_compress_n<2>(s, w);
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) out[r][t] = s[r].h[t];
 }
 
 // SHA-256 over the concatenation of two 32-byte digests (Merkle node,

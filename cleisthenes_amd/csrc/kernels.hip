@@ -278,6 +278,73 @@ __global__ __launch_bounds__(256) void sha_rows_kernel(ShaArgs a) {
     }
 }
 
+// Two rows per lane (rows 2t, 2t+1 of one instance, so one length), the
+// compressions interleaved: the per-wave dependent chain halves its stalls
+// (profiles/r01_sha_probe.txt: 6,071 SIMD clk per row-compression at one
+// wave per SIMD vs 6,423 for one row per lane at two).  Launched for the
+// full-instance grids (leaves, ECHO verify) when N is even; list mode and
+// per-message verify keep sha_rows_kernel.
+template <bool VERIFY>
+__global__ __launch_bounds__(256) void sha_rows2_kernel(ShaArgs a) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int half = a.rows_per_inst >> 1;
+    if (t >= a.count * half) return;
+    const int inst = t / half;
+    const int slot = 2 * (t - inst * half);
+    if (a.status && a.status[inst] != 0) return;
+    int pos[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+        pos[r] = a.idx ? (int)a.idx[(size_t)inst * a.idx_stride + slot + r] : slot + r;
+    const uint32_t S = inst_len(a.lens, a.uniform_len, inst);
+    const uint8_t *base = a.rows + (size_t)inst * a.inst_pitch;
+    Sha256State s[2];
+    sha256_row2(base + (size_t)pos[0] * a.row_pitch, base + (size_t)pos[1] * a.row_pitch, S, s);
+    uint32_t h[2][8];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) h[r][q] = s[r].h[q];
+    if (a.leaves)
+#pragma unroll
+        for (int r = 0; r < 2; ++r) store_digest(a.leaves + (size_t)inst * a.leaves_inst_pitch + 32u * pos[r], h[r]);
+    if (VERIFY) {
+        // N even: every level-0 sibling exists (no empty padding leaf)
+        const uint8_t *br[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) br[r] = a.branches + (size_t)inst * a.br_inst_pitch + (size_t)pos[r] * a.depth * 32u;
+        for (int l = 0; l < a.depth; ++l) {
+            uint32_t L[2][8], Rr[2][8], o[2][8];
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                uint32_t sib[8];
+                load_digest(br[r] + 32u * l, sib);
+                const bool right = ((uint32_t)pos[r] >> l) & 1u;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    L[r][q] = right ? sib[q] : h[r][q];
+                    Rr[r][q] = right ? h[r][q] : sib[q];
+                }
+            }
+            sha256_node64x2(L, Rr, o);
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+#pragma unroll
+                for (int q = 0; q < 8; ++q) h[r][q] = o[r][q];
+        }
+        uint32_t root[8];
+        load_digest(a.roots + (size_t)inst * 32u, root);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            bool ok = true;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) ok = ok && (h[r][q] == root[q]);
+            const bool present = a.present ? a.present[(size_t)inst * a.n + pos[r]] != 0 : true;
+            a.valid[(size_t)inst * a.n + pos[r]] = (ok && present && pos[r] < a.n) ? 1 : 0;
+        }
+    }
+}
+
 // ============================================================================
 // merkle: one wave per instance.  BUILD writes root + all N branches;
 // CHECK recomputes the root over the re-encoded leaves, compares it with the
@@ -815,6 +882,30 @@ hipError_t rbc_launch_gf_rows(const GfArgs &a, hipStream_t st) {
 hipError_t rbc_launch_sha_rows(const ShaArgs &a, bool verify, hipStream_t st) {
     const long total = (long)a.count * a.rows_per_inst;
     if (total <= 0) return hipSuccess;
+    // Measured (MI355X, bench): two rows per lane wins only where its ILP hits
+    // the branch walk's short, cache-resident compressions and waves are
+    // plentiful -- C4 verify 5.47 -> 4.51 ms (4 M rows) -- and loses wherever
+    // the leaf hashing streams HBM at ~1 wave per SIMD (C2 leaves 1.93 -> 2.13,
+    // C2 verify 1.99 -> 2.18, C4 leaves 2.15 -> 2.38): it halves the waves
+    // that hide load latency.  RBC_SHA_ROWS: 1 never, 2 leaves+verify,
+    // 3 (default) verify only, from 4 waves per SIMD of one-row work.
+    static const int rows_env = [] {
+        const char *e = getenv("RBC_SHA_ROWS");
+        return e ? atoi(e) : 3;
+    }();
+    static const int tpb2 = [] {
+        const char *e = getenv("RBC_SHA2_TPB");
+        return e ? atoi(e) : 256;
+    }();
+    const bool two = (rows_env == 2 || (rows_env == 3 && verify)) && !a.list && !a.per_message &&
+                     a.rows_per_inst % 2 == 0 && (!verify || a.n % 2 == 0) &&
+                     total >= 4L * 64 * 1024;
+    if (two) {
+        dim3 g2((unsigned)((total / 2 + tpb2 - 1) / tpb2));
+        if (verify) hipLaunchKernelGGL(sha_rows2_kernel<true>, g2, dim3(tpb2), 0, st, a);
+        else hipLaunchKernelGGL(sha_rows2_kernel<false>, g2, dim3(tpb2), 0, st, a);
+        return hipGetLastError();
+    }
     dim3 grid((unsigned)((total + 255) / 256));
     if (verify) hipLaunchKernelGGL(sha_rows_kernel<true>, grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(sha_rows_kernel<false>, grid, dim3(256), 0, st, a);

@@ -91,6 +91,9 @@ class Stream:
     def sync(self) -> None:
         check(lib.rbc_stream_sync(self.ptr), "rbc_stream_sync")
 
+    def wait(self, event: "Event") -> None:
+        check(lib.rbc_stream_wait_event(self.ptr, event.ptr), "rbc_stream_wait_event")
+
     def __del__(self):
         try:
             if self.ptr:

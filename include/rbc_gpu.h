@@ -99,6 +99,8 @@ int rbc_event_create(void **event);
 int rbc_event_destroy(void *event);
 int rbc_event_record(void *event, void *stream);
 int rbc_event_elapsed_ms(void *start, void *stop, float *ms);
+/* Make later work on `stream` wait for `event` (cross-stream pipelining). */
+int rbc_stream_wait_event(void *stream, void *event);
 int rbc_device_sync(int device);
 
 /* ---- device-resident batch stages -----------------------------------------
