@@ -708,13 +708,25 @@ __global__ __launch_bounds__(256) void decode_prepare_fft_kernel(PrepArgs a, con
         if (tid == 0) a.status[inst] = 0;
         return;
     }
-    auto gmul = [&](uint32_t x, uint32_t y) -> uint32_t {
-        return (x && y) ? (uint32_t)s_exp[s_log[x] + s_log[y]] : 0u;
+    // Log-domain products: every multiply below is one exp lookup (log 255
+    // marks a zero operand).  The operands reused across a pivot step (the
+    // scaled pivot row, the column factors) and across D (inverse, the used
+    // parity rows of M) are converted to logs once, into LDS.
+    auto glog = [&](uint32_t x) -> uint32_t { return x ? (uint32_t)s_log[x] : 255u; };
+    auto gexpl = [&](uint32_t la, uint32_t lb) -> uint32_t {
+        return (la == 255u || lb == 255u) ? 0u : (uint32_t)s_exp[la + lb];
     };
     const int m2 = 2 * m, kp = k - m;  // U = D_p (kp rows) then P_u (m rows)
+    uint8_t *s_plog = A + (size_t)m * m2;          // m2: log of the scaled pivot row
+    uint8_t *s_alog = s_plog + m2;                 // m x m: log of A^-1
+    uint8_t *s_mlog = s_alog + (size_t)m * m;      // m x kp: log M[P_u[i]][D_p[u]]
     for (int e = tid; e < m * m2; e += 256) {
         const int r = e / m2, c = e - r * m2;
         A[e] = c < m ? a.M[(size_t)s_used[kp + r] * k + s_miss[c]] : (uint8_t)((c - m) == r);
+    }
+    for (int e = tid; e < m * kp; e += 256) {
+        const int i = e / kp, u = e - i * kp;
+        s_mlog[e] = (uint8_t)glog(a.M[(size_t)s_used[kp + i] * k + s_used[u]]);
     }
     __syncthreads();
     for (int col = 0; col < m; ++col) {
@@ -726,6 +738,7 @@ __global__ __launch_bounds__(256) void decode_prepare_fft_kernel(PrepArgs a, con
                     if (A[b * m2 + col]) { piv = b; break; }
             }
             s_misc[4] = piv;
+            s_misc[5] = piv >= 0 ? A[piv * m2 + col] : 0;  // read before the row moves
         }
         __syncthreads();
         const int piv = s_misc[4];
@@ -733,26 +746,32 @@ __global__ __launch_bounds__(256) void decode_prepare_fft_kernel(PrepArgs a, con
             if (tid == 0) a.status[inst] = RBC_ERR_SINGULAR;
             return;
         }
-        if (piv != col) {
-            for (int c = tid; c < m2; c += 256) {
-                const uint8_t x = A[col * m2 + c];
-                A[col * m2 + c] = A[piv * m2 + c];
-                A[piv * m2 + c] = x;
-            }
-            __syncthreads();
+        // columns < col of the pivot row are zero: only [col, m2) moves
+        const uint32_t linv = 255u - s_log[s_misc[5]];  // log of the pivot's inverse
+        for (int c = col + tid; c < m2; c += 256) {
+            const uint32_t x = A[piv * m2 + c];
+            const uint32_t y = gexpl(linv % 255u, glog(x));
+            if (piv != col) A[piv * m2 + c] = A[col * m2 + c];
+            s_plog[c] = (uint8_t)glog(y);
         }
-        const uint32_t inv = s_exp[255 - s_log[A[col * m2 + col]]];
+        for (int r = tid; r < m; r += 256) {
+            const int src = (r == piv) ? col : r;  // the row that lands at r after the swap
+            s_fac[r] = (r == col) ? (uint8_t)255 : (uint8_t)glog(A[src * m2 + col]);
+        }
         __syncthreads();
-        for (int c = tid; c < m2; c += 256) A[col * m2 + c] = (uint8_t)gmul(inv, A[col * m2 + c]);
-        for (int r = tid; r < m; r += 256) s_fac[r] = (r == col) ? 0 : A[r * m2 + col];
-        __syncthreads();
-        for (int e = tid; e < m * m2; e += 256) {
-            const int r = e / m2, c = e - r * m2;
-            const uint32_t f = s_fac[r];
-            if (f) A[e] ^= (uint8_t)gmul(f, A[col * m2 + c]);
+        const int w = m2 - col;
+        for (int e = tid; e < m * w; e += 256) {
+            const int r = e / w, c = col + (e - r * w);
+            if (r == col) A[r * m2 + c] = (uint8_t)gexpl(s_plog[c], 0u);
+            else A[r * m2 + c] ^= (uint8_t)gexpl(s_fac[r], s_plog[c]);
         }
         __syncthreads();
     }
+    for (int e = tid; e < m * m; e += 256) {
+        const int r = e / m, i = e - r * m;
+        s_alog[e] = (uint8_t)glog(A[r * m2 + m + i]);
+    }
+    __syncthreads();
     // D[r][u]: u < kp -> sum_i Ainv[r][i] * M[P_u[i]][D_p[u]];  u >= kp -> Ainv[r][u-kp]
     uint8_t *D = a.dmat + (size_t)inst * a.dmat_stride;
     for (int e = tid; e < m * k; e += 256) {
@@ -762,8 +781,13 @@ __global__ __launch_bounds__(256) void decode_prepare_fft_kernel(PrepArgs a, con
             acc = A[r * m2 + m + (u - kp)];
         } else {
             acc = 0;
-            const int dp = s_used[u];
-            for (int i = 0; i < m; ++i) acc ^= gmul(A[r * m2 + m + i], a.M[(size_t)s_used[kp + i] * k + dp]);
+            const uint8_t *al = s_alog + r * m;
+            const uint8_t *ml = s_mlog + u;
+            int i = 0;
+            for (; i + 4 <= m; i += 4)
+                acc ^= gexpl(al[i], ml[i * kp]) ^ gexpl(al[i + 1], ml[(i + 1) * kp]) ^
+                       gexpl(al[i + 2], ml[(i + 2) * kp]) ^ gexpl(al[i + 3], ml[(i + 3) * kp]);
+            for (; i < m; ++i) acc ^= gexpl(al[i], ml[i * kp]);
         }
         D[e] = (uint8_t)acc;
     }
@@ -932,7 +956,9 @@ hipError_t rbc_launch_decode_prepare(const PrepArgs &a, hipStream_t st) {
     if (a.count <= 0) return hipSuccess;
     if (a.fft) {
         const int mmax = std::min(a.k, a.n - a.k);
-        const size_t lds = 1616 + (size_t)mmax * 2 * mmax;
+        // [A | I], pivot-row logs, log A^-1, log M[P_u][D_p] (m * kp <= k^2 / 4)
+        const size_t lds = 1616 + (size_t)mmax * 2 * mmax + 2 * (size_t)mmax + (size_t)mmax * mmax +
+                           (size_t)a.k * a.k / 4 + 16;
         hipLaunchKernelGGL(decode_prepare_fft_kernel, dim3(a.count), dim3(256), lds, st, a, a.gf_exp, a.gf_log);
         return hipGetLastError();
     }

@@ -268,7 +268,9 @@ namespace {
 RBC_DEV uint32_t keep_bytes4(int nv) { return nv >= 4 ? 0xffffffffu : (nv <= 0 ? 0u : ((1u << (8 * nv)) - 1u)); }
 
 template <int LOGW, int K, int N, int MODE>
-__global__ __launch_bounds__(64) void rs_fft_kernel(FftArgs a) {
+// waves_per_eu(2): at N=256 the decode variant otherwise takes 256 VGPRs + 25
+// AGPRs (one wave per SIMD); with the hint it fits 256 with no scratch
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void rs_fft_kernel(FftArgs a) {
     constexpr int W = 1 << LOGW;
     constexpr int G = 3;   // encode: outputs are stored in groups of 2^G rows
 #ifndef RBC_FFT_GD
