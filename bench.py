@@ -150,12 +150,16 @@ def main():
     ctxs = [ctx] + [ca.Context(n, f, device=dev) for _ in range(nstreams - 1)]  # own decode workspace each
     bounds = [(g * I // nstreams, (g + 1) * I // nstreams) for g in range(nstreams)]
     stream = streams[0]
-    ev = {name: ca.Event() for name in ("t0", "enc", "leaf", "tree", "fault", "verify", "interp", "gather")}
+    stage_names = ("t0", "enc", "leaf", "tree", "fault", "verify", "interp", "gather")
+    # one event set per timed step: stage times are read after the closing
+    # barrier, so the timed loop never waits on the host between steps
+    ev_sets = [{name: ca.Event() for name in stage_names} for _ in range(max(args.steps, 3))]
 
     def at(buf, i0, per):
         return buf.value + i0 * per
 
-    def step(timed):
+    def step(ev):
+        timed = ev is not None
         for g, (i0, i1) in enumerate(bounds):
             st, cx, cnt = streams[g].ptr, ctxs[g], i1 - i0
             rec = timed and g == 0  # per-stage events on stream 0 (group 0)
@@ -240,7 +244,7 @@ def main():
         d_roots = last_set["roots"]  # the set the last decode (and gather) read
     else:
         for _ in range(args.warmup):
-            step(False)
+            step(None)
     barrier()
     # correctness guard on the warmed-up state: every instance must decode
     status = np.frombuffer(d_status.download().tobytes(), dtype=np.int32)
@@ -260,21 +264,22 @@ def main():
         for t in range(args.warmup, args.warmup + args.steps):
             pstep(t)
     else:
-        for _ in range(args.steps):
-            step(True)
-            for s_ in streams:
-                s_.sync()
-            for a, b in zip(order[:-1], order[1:]):
-                stage_ms[b] += ev[a].elapsed_ms(ev[b])
+        for t in range(args.steps):
+            step(ev_sets[t])
     barrier()
     elapsed = time.perf_counter() - t0
+    if not pipe:
+        for ev in ev_sets[: args.steps]:
+            for a, b in zip(order[:-1], order[1:]):
+                stage_ms[b] += ev[a].elapsed_ms(ev[b])
     if pipe:
         # per-stage (and roofline) timings from an isolated serial pass: under
         # the overlap, one kernel's event span includes the other stream's work
         d_shards, d_leaves_p, d_roots, d_branches = (sets[0][x] for x in ("shards", "leaves", "roots", "branches"))
         iso = 3
-        for _ in range(iso):
-            step(True)
+        for it in range(iso):
+            ev = ev_sets[it]
+            step(ev)
             stream.sync()
             for a, b in zip(order[:-1], order[1:]):
                 stage_ms[b] += ev[a].elapsed_ms(ev[b]) * args.steps / iso

@@ -78,6 +78,7 @@ struct MerkleArgs {
     const uint8_t *expect_roots;  // check
     int32_t *status;           // check: in/out
     uint8_t *digests;          // check: [I][32] (nullable)
+    int trees_per_block;       // set by rbc_launch_merkle
 };
 
 struct PrepArgs {
@@ -112,6 +113,7 @@ struct PrepArgs {
 struct JoinArgs {
     int count, k;
     uint32_t chunks;           // 16-byte chunks per instance (= value_pitch / 16)
+    uint32_t blocks_per_inst;  // set by rbc_launch_join
     const uint8_t *shards;     // full codeword rows
     uint64_t inst_pitch;
     uint32_t row_pitch;

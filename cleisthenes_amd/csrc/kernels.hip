@@ -346,86 +346,105 @@ __global__ __launch_bounds__(256) void sha_rows2_kernel(ShaArgs a) {
 }
 
 // ============================================================================
-// merkle: one wave per instance.  BUILD writes root + all N branches;
+// merkle: G trees per 256-thread block.  BUILD writes root + all N branches;
 // CHECK recomputes the root over the re-encoded leaves, compares it with the
-// expected root (interpolate's recheck) and writes the batch digest
-// SHA-256(leaf_0 || .. || leaf_{k-1}).  Node convention (frozen):
+// expected root (interpolate's recheck).  Node convention (frozen):
 // H(L || R), empty padding leaves contribute no bytes.
+// The node hashes of one level of all G trees are packed onto consecutive
+// threads, so the narrow upper levels of a tree fill one wave instead of
+// idling most lanes of one wave per tree (at N = 256: 4.75 instead of 9
+// wave-passes per tree).  Only internal nodes live in LDS ([G][W][8] words,
+// node i of tree g at g*W + i, i in [1, W)); the leaf level reads its children
+// straight from the leaves in HBM.
 // ============================================================================
 template <bool CHECK>
-__global__ __launch_bounds__(64) void merkle_kernel(MerkleArgs a) {
+__global__ __launch_bounds__(256) void merkle_kernel(MerkleArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint32_t *nodes = reinterpret_cast<uint32_t *>(smem);  // [2W][8] big-endian words
-    const int inst = blockIdx.x;
-    const int lane = threadIdx.x;
-    if (CHECK && a.status && a.status[inst] != 0) return;
-    const int W = a.width;
-    const uint8_t *lv = a.leaves + (size_t)inst * a.leaves_inst_pitch;
-    for (int j = lane; j < a.n; j += 64) {
-        uint32_t h[8];
-        load_digest(lv + 32u * j, h);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) nodes[(W + j) * 8 + q] = h[q];
-    }
-    __syncthreads();
-    for (int m = W >> 1; m >= 1; m >>= 1) {
-        for (int i = m + lane; i < 2 * m; i += 64) {
-            const int lc = 2 * i, rc = 2 * i + 1;
-            const bool leaf_level = (lc >= W);
-            const bool lempty = leaf_level && (lc - W >= a.n);
-            const bool rempty = leaf_level && (rc - W >= a.n);
+    uint32_t *nodes = reinterpret_cast<uint32_t *>(smem);
+    const int G = a.trees_per_block, W = a.width, n = a.n;
+    const int inst0 = (int)blockIdx.x * G;
+    const int tid = threadIdx.x;
+    for (int m = W >> 1, lgm = a.depth - 1; m >= 1; m >>= 1, --lgm) {
+        for (int t = tid; t < G * m; t += 256) {
+            const int g = t >> lgm, i = m + (t & (m - 1));
+            const int inst = inst0 + g;
+            if (inst >= a.count) continue;
+            const int lc = 2 * i, rc = lc + 1;
             uint32_t o[8];
-            if (lempty) {
-                sha256_empty(o);
-            } else {
-                uint32_t l[8];
-#pragma unroll
-                for (int q = 0; q < 8; ++q) l[q] = nodes[lc * 8 + q];
-                if (rempty) {
-                    sha256_node32(l, o);
+            if (lc >= W) {  // leaf level: children are leaves lc-W, rc-W (empty past n)
+                const int jl = lc - W, jr = rc - W;
+                const uint8_t *lv = a.leaves + (size_t)inst * a.leaves_inst_pitch;
+                if (jl >= n) {
+                    sha256_empty(o);
                 } else {
-                    uint32_t r[8];
-#pragma unroll
-                    for (int q = 0; q < 8; ++q) r[q] = nodes[rc * 8 + q];
-                    sha256_node64(l, r, o);
+                    uint32_t l[8];
+                    load_digest(lv + 32u * jl, l);
+                    if (jr >= n) {
+                        sha256_node32(l, o);
+                    } else {
+                        uint32_t r[8];
+                        load_digest(lv + 32u * jr, r);
+                        sha256_node64(l, r, o);
+                    }
                 }
-            }
+            } else {
+                uint32_t l[8], r[8];
+                const uint32_t *nl = nodes + ((size_t)g * W + lc) * 8, *nr = nodes + ((size_t)g * W + rc) * 8;
 #pragma unroll
-            for (int q = 0; q < 8; ++q) nodes[i * 8 + q] = o[q];
+                for (int q = 0; q < 8; ++q) { l[q] = nl[q]; r[q] = nr[q]; }
+                sha256_node64(l, r, o);
+            }
+            uint32_t *dst = nodes + ((size_t)g * W + i) * 8;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) dst[q] = o[q];
         }
         __syncthreads();
     }
-    uint32_t root[8];
+    // roots: one thread per tree (W == 1: the root is leaf 0)
+    for (int g = tid; g < G; g += 256) {
+        const int inst = inst0 + g;
+        if (inst >= a.count) continue;
+        uint32_t root[8];
+        if (W == 1) {
+            load_digest(a.leaves + (size_t)inst * a.leaves_inst_pitch, root);
+        } else {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) root[q] = nodes[8 + q];
-    if (!CHECK) {
-        if (lane == 0) store_digest(a.roots + (size_t)inst * 32u, root);
-        if (a.branches) {
-            // branch[j][l] = nodes[((W + j) >> l) ^ 1]; one 16-byte half per item
-            uint8_t *br = a.branches + (size_t)inst * a.br_inst_pitch;
-            const int items = a.n * a.depth * 2;
-            for (int e = lane; e < items; e += 64) {
-                const int half = e & 1, jl = e >> 1;
-                const int j = jl / a.depth, l = jl - j * a.depth;
-                const int node = ((W + j) >> l) ^ 1;
-                const bool empty = (l == 0) && (node - W >= a.n);
-                uint4 v = make_uint4(0, 0, 0, 0);
-                if (!empty) {
-                    const uint32_t *nd = nodes + node * 8 + 4 * half;
-                    v = make_uint4(bswap32(nd[0]), bswap32(nd[1]), bswap32(nd[2]), bswap32(nd[3]));
-                }
-                *reinterpret_cast<uint4 *>(br + (size_t)jl * 32u + 16u * half) = v;
-            }
+            for (int q = 0; q < 8; ++q) root[q] = nodes[((size_t)g * W + 1) * 8 + q];
         }
-    } else {
-        uint32_t ex[8];
-        load_digest(a.expect_roots + (size_t)inst * 32u, ex);
-        bool ok = true;
+        if (!CHECK) {
+            store_digest(a.roots + (size_t)inst * 32u, root);
+        } else {
+            if (a.status && a.status[inst] != 0) continue;
+            uint32_t ex[8];
+            load_digest(a.expect_roots + (size_t)inst * 32u, ex);
+            bool ok = true;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) ok = ok && (ex[q] == root[q]);
-        if (lane == 0) {
+            for (int q = 0; q < 8; ++q) ok = ok && (ex[q] == root[q]);
             if (a.status) a.status[inst] = ok ? 0 : RBC_ERR_ROOT_MISMATCH;
             if (a.roots) store_digest(a.roots + (size_t)inst * 32u, root);
+        }
+    }
+    if (!CHECK && a.branches) {
+        // branch[j][l] = node ((W + j) >> l) ^ 1; one 16-byte half per item.
+        // Level 0 siblings are leaves (zero slot when past n).
+        const int items = n * a.depth * 2;
+        for (int e = tid; e < G * items; e += 256) {
+            const int g = e / items, r = e - g * items;
+            const int inst = inst0 + g;
+            if (inst >= a.count) continue;
+            const int half = r & 1, jl = r >> 1;
+            const int j = jl / a.depth, l = jl - j * a.depth;
+            const int node = ((W + j) >> l) ^ 1;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (l == 0) {
+                if (node - W < n)
+                    v = *reinterpret_cast<const uint4 *>(a.leaves + (size_t)inst * a.leaves_inst_pitch +
+                                                         32u * (node - W) + 16u * half);
+            } else {
+                const uint32_t *nd = nodes + ((size_t)g * W + node) * 8 + 4 * half;
+                v = make_uint4(bswap32(nd[0]), bswap32(nd[1]), bswap32(nd[2]), bswap32(nd[3]));
+            }
+            *reinterpret_cast<uint4 *>(a.branches + (size_t)inst * a.br_inst_pitch + (size_t)jl * 32u + 16u * half) = v;
         }
     }
 }
@@ -795,52 +814,70 @@ __global__ __launch_bounds__(256) void decode_prepare_fft_kernel(PrepArgs a, con
 }
 
 // ============================================================================
-// join: value = data shards 0..k-1 concatenated (k*S bytes, pad kept), one
-// thread per aligned 16-byte output chunk (a chunk may straddle two rows).
+// join: value = data shards 0..k-1 concatenated (k*S bytes, pad kept).  One
+// block covers JOIN_U x 256 aligned 16-byte output chunks of ONE instance
+// (blockIdx.x = inst * blocks_per_inst + tile, a scalar division); a chunk may
+// straddle two rows.  The row index o / S comes from a float reciprocal with a
+// +-1 correction (o < 2^32, j < 256: the estimate is never further off), and
+// all loads of a thread are issued before its stores.
 // ============================================================================
+constexpr int JOIN_U = 4;
 __global__ __launch_bounds__(256) void join_kernel(JoinArgs a) {
-    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (long)a.count * a.chunks) return;
-    const int inst = (int)(t / a.chunks);
-    const uint32_t ch = (uint32_t)(t - (long)inst * a.chunks);
+    const int inst = (int)(blockIdx.x / a.blocks_per_inst);
+    const uint32_t tile = blockIdx.x - (uint32_t)inst * a.blocks_per_inst;
     if (a.status && a.status[inst] != 0) return;
     const uint32_t S = inst_len(a.lens, a.uniform_len, inst);
     const uint32_t total = S * (uint32_t)a.k;
-    const uint32_t o = ch * 16u;
-    if (o >= a.value_pitch) return;
-    uint4 *dst = reinterpret_cast<uint4 *>(a.values + (size_t)inst * a.value_pitch + o);
-    if (o >= total) { *dst = make_uint4(0, 0, 0, 0); return; }
+    uint8_t *vrow = a.values + (size_t)inst * a.value_pitch;
     const uint8_t *rows = a.shards + (size_t)inst * a.inst_pitch;
     const rsrc_t r = make_rsrc(rows, a.inst_bytes);
+    uint4 v[JOIN_U];
     if (S >= 16) {
-        const uint32_t j0 = o / S;
-        const uint32_t s0 = o - j0 * S;
-        uint4 v = bload16(r, j0 * a.row_pitch + s0);
-        const int c0 = (int)min(16u, S - s0);
-        if (c0 < 16) {
-            // bytes c0..15 come from the start of row j0+1: read the 16 bytes
-            // that END at row j0+1 byte 16-c0, then blend by byte mask
-            uint4 w = make_uint4(0, 0, 0, 0);
-            if (j0 + 1 < (uint32_t)a.k) w = bload16(r, (j0 + 1) * a.row_pitch - (uint32_t)c0);
-            const uint4 m = mask16(make_uint4(~0u, ~0u, ~0u, ~0u), c0);
-            v.x = (v.x & m.x) | (w.x & ~m.x);
-            v.y = (v.y & m.y) | (w.y & ~m.y);
-            v.z = (v.z & m.z) | (w.z & ~m.z);
-            v.w = (v.w & m.w) | (w.w & ~m.w);
+        const float invS = 1.0f / (float)S;
+#pragma unroll
+        for (int u = 0; u < JOIN_U; ++u) {
+            const uint32_t o = ((tile * JOIN_U + u) * 256u + threadIdx.x) * 16u;
+            v[u] = make_uint4(0, 0, 0, 0);
+            if (o >= total) continue;
+            uint32_t j0 = (uint32_t)((float)o * invS);
+            int32_t s0 = (int32_t)(o - j0 * S);
+            if (s0 < 0) { --j0; s0 += (int32_t)S; }
+            if (s0 >= (int32_t)S) { ++j0; s0 -= (int32_t)S; }
+            v[u] = bload16(r, j0 * a.row_pitch + (uint32_t)s0);
+            const int c0 = (int)min(16u, S - (uint32_t)s0);
+            if (c0 < 16) {
+                // bytes c0..15 come from the start of row j0+1: read the 16 bytes
+                // that END at row j0+1 byte 16-c0, then blend by byte mask
+                uint4 w = make_uint4(0, 0, 0, 0);
+                if (j0 + 1 < (uint32_t)a.k) w = bload16(r, (j0 + 1) * a.row_pitch - (uint32_t)c0);
+                const uint4 m = mask16(make_uint4(~0u, ~0u, ~0u, ~0u), c0);
+                v[u].x = (v[u].x & m.x) | (w.x & ~m.x);
+                v[u].y = (v[u].y & m.y) | (w.y & ~m.y);
+                v[u].z = (v[u].z & m.z) | (w.z & ~m.z);
+                v[u].w = (v[u].w & m.w) | (w.w & ~m.w);
+            }
+            if (o + 16u > total) v[u] = mask16(v[u], (int)(total - o));
         }
-        if (o + 16u > total) v = mask16(v, (int)(total - o));
-        *dst = v;
     } else {
         // tiny shards: byte path
-        uint32_t w[4] = {0, 0, 0, 0};
-        for (int b = 0; b < 16; ++b) {
-            const uint32_t g = o + b;
-            if (g >= total) break;
-            const uint32_t j = g / S, off = g - j * S;
-            const uint32_t byte = rows[(size_t)j * a.row_pitch + off];
-            w[b >> 2] |= byte << (8 * (b & 3));
+#pragma unroll
+        for (int u = 0; u < JOIN_U; ++u) {
+            const uint32_t o = ((tile * JOIN_U + u) * 256u + threadIdx.x) * 16u;
+            uint32_t w[4] = {0, 0, 0, 0};
+            for (int b = 0; b < 16; ++b) {
+                const uint32_t g = o + b;
+                if (g >= total) break;
+                const uint32_t j = g / S, off = g - j * S;
+                const uint32_t byte = rows[(size_t)j * a.row_pitch + off];
+                w[b >> 2] |= byte << (8 * (b & 3));
+            }
+            v[u] = make_uint4(w[0], w[1], w[2], w[3]);
         }
-        *dst = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+#pragma unroll
+    for (int u = 0; u < JOIN_U; ++u) {
+        const uint32_t o = ((tile * JOIN_U + u) * 256u + threadIdx.x) * 16u;
+        if (o < a.value_pitch) *reinterpret_cast<uint4 *>(vrow + o) = v[u];
     }
 }
 
@@ -938,9 +975,14 @@ hipError_t rbc_launch_sha_rows(const ShaArgs &a, bool verify, hipStream_t st) {
 
 hipError_t rbc_launch_merkle(const MerkleArgs &a, bool check, hipStream_t st) {
     if (a.count <= 0) return hipSuccess;
-    const size_t lds = (size_t)64 * a.width;
-    if (check) hipLaunchKernelGGL(merkle_kernel<true>, dim3(a.count), dim3(64), lds, st, a);
-    else hipLaunchKernelGGL(merkle_kernel<false>, dim3(a.count), dim3(64), lds, st, a);
+    if (a.width < 1 || a.width > 1024 || (a.width & (a.width - 1)) || (1 << a.depth) != a.width)
+        return hipErrorInvalidValue;
+    MerkleArgs b = a;
+    b.trees_per_block = a.width >= 1024 ? 1 : (1024 / a.width < 64 ? 1024 / a.width : 64);
+    const size_t lds = (size_t)b.trees_per_block * a.width * 32;  // 32 KiB at most
+    const unsigned blocks = (unsigned)((a.count + b.trees_per_block - 1) / b.trees_per_block);
+    if (check) hipLaunchKernelGGL(merkle_kernel<true>, dim3(blocks), dim3(256), lds, st, b);
+    else hipLaunchKernelGGL(merkle_kernel<false>, dim3(blocks), dim3(256), lds, st, b);
     return hipGetLastError();
 }
 
@@ -972,9 +1014,12 @@ hipError_t rbc_launch_decode_prepare(const PrepArgs &a, hipStream_t st) {
 }
 
 hipError_t rbc_launch_join(const JoinArgs &a, hipStream_t st) {
-    const long total = (long)a.count * a.chunks;
-    if (total <= 0) return hipSuccess;
-    hipLaunchKernelGGL(join_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a);
+    if (a.count <= 0 || a.chunks == 0) return hipSuccess;
+    JoinArgs b = a;
+    b.blocks_per_inst = (a.chunks + 256u * JOIN_U - 1) / (256u * JOIN_U);
+    const uint64_t blocks = (uint64_t)a.count * b.blocks_per_inst;
+    if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(join_kernel, dim3((unsigned)blocks), dim3(256), 0, st, b);
     return hipGetLastError();
 }
 
