@@ -104,7 +104,7 @@ struct DevBuf {
 // value assembly beside the regen hashing).  One per independent stream of
 // work: the context's device API has one, every host-API slot has its own.
 struct Ws {
-    DevBuf used, regen, dmat, nmiss, flags, list, counter, rcount, cls;
+    DevBuf used, regen, dmat, nmiss, flags, list, counter, rcount, cls, vleaves;
     hipStream_t aux = nullptr;  // created on first use
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool init() {
@@ -112,7 +112,7 @@ struct Ws {
                hipEventCreateWithFlags(&ev_join, hipEventDisableTiming) == hipSuccess;
     }
     void release() {
-        for (DevBuf *b : {&used, &regen, &dmat, &nmiss, &flags, &list, &counter, &rcount, &cls}) b->release();
+        for (DevBuf *b : {&used, &regen, &dmat, &nmiss, &flags, &list, &counter, &rcount, &cls, &vleaves}) b->release();
         if (aux) (void)hipStreamDestroy(aux);
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         if (ev_join) (void)hipEventDestroy(ev_join);
@@ -352,6 +352,37 @@ int stage_verify(rbc_ctx *c, hipStream_t st, int count, const uint8_t *shards, u
     a.roots = roots;
     a.present = present;
     a.valid = valid;
+    // Shared-path verification: leaves, then one hash per
+    // distinct branch-walk input.  RBC_VERIFY_PATH=0 runs the per-leaf walk.
+    static const bool path_env = [] {
+        const char *e = getenv("RBC_VERIFY_PATH");
+        return !e || atoi(e) != 0;
+    }();
+    if (path_env && c->depth >= 1 && c->width <= 256) {
+        uint8_t *lv = leaves;
+        if (!lv) {
+            std::lock_guard<std::mutex> lk(c->mu);
+            RBC_HIP(c->ws.vleaves.ensure((size_t)count * c->n * 32));
+            lv = c->ws.vleaves.as<uint8_t>();
+        }
+        a.leaves = lv;
+        RBC_HIP(rbc_launch_sha_rows(a, false, st));
+        PathArgs p{};
+        p.count = count;
+        p.n = c->n;
+        p.width = c->width;
+        p.lg_width = c->depth;
+        p.depth = c->depth;
+        p.leaves = lv;
+        p.leaves_inst_pitch = (uint64_t)c->n * 32;
+        p.branches = branches;
+        p.br_inst_pitch = (uint64_t)c->n * c->depth * 32;
+        p.roots = roots;
+        p.present = present;
+        p.valid = valid;
+        RBC_HIP(rbc_launch_merkle_path(p, st));
+        return RBC_OK;
+    }
     RBC_HIP(rbc_launch_sha_rows(a, true, st));
     return RBC_OK;
 }

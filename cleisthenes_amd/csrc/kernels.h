@@ -81,6 +81,20 @@ struct MerkleArgs {
     int trees_per_block;       // set by rbc_launch_merkle
 };
 
+// merkle_path_kernel: shared-path branch verification over precomputed leaves
+struct PathArgs {
+    int count, n, width, lg_width, depth;
+    const uint8_t *leaves;     // [I][N][32]
+    uint64_t leaves_inst_pitch;
+    const uint8_t *branches;   // [I][N][d][32]
+    uint64_t br_inst_pitch;
+    const uint8_t *roots;      // [I][32]
+    const uint8_t *present;    // [I][N] (nullable -> all present)
+    const int32_t *status;     // nullable
+    uint8_t *valid;            // [I][N]
+    int inst_per_block;        // set by rbc_launch_merkle_path
+};
+
 struct PrepArgs {
     int count, n, k;
     const uint8_t *valid;      // [I][valid_stride]
@@ -177,6 +191,7 @@ int rbc_gf_pick_rc(int R, int rcmax);
 hipError_t rbc_launch_gf_rows(const GfArgs &a, hipStream_t st);
 hipError_t rbc_launch_sha_rows(const ShaArgs &a, bool verify, hipStream_t st);
 hipError_t rbc_launch_merkle(const MerkleArgs &a, bool check, hipStream_t st);
+hipError_t rbc_launch_merkle_path(const PathArgs &a, hipStream_t st);
 hipError_t rbc_launch_decode_prepare(const PrepArgs &a, hipStream_t st);
 hipError_t rbc_launch_digest(const uint8_t *leaves, uint64_t leaves_inst_pitch, int k, const int32_t *status,
                              uint8_t *digests, int count, hipStream_t st);

@@ -450,6 +450,134 @@ __global__ __launch_bounds__(256) void merkle_kernel(MerkleArgs a) {
 }
 
 // ============================================================================
+// merkle_path: batched branch verification with shared paths (ECHO side of
+// validateMessage, rbc/rbc.go:92-95, for all N shards of an instance).
+// Leaf j's walk is h <- H(order_l(h, branch_j[l])) for l = 0..d-1 and it is
+// valid iff the end equals the root.  Walks of leaves under one level-(l+1)
+// node hash the SAME 64-byte input whenever their inputs agree -- the honest
+// case -- so each level hashes every distinct input once: the group's first
+// participating leaf (rep) owns one hash task, and any leaf whose input
+// differs from the rep's owns one more (its own walk).  Each leaf then takes
+// the digest of the task whose input equals its own, which is exactly the
+// value its own walk would compute: the result is bit-identical to the
+// per-leaf walk for every input, honest or not.  Per instance that is W-1
+// node hashes plus one per divergent (leaf, level) instead of N*d.
+// G = 256/W instances per 256-thread block (thread t: instance t/W, leaf
+// t%W); the tasks of all G instances are packed onto consecutive threads.
+// Leaves come from sha_rows_kernel<false>; this kernel writes valid[].
+// ============================================================================
+__global__ __launch_bounds__(256) void merkle_path_kernel(PathArgs a) {
+    __shared__ uint32_t s_pair[256][17];  // +1 word: conflict-free per-thread rows; an owner's
+                                          // task digest overwrites words 0..7 of its own row
+    __shared__ uint8_t s_empty[256];
+    __shared__ uint16_t s_owner[256];
+    __shared__ uint64_t s_wmask[4];
+    __shared__ int s_wcnt[4];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int W = a.width, lgW = a.lg_width;
+    const int g = t >> lgW, j = t & (W - 1);
+    const int inst = (int)blockIdx.x * a.inst_per_block + g;
+    const bool inst_ok = g < a.inst_per_block && inst < a.count && !(a.status && a.status[inst] != 0);
+    const bool part = inst_ok && j < a.n && (!a.present || a.present[(size_t)inst * a.n + j] != 0);
+    const uint64_t pm = __ballot(part);
+    if (lane == 0) s_wmask[wv] = pm;
+    uint32_t x[8];
+    if (part) load_digest(a.leaves + (size_t)inst * a.leaves_inst_pitch + 32u * j, x);
+    const uint8_t *br = a.branches + (size_t)(inst_ok ? inst : 0) * a.br_inst_pitch + (size_t)j * a.depth * 32u;
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int l = 0; l < a.depth; ++l) {
+        // 1. this leaf's ordered input (left || right) for level l
+        if (part) {
+            const bool empty = (l == 0) && ((j ^ 1) >= a.n);
+            uint32_t sib[8];
+            if (empty) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) sib[q] = 0;
+            } else {
+                load_digest(br + 32u * l, sib);
+            }
+            const bool right = (j >> l) & 1;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                s_pair[t][q] = right ? sib[q] : x[q];
+                s_pair[t][8 + q] = right ? x[q] : sib[q];
+            }
+            s_empty[t] = empty ? 1 : 0;
+        }
+        __syncthreads();
+        // 2. rep = first participating thread of this leaf's level-(l+1) group
+        int rep = t;
+        bool owner = false;
+        if (part) {
+            const int gs = 2 << l;
+            const int t0 = t & ~(gs - 1), t1 = t0 + gs;
+            for (int w = t0 >> 6; w <= (t1 - 1) >> 6; ++w) {
+                uint64_t m = s_wmask[w];
+                const int lo = t0 - w * 64, hi = t1 - w * 64;
+                if (lo > 0) m &= ~0ull << lo;
+                if (hi < 64) m &= (1ull << hi) - 1ull;
+                if (m) { rep = w * 64 + __builtin_ctzll(m); break; }
+            }
+            bool same = true;
+            if (rep != t) {
+                same = s_empty[t] == s_empty[rep];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) same = same && (s_pair[t][q] == s_pair[rep][q]);
+            }
+            owner = (rep == t) || !same;
+        }
+        // 3. number the hash tasks (owners) across the block
+        const uint64_t om = __ballot(owner);
+        if (lane == 0) s_wcnt[wv] = __popcll(om);
+        __syncthreads();
+        int base = 0, total = 0;
+        for (int w = 0; w < 4; ++w) {
+            if (w < wv) base += s_wcnt[w];
+            total += s_wcnt[w];
+        }
+        if (owner) s_owner[base + __popcll(om & below)] = (uint16_t)t;
+        __syncthreads();
+        // 4. hash the tasks on consecutive threads
+        for (int i = t; i < total; i += 256) {
+            const int o = s_owner[i];
+            uint32_t L[8], o8[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) L[q] = s_pair[o][q];
+            if (s_empty[o]) {
+                sha256_node32(L, o8);
+            } else {
+                uint32_t R[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) R[q] = s_pair[o][8 + q];
+                sha256_node64(L, R, o8);
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) s_pair[o][q] = o8[q];
+        }
+        __syncthreads();
+        // 5. every walk takes the digest of the task with its input (the
+        //    rep's task unless it owns one)
+        if (part) {
+            const int o = owner ? t : rep;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) x[q] = s_pair[o][q];
+        }
+        __syncthreads();
+    }
+    if (inst_ok && j < a.n) {
+        bool ok = false;
+        if (part) {
+            uint32_t root[8];
+            load_digest(a.roots + (size_t)inst * 32u, root);
+            ok = true;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) ok = ok && (x[q] == root[q]);
+        }
+        a.valid[(size_t)inst * a.n + j] = ok ? 1 : 0;
+    }
+}
+
+// ============================================================================
 // digest: batch digest = SHA-256(leaf_0 || .. || leaf_{k-1}) of every
 // instance that passed the root recheck, one lane per instance.  The message
 // is the first 32k bytes of the instance's leaves; the last partial block is
@@ -970,6 +1098,17 @@ hipError_t rbc_launch_sha_rows(const ShaArgs &a, bool verify, hipStream_t st) {
     dim3 grid((unsigned)((total + 255) / 256));
     if (verify) hipLaunchKernelGGL(sha_rows_kernel<true>, grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(sha_rows_kernel<false>, grid, dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t rbc_launch_merkle_path(const PathArgs &a, hipStream_t st) {
+    if (a.count <= 0) return hipSuccess;
+    if (a.width < 1 || a.width > 256 || (1 << a.lg_width) != a.width || a.depth != a.lg_width || a.n > a.width)
+        return hipErrorInvalidValue;
+    PathArgs b = a;
+    b.inst_per_block = 256 / a.width;
+    hipLaunchKernelGGL(merkle_path_kernel, dim3((unsigned)((a.count + b.inst_per_block - 1) / b.inst_per_block)),
+                       dim3(256), 0, st, b);
     return hipGetLastError();
 }
 

@@ -561,3 +561,56 @@ def test_two_rows_per_lane_sha_path(gpu, ref, n, f, S):
     assert (pl.arr("status", np.int32) == 0).all()
     out = pl.arr("out", shape=(I, pl.opitch))
     assert np.array_equal(out[:, :B], pl.values[:, :B])
+
+
+@pytest.mark.parametrize("n,f,B,I", [(4, 1, 1024, 8), (7, 2, 333, 8), (13, 4, 5 * 55, 8), (16, 5, 600, 8),
+                                     (128, 42, 44 * 70, 8), (256, 85, 86 * 9, 8)])
+def test_device_verify_shared_paths_adversarial(gpu, ref, n, f, B, I):
+    """rbc_dev_verify (shared-path kernel: one hash per distinct walk input)
+    against the per-leaf oracle walk on adversarial ECHO sets: corrupted
+    shards, corrupted branch slots at every level, branches spliced from a
+    different tree, a wrong root, garbage in the empty level-0 slot, sparse
+    present masks.  valid[i][j] must equal present && oracle verify."""
+    pl = Pipeline(gpu, n, f, B, I, seed=1000 + n, corrupt_frac=0.0, present_n=n)
+    pl.commit()
+    c, b, d, S = pl.ctx, pl.b, pl.d, pl.S
+    sh = pl.shards().copy()
+    roots = pl.arr("roots", shape=(I, 32)).copy()
+    brs = pl.arr("branches", shape=(I, n, d, 32)).copy()
+    rng = np.random.default_rng(77 + n)
+    present = np.ones((I, n), np.uint8)
+    # 1: one corrupted shard; 2: one corrupted branch slot per level;
+    # 3: leaves 0..n/2 carry instance 0's shards + branches (another tree);
+    # 4: wrong root; 5: 30% of branch slots corrupted; 6: sparse present;
+    # 7: garbage in every (empty or not) level-0 slot of odd-N last leaf + a
+    #    shard corrupted so that its sibling's walk diverges
+    sh[1, rng.integers(n), rng.integers(S)] ^= 0x5A
+    for l in range(d):
+        brs[2, rng.integers(n), l, rng.integers(32)] ^= 1
+    h = max(1, n // 2)
+    sh[3, :h] = sh[0, :h]
+    brs[3, :h] = brs[0, :h]
+    roots[4, 0] ^= 0x80
+    m = rng.random((n, d)) < 0.3
+    brs[5][m] ^= 0xFF
+    present[6] = (rng.random(n) < 0.5).astype(np.uint8)
+    brs[7, n - 1, 0] = 0xEE
+    sh[7, 0, 0] ^= 1
+    b["shards"].upload(sh)
+    b["branches"].upload(brs)
+    b["roots"].upload(roots)
+    b["present"].upload(present)
+    b["valid"].upload(np.full((I, n), 7, np.uint8))
+    c.dev_verify(None, I, b["shards"], pl.spitch, None, S, b["branches"], b["roots"], b["present"], b["valid"],
+                 b["leaves_r"])
+    got = pl.arr("valid", shape=(I, n))
+    leaves = pl.arr("leaves_r", shape=(I, n, 32))
+    for i in range(I):
+        for j in range(n):
+            slots = brs[i, j].copy()
+            if (j ^ 1) >= n:
+                slots[0] = 0  # device form: an empty level-0 sibling is a zero slot
+            want = bool(present[i, j]) and ref.verify(n, sh[i, j, :S], j, slots, bytes(roots[i]))
+            assert got[i, j] == int(want), (n, i, j)
+            assert leaves[i, j].tobytes() == ref.sha256(sh[i, j, :S].tobytes()), (n, i, j)
+    assert got[0].all() and not got[4].any()
