@@ -614,3 +614,46 @@ def test_device_verify_shared_paths_adversarial(gpu, ref, n, f, B, I):
             assert got[i, j] == int(want), (n, i, j)
             assert leaves[i, j].tobytes() == ref.sha256(sh[i, j, :S].tobytes()), (n, i, j)
     assert got[0].all() and not got[4].any()
+
+
+def test_device_verify_shared_paths_large_grid(gpu, ref):
+    """The shared-path kernel over a large grid: 4096 instances at N = 256, 64 of them adversarial (corrupted shards and
+    branch slots at random levels, a wrong root, a spliced subtree), checked
+    against the per-leaf oracle walk; the honest rest must be all-valid."""
+    n, f, B, I = 256, 85, 86 * 9, 4096
+    pl = Pipeline(gpu, n, f, B, I, seed=4242, corrupt_frac=0.0, present_n=n)
+    pl.commit()
+    c, b, d, S = pl.ctx, pl.b, pl.d, pl.S
+    sh = pl.shards().copy()
+    roots = pl.arr("roots", shape=(I, 32)).copy()
+    brs = pl.arr("branches", shape=(I, n, d, 32)).copy()
+    rng = np.random.default_rng(99)
+    bad = sorted(rng.choice(I, 64, replace=False).tolist())
+    for q, i in enumerate(bad):
+        kind = q % 4
+        if kind == 0:
+            sh[i, rng.integers(n), rng.integers(S)] ^= 0x11
+        elif kind == 1:
+            for _ in range(3):
+                brs[i, rng.integers(n), rng.integers(d), rng.integers(32)] ^= 4
+        elif kind == 2:
+            roots[i, 5] ^= 1
+        else:
+            o = (i + 1) % I
+            lo = 32 * rng.integers(8)
+            sh[i, lo:lo + 32] = sh[o, lo:lo + 32]
+            brs[i, lo:lo + 32] = brs[o, lo:lo + 32]
+    b["shards"].upload(sh)
+    b["branches"].upload(brs)
+    b["roots"].upload(roots)
+    c.dev_verify(None, I, b["shards"], pl.spitch, None, S, b["branches"], b["roots"], None, b["valid"],
+                 b["leaves_r"])
+    got = pl.arr("valid", shape=(I, n))
+    honest = np.ones(I, bool)
+    honest[bad] = False
+    assert got[honest].all()
+    for i in bad:
+        for j in range(n):
+            want = ref.verify(n, sh[i, j, :S], j, brs[i, j], bytes(roots[i]))
+            assert got[i, j] == int(want), (i, j)
+        assert not got[i].all()
