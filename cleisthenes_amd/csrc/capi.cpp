@@ -358,7 +358,13 @@ int stage_verify(rbc_ctx *c, hipStream_t st, int count, const uint8_t *shards, u
         const char *e = getenv("RBC_VERIFY_PATH");
         return !e || atoi(e) != 0;
     }();
-    if (path_env && c->depth >= 1 && c->width <= 256) {
+    // The per-leaf walk costs 2d compressions per row on top of the leaf's
+    // ceil((S+9)/64); the shared-path form pays off where that walk is a real
+    // share (C4: 16 vs 13) and only adds a launch where it is not (C2: 14 vs
+    // 373, measured equal alone and slower beside a second stream).
+    const uint32_t blocks_per_row = shard_lens ? 0u : (uniform_shard_len + 9 + 63) / 64;
+    const bool path_pays = shard_lens || 16u * (uint32_t)c->depth >= blocks_per_row;
+    if (path_env && path_pays && c->depth >= 1 && c->width <= 256) {
         uint8_t *lv = leaves;
         if (!lv) {
             std::lock_guard<std::mutex> lk(c->mu);

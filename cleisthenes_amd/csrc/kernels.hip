@@ -346,26 +346,28 @@ __global__ __launch_bounds__(256) void sha_rows2_kernel(ShaArgs a) {
 }
 
 // ============================================================================
-// merkle: G trees per 256-thread block.  BUILD writes root + all N branches;
+// merkle: G trees per one-wave block.  BUILD writes root + all N branches;
 // CHECK recomputes the root over the re-encoded leaves, compares it with the
 // expected root (interpolate's recheck).  Node convention (frozen):
 // H(L || R), empty padding leaves contribute no bytes.
 // The node hashes of one level of all G trees are packed onto consecutive
-// threads, so the narrow upper levels of a tree fill one wave instead of
-// idling most lanes of one wave per tree (at N = 256: 4.75 instead of 9
-// wave-passes per tree).  Only internal nodes live in LDS ([G][W][8] words,
+// lanes, so the narrow upper levels of a tree share a pass instead of idling
+// most lanes of one wave per tree (N = 256, G = 2: 6 instead of 9 passes per
+// tree; N = 128, G = 2: 4.5 instead of 7).  One-wave blocks: a 256-thread
+// form measured the same alone but slowed the bench's two-stream pipeline
+// (it is the hardest block shape to place beside the other stream's kernels).  Only internal nodes live in LDS ([G][W][8] words,
 // node i of tree g at g*W + i, i in [1, W)); the leaf level reads its children
 // straight from the leaves in HBM.
 // ============================================================================
 template <bool CHECK>
-__global__ __launch_bounds__(256) void merkle_kernel(MerkleArgs a) {
+__global__ __launch_bounds__(64) void merkle_kernel(MerkleArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t *nodes = reinterpret_cast<uint32_t *>(smem);
     const int G = a.trees_per_block, W = a.width, n = a.n;
     const int inst0 = (int)blockIdx.x * G;
     const int tid = threadIdx.x;
     for (int m = W >> 1, lgm = a.depth - 1; m >= 1; m >>= 1, --lgm) {
-        for (int t = tid; t < G * m; t += 256) {
+        for (int t = tid; t < G * m; t += 64) {
             const int g = t >> lgm, i = m + (t & (m - 1));
             const int inst = inst0 + g;
             if (inst >= a.count) continue;
@@ -401,7 +403,7 @@ __global__ __launch_bounds__(256) void merkle_kernel(MerkleArgs a) {
         __syncthreads();
     }
     // roots: one thread per tree (W == 1: the root is leaf 0)
-    for (int g = tid; g < G; g += 256) {
+    for (int g = tid; g < G; g += 64) {
         const int inst = inst0 + g;
         if (inst >= a.count) continue;
         uint32_t root[8];
@@ -428,7 +430,7 @@ __global__ __launch_bounds__(256) void merkle_kernel(MerkleArgs a) {
         // branch[j][l] = node ((W + j) >> l) ^ 1; one 16-byte half per item.
         // Level 0 siblings are leaves (zero slot when past n).
         const int items = n * a.depth * 2;
-        for (int e = tid; e < G * items; e += 256) {
+        for (int e = tid; e < G * items; e += 64) {
             const int g = e / items, r = e - g * items;
             const int inst = inst0 + g;
             if (inst >= a.count) continue;
@@ -1123,11 +1125,15 @@ hipError_t rbc_launch_merkle(const MerkleArgs &a, bool check, hipStream_t st) {
     if (a.width < 1 || a.width > 1024 || (a.width & (a.width - 1)) || (1 << a.depth) != a.width)
         return hipErrorInvalidValue;
     MerkleArgs b = a;
-    b.trees_per_block = a.width >= 1024 ? 1 : (1024 / a.width < 64 ? 1024 / a.width : 64);
-    const size_t lds = (size_t)b.trees_per_block * a.width * 32;  // 32 KiB at most
+    // up to 512 / W trees per block (<= 64), but keep >= 512 blocks so that a
+    // small batch still spreads over every CU (C2 and C4: 2 trees per block)
+    int g = a.width >= 512 ? 1 : (512 / a.width < 64 ? 512 / a.width : 64);
+    while (g > 1 && (a.count + g - 1) / g < 512) g >>= 1;
+    b.trees_per_block = g;
+    const size_t lds = (size_t)b.trees_per_block * a.width * 32;  // 16 KiB at most
     const unsigned blocks = (unsigned)((a.count + b.trees_per_block - 1) / b.trees_per_block);
-    if (check) hipLaunchKernelGGL(merkle_kernel<true>, dim3(blocks), dim3(256), lds, st, b);
-    else hipLaunchKernelGGL(merkle_kernel<false>, dim3(blocks), dim3(256), lds, st, b);
+    if (check) hipLaunchKernelGGL(merkle_kernel<true>, dim3(blocks), dim3(64), lds, st, b);
+    else hipLaunchKernelGGL(merkle_kernel<false>, dim3(blocks), dim3(64), lds, st, b);
     return hipGetLastError();
 }
 
