@@ -49,13 +49,16 @@ int codec_default() {
 }
 
 // rows per chunk for the FFT codec's missing-data GF pass (RBC_GF_MDRC)
-int gf_md_rcmax() {
+int gf_md_rcmax(uint32_t shard_pitch) {
+    // rows per GF chunk for interpolate's missing data rows: 8 with 4 KiB
+    // column tiles; 4 with the one-wave tiles of short rows (C4: twice the
+    // blocks per CU for the 64-thread blocks, 2.32 -> 2.00 ms)
     static const int v = [] {
         const char *e = getenv("RBC_GF_MDRC");
         int x = e ? atoi(e) : 0;
-        return (x >= 1 && x <= 48) ? x : 8;
+        return (x >= 1 && x <= 48) ? x : 0;
     }();
-    return v;
+    return v ? v : (shard_pitch <= 2048 ? 4 : 8);
 }
 
 int tree_width(int n) {
@@ -453,9 +456,9 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
         g.count = count;
         g.R = rmax;
         g.K = c->k;
-        g.rc = rbc_gf_pick_rc(rmax, gf_md_rcmax());
+        g.rc = rbc_gf_pick_rc(rmax, gf_md_rcmax(shard_pitch));
         // short rows (C4: 763 B) would leave most of a 4 KiB tile idle
-        g.tpb = (g.rc == 8 && shard_pitch <= 2048) ? 64 : 256;
+        g.tpb = ((g.rc == 8 || g.rc == 4) && shard_pitch <= 2048) ? 64 : 256;
         g.tiles = (int)((shard_pitch + 16 * g.tpb - 1) / (16 * g.tpb));
         g.mode = GF_MODE_DECODE;
         g.in = shards;

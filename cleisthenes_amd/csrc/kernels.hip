@@ -1056,6 +1056,7 @@ hipError_t rbc_launch_gf_rows(const GfArgs &a, hipStream_t st) {
     if (a.count <= 0 || (a.R <= 0 && !a.copy)) return hipSuccess;
     if (a.tpb == 64) {  // short rows: 1 KiB column tiles (one wave per block)
         if (a.rc == 8) return launch_gf_rc<8, 64>(a, st);
+        if (a.rc == 4) return launch_gf_rc<4, 64>(a, st);
         return hipErrorInvalidValue;
     }
     if (a.tpb != 0 && a.tpb != 256) return hipErrorInvalidValue;
