@@ -16,6 +16,7 @@ from .rbc import (  # noqa: F401
     Stream,
     Event,
     device_count,
+    pinned_empty,
 )
 
-__all__ = ["Batcher", "Context", "DeviceBuffer", "Encoder", "RBCError", "Stream", "Event", "device_count"]
+__all__ = ["Batcher", "Context", "DeviceBuffer", "Encoder", "RBCError", "Stream", "Event", "device_count", "pinned_empty"]

@@ -1022,6 +1022,23 @@ int submit(rbc_ctx *c, Slot &s, uint64_t *ticket, std::function<int()> finish) {
 }  // namespace
 }  // extern "C++"
 
+// Caller memory that is already pinned (rbc_host_alloc / hipHostMalloc /
+// hipHostRegister) is copied to and from directly: no staging memcpy.  A Go
+// batcher that keeps its request and result rings in rbc_host_alloc memory
+// gets the PCIe-only path.
+static bool host_pinned(const void *p, size_t bytes) {
+    if (!p) return false;
+    for (const void *q : {p, (const void *)((const uint8_t *)p + (bytes ? bytes - 1 : 0))}) {
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        if (a.type != hipMemoryTypeHost) return false;
+    }
+    return true;
+}
+
 int rbc_shard_commit(rbc_ctx *c, int count, const uint8_t *const *values, const size_t *value_lens,
                      uint8_t *shards_out, size_t shard_pitch, uint32_t *shard_lens_out, uint8_t *roots_out,
                      uint8_t *branches_out, uint64_t *ticket) {
@@ -1056,13 +1073,25 @@ int rbc_shard_commit(rbc_ctx *c, int count, const uint8_t *const *values, const 
     RBC_HIP(s.h_out.ensure(sh_bytes + (size_t)count * 32 + br_bytes));
     uint8_t *stage = s.h_in.as<uint8_t>();
     uint32_t *lens = reinterpret_cast<uint32_t *>(stage + (size_t)count * vpitch);
-    parallel_for(count, vpitch, [&](int i) {
-        memcpy(stage + (size_t)i * vpitch, values[i], value_lens[i]);
-        memset(stage + (size_t)i * vpitch + value_lens[i], 0, vpitch - value_lens[i]);
-        lens[i] = (uint32_t)value_lens[i];
-        lens[count + i] = (uint32_t)((value_lens[i] + c->k - 1) / c->k);
-    });
-    RBC_HIP(hipMemcpyAsync(s.d_values.p, stage, (size_t)count * vpitch, hipMemcpyHostToDevice, st));
+    bool in_direct = true;
+    for (int i = 0; i < count && in_direct; ++i) in_direct = host_pinned(values[i], value_lens[i]);
+    if (in_direct) {
+        // the encode kernel masks the Split pad (bytes past len are never used)
+        for (int i = 0; i < count; ++i) {
+            lens[i] = (uint32_t)value_lens[i];
+            lens[count + i] = (uint32_t)((value_lens[i] + c->k - 1) / c->k);
+            RBC_HIP(hipMemcpyAsync(s.d_values.as<uint8_t>() + (size_t)i * vpitch, values[i], value_lens[i],
+                                   hipMemcpyHostToDevice, st));
+        }
+    } else {
+        parallel_for(count, vpitch, [&](int i) {
+            memcpy(stage + (size_t)i * vpitch, values[i], value_lens[i]);
+            memset(stage + (size_t)i * vpitch + value_lens[i], 0, vpitch - value_lens[i]);
+            lens[i] = (uint32_t)value_lens[i];
+            lens[count + i] = (uint32_t)((value_lens[i] + c->k - 1) / c->k);
+        });
+        RBC_HIP(hipMemcpyAsync(s.d_values.p, stage, (size_t)count * vpitch, hipMemcpyHostToDevice, st));
+    }
     RBC_HIP(hipMemcpyAsync(s.d_lens.p, lens, (size_t)count * 8, hipMemcpyHostToDevice, st));
     const uint32_t *d_vlens = s.d_lens.as<uint32_t>(), *d_slens = d_vlens + count;
     int rc = stage_encode(c, st, count, s.d_values.as<uint8_t>(), vpitch, d_vlens, 0, s.d_shards.as<uint8_t>(),
@@ -1073,18 +1102,28 @@ int rbc_shard_commit(rbc_ctx *c, int count, const uint8_t *const *values, const 
                                      s.d_branches.as<uint8_t>());
     if (rc) return rc;
     uint8_t *o_sh = s.h_out.as<uint8_t>(), *o_rt = o_sh + sh_bytes, *o_br = o_rt + (size_t)count * 32;
-    RBC_HIP(hipMemcpyAsync(o_sh, s.d_shards.p, sh_bytes, hipMemcpyDeviceToHost, st));
-    RBC_HIP(hipMemcpyAsync(o_rt, s.d_roots.p, (size_t)count * 32, hipMemcpyDeviceToHost, st));
-    if (branches_out && d > 0) RBC_HIP(hipMemcpyAsync(o_br, s.d_branches.p, br_bytes, hipMemcpyDeviceToHost, st));
+    const size_t br_out = (size_t)count * n * d * 32;
+    const bool sh_direct = host_pinned(shards_out, ((size_t)count * n - 1) * shard_pitch + Smax);
+    const bool rt_direct = host_pinned(roots_out, (size_t)count * 32);
+    const bool br_direct = branches_out && d > 0 && host_pinned(branches_out, br_out);
+    if (sh_direct)  // Smax bytes per row: the device rows are zero past S_i
+        RBC_HIP(hipMemcpy2DAsync(shards_out, shard_pitch, s.d_shards.p, dpitch, Smax, (size_t)count * n,
+                                 hipMemcpyDeviceToHost, st));
+    else
+        RBC_HIP(hipMemcpyAsync(o_sh, s.d_shards.p, sh_bytes, hipMemcpyDeviceToHost, st));
+    RBC_HIP(hipMemcpyAsync(rt_direct ? roots_out : o_rt, s.d_roots.p, (size_t)count * 32, hipMemcpyDeviceToHost, st));
+    if (branches_out && d > 0)
+        RBC_HIP(hipMemcpyAsync(br_direct ? branches_out : o_br, s.d_branches.p, br_bytes, hipMemcpyDeviceToHost, st));
     return submit(c, s, ticket, [=]() {
-        parallel_for(count, (size_t)n * Smax, [&](int i) {
+        parallel_for(count, sh_direct ? 0 : (size_t)n * Smax, [&](int i) {
             const size_t S = lens[count + i];
-            for (int j = 0; j < n; ++j)  // Smax bytes per row: the device rows are zero past S_i
-                memcpy(shards_out + ((size_t)i * n + j) * shard_pitch, o_sh + ((size_t)i * n + j) * dpitch, Smax);
+            if (!sh_direct)
+                for (int j = 0; j < n; ++j)
+                    memcpy(shards_out + ((size_t)i * n + j) * shard_pitch, o_sh + ((size_t)i * n + j) * dpitch, Smax);
             if (shard_lens_out) shard_lens_out[i] = (uint32_t)S;
         });
-        memcpy(roots_out, o_rt, (size_t)count * 32);
-        if (branches_out && d > 0) memcpy(branches_out, o_br, (size_t)count * n * d * 32);
+        if (!rt_direct) memcpy(roots_out, o_rt, (size_t)count * 32);
+        if (branches_out && d > 0 && !br_direct) memcpy(branches_out, o_br, br_out);
         return RBC_OK;
     });
 }
@@ -1215,18 +1254,30 @@ int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t s
     RBC_HIP(s.h_out.ensure((size_t)count * (vpitch + 32 + 4)));
     uint8_t *i_sh = s.h_in.as<uint8_t>(), *i_pr = i_sh + sh_bytes, *i_rt = i_pr + (size_t)count * n;
     uint32_t *ln = reinterpret_cast<uint32_t *>(i_rt + (size_t)count * 32);
-    parallel_for(count, (size_t)n * dpitch, [&](int i) {
-        ln[i] = (uint32_t)shard_lens[i];
-        for (int j = 0; j < n; ++j) {
-            uint8_t *dst = i_sh + ((size_t)i * n + j) * dpitch;
-            const uint8_t *src = shards + ((size_t)i * n + j) * shard_pitch;
-            memcpy(dst, src, shard_lens[i]);
-            memset(dst + shard_lens[i], 0, dpitch - shard_lens[i]);
-        }
-    });
+    // direct H2D of a pinned, uniform-length batch (bytes past S must arrive
+    // as zero: the rows are zeroed on the device first)
+    bool uniform = true;
+    for (int i = 0; i < count && uniform; ++i) uniform = shard_lens[i] == Smax;
+    const bool in_direct = uniform && host_pinned(shards, ((size_t)count * n - 1) * shard_pitch + Smax);
+    if (in_direct) {
+        for (int i = 0; i < count; ++i) ln[i] = (uint32_t)shard_lens[i];
+        if (dpitch > Smax) RBC_HIP(hipMemsetAsync(s.d_shards.p, 0, sh_bytes, st));
+        RBC_HIP(hipMemcpy2DAsync(s.d_shards.p, dpitch, shards, shard_pitch, Smax, (size_t)count * n,
+                                 hipMemcpyHostToDevice, st));
+    } else {
+        parallel_for(count, (size_t)n * dpitch, [&](int i) {
+            ln[i] = (uint32_t)shard_lens[i];
+            for (int j = 0; j < n; ++j) {
+                uint8_t *dst = i_sh + ((size_t)i * n + j) * dpitch;
+                const uint8_t *src = shards + ((size_t)i * n + j) * shard_pitch;
+                memcpy(dst, src, shard_lens[i]);
+                memset(dst + shard_lens[i], 0, dpitch - shard_lens[i]);
+            }
+        });
+        RBC_HIP(hipMemcpyAsync(s.d_shards.p, i_sh, sh_bytes, hipMemcpyHostToDevice, st));
+    }
     memcpy(i_pr, present, (size_t)count * n);
     memcpy(i_rt, roots, (size_t)count * 32);
-    RBC_HIP(hipMemcpyAsync(s.d_shards.p, i_sh, sh_bytes, hipMemcpyHostToDevice, st));
     RBC_HIP(hipMemcpyAsync(s.d_valid.p, i_pr, (size_t)count * n, hipMemcpyHostToDevice, st));
     RBC_HIP(hipMemcpyAsync(s.d_roots.p, i_rt, (size_t)count * 32, hipMemcpyHostToDevice, st));
     RBC_HIP(hipMemcpyAsync(s.d_slens.p, ln, (size_t)count * 4, hipMemcpyHostToDevice, st));
@@ -1239,14 +1290,20 @@ int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t s
     if (rc) return rc;
     uint8_t *o_val = s.h_out.as<uint8_t>(), *o_dig = o_val + (size_t)count * vpitch;
     int32_t *o_st = reinterpret_cast<int32_t *>(o_dig + (size_t)count * 32);
-    RBC_HIP(hipMemcpyAsync(o_val, s.d_values.p, (size_t)count * vpitch, hipMemcpyDeviceToHost, st));
+    const bool out_direct = host_pinned(values_out, (size_t)(count - 1) * value_pitch + (size_t)k * Smax);
+    if (out_direct)
+        RBC_HIP(hipMemcpy2DAsync(values_out, value_pitch, s.d_values.p, vpitch, (size_t)k * Smax, (size_t)count,
+                                 hipMemcpyDeviceToHost, st));
+    else
+        RBC_HIP(hipMemcpyAsync(o_val, s.d_values.p, (size_t)count * vpitch, hipMemcpyDeviceToHost, st));
     RBC_HIP(hipMemcpyAsync(o_dig, s.d_digests.p, (size_t)count * 32, hipMemcpyDeviceToHost, st));
     RBC_HIP(hipMemcpyAsync(o_st, s.d_status.p, (size_t)count * 4, hipMemcpyDeviceToHost, st));
     return submit(c, s, ticket, [=]() {
         memcpy(status_out, o_st, (size_t)count * 4);
-        parallel_for(count, (size_t)k * Smax, [&](int i) {
-            memcpy(values_out + (size_t)i * value_pitch, o_val + (size_t)i * vpitch, (size_t)k * Smax);
-        });
+        if (!out_direct)
+            parallel_for(count, (size_t)k * Smax, [&](int i) {
+                memcpy(values_out + (size_t)i * value_pitch, o_val + (size_t)i * vpitch, (size_t)k * Smax);
+            });
         if (digests_out) memcpy(digests_out, o_dig, (size_t)count * 32);
         return RBC_OK;
     });

@@ -102,6 +102,20 @@ class Stream:
             pass
 
 
+def pinned_empty(shape, dtype=np.uint8) -> np.ndarray:
+    """numpy array over C-owned pinned host memory (rbc_host_alloc).  The batch
+    entry points copy to and from such buffers directly (no staging memcpy):
+    what a Go batcher gets by keeping its rings in rbc_host_alloc memory."""
+    import ctypes
+    import weakref
+    nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+    p = c_void_p()
+    check(lib.rbc_host_alloc(max(nbytes, 1), byref(p)), "rbc_host_alloc")
+    buf = (ctypes.c_uint8 * max(nbytes, 1)).from_address(p.value)
+    weakref.finalize(buf, lib.rbc_host_free, p)
+    return np.frombuffer(buf, dtype=dtype, count=int(np.prod(shape))).reshape(shape)
+
+
 class Event:
     def __init__(self):
         p = c_void_p()
@@ -253,16 +267,24 @@ class Context:
     def shard_commit_batch(self, values: Sequence[bytes]) -> dict:
         return self.shard_commit_submit(values).wait()
 
-    def shard_commit_submit(self, values: Sequence[bytes]) -> "HostTicket":
+    def shard_commit_submit(self, values: Sequence[bytes], out: Optional[dict] = None) -> "HostTicket":
         """Asynchronous rbc_shard_commit: returns at once; .wait() completes
-        it (the context pipelines consecutive submissions through its slots)."""
+        it (the context pipelines consecutive submissions through its slots).
+        `out` may hold preallocated (e.g. pinned_empty) "shards" [count][N][Smax],
+        "roots" [count][32] and "branches" [count][N][max(d,1)][32] arrays."""
         count = len(values)
-        arrs = [_bytes_array(v) for v in values]
+        arrs = [v if isinstance(v, np.ndarray) and v.dtype == np.uint8 and v.flags.c_contiguous
+                else _bytes_array(v) for v in values]
         Smax = max((len(a) + self.k - 1) // self.k for a in arrs)
         pitch = Smax
-        shards = np.zeros((count, self.n, pitch), dtype=np.uint8)
-        roots = np.zeros((count, 32), dtype=np.uint8)
-        br = np.zeros((count, self.n, max(self.depth, 1), 32), dtype=np.uint8)
+        bshape = (count, self.n, max(self.depth, 1), 32)
+        if out is not None:
+            shards, roots, br = out["shards"], out["roots"], out["branches"]
+            assert shards.shape == (count, self.n, pitch) and roots.shape == (count, 32) and br.shape == bshape
+        else:
+            shards = np.zeros((count, self.n, pitch), dtype=np.uint8)
+            roots = np.zeros((count, 32), dtype=np.uint8)
+            br = np.zeros(bshape, dtype=np.uint8)
         slens = np.zeros(count, dtype=np.uint32)
         vlens = (c_size_t * count)(*[len(a) for a in arrs])
         vptrs = (c_void_p * count)(*[a.ctypes.data if len(a) else None for a in arrs])
@@ -291,7 +313,8 @@ class Context:
         check(lib.rbc_wait(self._p, t.value))
         return ok.astype(bool)
 
-    def interpolate_batch(self, shards: np.ndarray, shard_lens, present: np.ndarray, roots: np.ndarray) -> dict:
+    def interpolate_batch(self, shards: np.ndarray, shard_lens, present: np.ndarray, roots: np.ndarray,
+                          values_out: Optional[np.ndarray] = None) -> dict:
         shards = np.ascontiguousarray(shards, dtype=np.uint8)
         count, n, pitch = shards.shape
         assert n == self.n
@@ -300,7 +323,11 @@ class Context:
         sl = (c_size_t * count)(*[int(x) for x in shard_lens])
         Smax = int(max(shard_lens))
         vp = self.k * Smax
-        values = np.zeros((count, max(vp, 1)), dtype=np.uint8)
+        if values_out is not None:
+            values = values_out
+            assert values.shape == (count, max(vp, 1)) and values.dtype == np.uint8
+        else:
+            values = np.zeros((count, max(vp, 1)), dtype=np.uint8)
         digests = np.zeros((count, 32), dtype=np.uint8)
         status = np.zeros(count, dtype=np.int32)
         t = c_uint64(0)

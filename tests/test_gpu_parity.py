@@ -657,3 +657,43 @@ def test_device_verify_shared_paths_large_grid(gpu, ref):
             want = ref.verify(n, sh[i, j, :S], j, brs[i, j], bytes(roots[i]))
             assert got[i, j] == int(want), (i, j)
         assert not got[i].all()
+
+
+@pytest.mark.parametrize("lens", [[5000] * 6, [1, 21, 22, 23, 1000, 4096 * 3 + 5]], ids=["uniform", "ragged"])
+def test_host_batch_pinned_direct_copies(gpu, ref, lens):
+    """Pinned (rbc_host_alloc) caller buffers take the direct H2D/D2H path of
+    rbc_shard_commit / rbc_interpolate_batch: results byte-identical to the
+    staged path and to the oracle, including the rows' bytes past S_i."""
+    n, f = 16, 5
+    ctx = gpu.Context(n, f)
+    rng = np.random.default_rng(31)
+    values = [rng.integers(0, 256, L, dtype=np.uint8) for L in lens]
+    staged = ctx.shard_commit_batch(values)
+    pv = []
+    for v in values:
+        p = gpu.pinned_empty(len(v))
+        p[:] = v
+        pv.append(p)
+    count, Smax, d = len(values), staged["shards"].shape[2], ctx.depth
+    out = {"shards": gpu.pinned_empty((count, n, Smax)), "roots": gpu.pinned_empty((count, 32)),
+           "branches": gpu.pinned_empty((count, n, d, 32))}
+    out["shards"][:] = 0xAB  # every byte of a row up to Smax must be written (zeros past S_i)
+    direct = ctx.shard_commit_submit(pv, out=out).wait()
+    for key in ("shards", "roots", "branches", "shard_lens"):
+        assert np.array_equal(np.asarray(direct[key]), np.asarray(staged[key])), key
+    for i, v in enumerate(values):
+        shards, root, br, _ = ref.encode_commit(n, f, v)
+        assert bytes(direct["roots"][i]) == root
+    present = np.zeros((count, n), np.uint8)
+    for i in range(count):
+        present[i, rng.permutation(n)[: n - f]] = 1
+    rx = gpu.pinned_empty((count, n, Smax))
+    rx[:] = direct["shards"] * present[:, :, None]
+    vout = gpu.pinned_empty((count, ctx.k * Smax))
+    vout[:] = 0xCD
+    res = ctx.interpolate_batch(rx, direct["shard_lens"], present, direct["roots"], values_out=vout)
+    ref_res = ctx.interpolate_batch(np.array(rx), direct["shard_lens"], present, direct["roots"])
+    assert (res["status"] == 0).all()
+    assert np.array_equal(res["values"], ref_res["values"]) and np.array_equal(res["digests"], ref_res["digests"])
+    for i, v in enumerate(values):
+        assert res["values"][i, : len(v)].tobytes() == v.tobytes()

@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--batches", type=int, default=8)
     ap.add_argument("--inflight", type=int, default=2)
+    ap.add_argument("--pinned", action="store_true",
+                    help="values, shard/root/branch outputs and interpolate buffers in rbc_host_alloc memory "
+                         "(the C ABI then copies to and from them directly, no staging memcpy)")
     args = ap.parse_args()
     import cleisthenes_amd as ca
 
@@ -39,15 +42,25 @@ def main():
     S = (B + k - 1) // k
     rng = np.random.default_rng(1)
     pool = [[rng.integers(0, 256, B, dtype=np.uint8) for _ in range(args.batch)] for _ in range(2)]
+    outsets = [None] * (args.inflight + 1)
+    if args.pinned:
+        for p_ in pool:
+            for i, v in enumerate(p_):
+                pv = ca.pinned_empty(B)
+                pv[:] = v
+                p_[i] = pv
+        outsets = [{"shards": ca.pinned_empty((args.batch, n, S)), "roots": ca.pinned_empty((args.batch, 32)),
+                    "branches": ca.pinned_empty((args.batch, n, max(ctx.depth, 1), 32))}
+                   for _ in range(args.inflight + 1)]
 
     # shard + commit (proposer side)
-    warm = [ctx.shard_commit_submit(pool[i % 2]) for i in range(args.inflight)]  # warm every slot's buffers
-    for w in warm:
+    warm = [ctx.shard_commit_submit(pool[i % 2], out=outsets[i]) for i in range(args.inflight)]
+    for w in warm:  # warm every slot's buffers
         w.wait()
     t0 = time.perf_counter()
     live, outs = [], []
     for b in range(args.batches):
-        live.append(ctx.shard_commit_submit(pool[b % 2]))
+        live.append(ctx.shard_commit_submit(pool[b % 2], out=outsets[b % len(outsets)]))
         if len(live) >= args.inflight:
             outs.append(live.pop(0).wait())
     while live:
@@ -60,19 +73,25 @@ def main():
     for i in range(args.batch):
         present[i, rng.permutation(n)[: n - f]] = 1
     rx = sh * present[:, :, None]
+    vout = None
+    if args.pinned:
+        prx = ca.pinned_empty(rx.shape)
+        prx[:] = rx
+        rx = prx
+        vout = ca.pinned_empty((args.batch, ctx.k * S))
     lens = outs[-1]["shard_lens"]
-    roots = outs[-1]["roots"]
-    ctx.interpolate_batch(rx, lens, present, roots)  # warm-up
+    roots = outs[-1]["roots"].copy()
+    ctx.interpolate_batch(rx, lens, present, roots, values_out=vout)  # warm-up
     t0 = time.perf_counter()
     for _ in range(args.batches):
-        res = ctx.interpolate_batch(rx, lens, present, roots)
+        res = ctx.interpolate_batch(rx, lens, present, roots, values_out=vout)
     t_dec = time.perf_counter() - t0
     assert (res["status"] == 0).all()
     shard_bytes = args.batch * n * S * args.batches
     print(json.dumps({
         "metric": "host-path RBC shard GB/s (PCIe-inclusive, host buffers in and out)",
         "config": {"workload": args.config, "n": n, "f": f, "value_bytes": B, "batch": args.batch,
-                   "batches": args.batches, "inflight": args.inflight},
+                   "batches": args.batches, "inflight": args.inflight, "pinned": args.pinned},
         "shard_commit_GBps": round(shard_bytes / t_enc / 1e9, 2),
         "interpolate_GBps": round(shard_bytes / t_dec / 1e9, 2),
         "shard_commit_ms_per_batch": round(t_enc * 1e3 / args.batches, 3),
