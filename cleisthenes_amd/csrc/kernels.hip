@@ -776,14 +776,11 @@ __global__ __launch_bounds__(256) void decode_prepare_kernel(PrepArgs a) {
 // ============================================================================
 // decode_prepare_fft: the FFT codec's interpolate plan.  With U = the first k
 // valid positions (klauspost's Reconstruct rule) = every present data row D_p
-// plus the first m valid parity rows P_u (m = #missing data rows D_m), only
-// the m x m block A = M[P_u][D_m] needs inverting:
-//   x_{D_m} = A^-1 (s_{P_u} + M[P_u][D_p] s_{D_p})            (char 2: - = +)
-// so D = [A^-1 M[P_u][D_p] | A^-1] over U in index order, an m x k matrix
-// (m^3 instead of klauspost's k^3 inversion; A is a square sub-matrix of the
-// parity part of a systematic MDS code, hence never singular).  Parity
-// positions are then re-encoded by rs_fft_kernel from the completed data
-// half; cls[pos] tells it what to do per position.
+// plus the first m valid parity rows P_u (m = #missing data rows D_m), the
+// missing data rows are x_{D_m} = D s_U with D the m x k Lagrange matrix of
+// U at D_m (below; equal to [A^-1 M[P_u][D_p] | A^-1], A = M[P_u][D_m]).
+// Parity positions are then re-encoded by rs_fft_kernel from the completed
+// data half; cls[pos] tells it what to do per position.
 // ============================================================================
 __global__ __launch_bounds__(256) void decode_prepare_fft_kernel(PrepArgs a, const uint8_t *exp_tab,
                                                                   const uint8_t *log_tab) {
@@ -794,9 +791,7 @@ __global__ __launch_bounds__(256) void decode_prepare_fft_kernel(PrepArgs a, con
     uint8_t *s_used = smem + 768;    // 256: U in index order
     uint8_t *s_miss = smem + 1024;   // 256: missing positions in index order
     int *s_misc = reinterpret_cast<int *>(smem + 1280);  // 8 ints
-    uint8_t *s_fac = smem + 1312;    // 256: elimination factors of one pivot step
     int *s_wcnt = reinterpret_cast<int *>(smem + 1568);  // 12 ints: per-wave counts
-    uint8_t *A = smem + 1616;        // m x 2m  [A | I] -> [I | A^-1]
     const int inst = blockIdx.x, tid = threadIdx.x;
     for (int t = tid; t < 512; t += 256) s_exp[t] = exp_tab[t];
     s_log[tid] = log_tab[tid];
@@ -859,88 +854,40 @@ __global__ __launch_bounds__(256) void decode_prepare_fft_kernel(PrepArgs a, con
         if (tid == 0) a.status[inst] = 0;
         return;
     }
-    // Log-domain products: every multiply below is one exp lookup (log 255
-    // marks a zero operand).  The operands reused across a pivot step (the
-    // scaled pivot row, the column factors) and across D (inverse, the used
-    // parity rows of M) are converted to logs once, into LDS.
-    auto glog = [&](uint32_t x) -> uint32_t { return x ? (uint32_t)s_log[x] : 255u; };
-    auto gexpl = [&](uint32_t la, uint32_t lb) -> uint32_t {
-        return (la == 255u || lb == 255u) ? 0u : (uint32_t)s_exp[la + lb];
-    };
-    const int m2 = 2 * m, kp = k - m;  // U = D_p (kp rows) then P_u (m rows)
-    uint8_t *s_plog = A + (size_t)m * m2;          // m2: log of the scaled pivot row
-    uint8_t *s_alog = s_plog + m2;                 // m x m: log of A^-1
-    uint8_t *s_mlog = s_alog + (size_t)m * m;      // m x kp: log M[P_u[i]][D_p[u]]
-    for (int e = tid; e < m * m2; e += 256) {
-        const int r = e / m2, c = e - r * m2;
-        A[e] = c < m ? a.M[(size_t)s_used[kp + r] * k + s_miss[c]] : (uint8_t)((c - m) == r);
+    // D[r][u] = L_u(x_r): the Lagrange basis of U evaluated at the missing
+    // data position x_r.  klauspost's code is an evaluation code (shard r =
+    // P(r), deg P < k, the labels 0..N-1 as field elements), so the map from
+    // the k values at U to the missing values is unique and this IS
+    // [A^-1 M[P_u][D_p] | A^-1] -- with no inversion, no pivoting and no
+    // barrier per pivot.  In logs (mod 255; x_a ^ x_b != 0 for distinct
+    // positions, so every operand is nonzero):
+    //   log w_u   = -sum_{v in U, v != u} log(x_u ^ x_v)     (barycentric weight)
+    //   log l(x_r) =  sum_{v in U}        log(x_r ^ x_v)     (x_r not in U)
+    //   D[r][u]   = exp(log w_u + log l(x_r) - log(x_r ^ x_u))
+    uint8_t *s_lw = smem + 1616;        // k: log w_u
+    uint8_t *s_ll = s_lw + 256;         // m: log l(x_r)
+    for (int u = tid; u < k; u += 256) {
+        const uint32_t xu = s_used[u];
+        uint32_t acc = 0;
+        for (int v = 0; v < k; ++v)
+            if (v != u) acc += s_log[xu ^ s_used[v]];
+        s_lw[u] = (uint8_t)((255u * 255u - acc) % 255u);
     }
-    for (int e = tid; e < m * kp; e += 256) {
-        const int i = e / kp, u = e - i * kp;
-        s_mlog[e] = (uint8_t)glog(a.M[(size_t)s_used[kp + i] * k + s_used[u]]);
-    }
-    __syncthreads();
-    for (int col = 0; col < m; ++col) {
-        if (tid == 0) {
-            int piv = col;
-            if (A[col * m2 + col] == 0) {
-                piv = -1;
-                for (int b = col + 1; b < m; ++b)
-                    if (A[b * m2 + col]) { piv = b; break; }
-            }
-            s_misc[4] = piv;
-            s_misc[5] = piv >= 0 ? A[piv * m2 + col] : 0;  // read before the row moves
-        }
-        __syncthreads();
-        const int piv = s_misc[4];
-        if (piv < 0) {  // impossible for an MDS code; report, don't hang
-            if (tid == 0) a.status[inst] = RBC_ERR_SINGULAR;
-            return;
-        }
-        // columns < col of the pivot row are zero: only [col, m2) moves
-        const uint32_t linv = 255u - s_log[s_misc[5]];  // log of the pivot's inverse
-        for (int c = col + tid; c < m2; c += 256) {
-            const uint32_t x = A[piv * m2 + c];
-            const uint32_t y = gexpl(linv % 255u, glog(x));
-            if (piv != col) A[piv * m2 + c] = A[col * m2 + c];
-            s_plog[c] = (uint8_t)glog(y);
-        }
-        for (int r = tid; r < m; r += 256) {
-            const int src = (r == piv) ? col : r;  // the row that lands at r after the swap
-            s_fac[r] = (r == col) ? (uint8_t)255 : (uint8_t)glog(A[src * m2 + col]);
-        }
-        __syncthreads();
-        const int w = m2 - col;
-        for (int e = tid; e < m * w; e += 256) {
-            const int r = e / w, c = col + (e - r * w);
-            if (r == col) A[r * m2 + c] = (uint8_t)gexpl(s_plog[c], 0u);
-            else A[r * m2 + c] ^= (uint8_t)gexpl(s_fac[r], s_plog[c]);
-        }
-        __syncthreads();
-    }
-    for (int e = tid; e < m * m; e += 256) {
-        const int r = e / m, i = e - r * m;
-        s_alog[e] = (uint8_t)glog(A[r * m2 + m + i]);
+    for (int r = tid; r < m; r += 256) {
+        const uint32_t xr = s_miss[r];
+        uint32_t acc = 0;
+        for (int v = 0; v < k; ++v) acc += s_log[xr ^ s_used[v]];
+        s_ll[r] = (uint8_t)(acc % 255u);
     }
     __syncthreads();
-    // D[r][u]: u < kp -> sum_i Ainv[r][i] * M[P_u[i]][D_p[u]];  u >= kp -> Ainv[r][u-kp]
     uint8_t *D = a.dmat + (size_t)inst * a.dmat_stride;
-    for (int e = tid; e < m * k; e += 256) {
-        const int r = e / k, u = e - r * k;
-        uint32_t acc;
-        if (u >= kp) {
-            acc = A[r * m2 + m + (u - kp)];
-        } else {
-            acc = 0;
-            const uint8_t *al = s_alog + r * m;
-            const uint8_t *ml = s_mlog + u;
-            int i = 0;
-            for (; i + 4 <= m; i += 4)
-                acc ^= gexpl(al[i], ml[i * kp]) ^ gexpl(al[i + 1], ml[(i + 1) * kp]) ^
-                       gexpl(al[i + 2], ml[(i + 2) * kp]) ^ gexpl(al[i + 3], ml[(i + 3) * kp]);
-            for (; i < m; ++i) acc ^= gexpl(al[i], ml[i * kp]);
+    const int lane = tid & 63, wv = tid >> 6;
+    for (int r = wv; r < m; r += 4) {
+        const uint32_t xr = s_miss[r], lr = s_ll[r] + 255u;
+        for (int u = lane; u < k; u += 64) {
+            const uint32_t e = (s_lw[u] + lr - s_log[xr ^ s_used[u]]) % 255u;
+            D[(size_t)r * k + u] = s_exp[e];
         }
-        D[e] = (uint8_t)acc;
     }
     if (tid == 0) a.status[inst] = 0;
 }
@@ -1149,10 +1096,7 @@ hipError_t rbc_launch_digest(const uint8_t *leaves, uint64_t leaves_inst_pitch, 
 hipError_t rbc_launch_decode_prepare(const PrepArgs &a, hipStream_t st) {
     if (a.count <= 0) return hipSuccess;
     if (a.fft) {
-        const int mmax = std::min(a.k, a.n - a.k);
-        // [A | I], pivot-row logs, log A^-1, log M[P_u][D_p] (m * kp <= k^2 / 4)
-        const size_t lds = 1616 + (size_t)mmax * 2 * mmax + 2 * (size_t)mmax + (size_t)mmax * mmax +
-                           (size_t)a.k * a.k / 4 + 16;
+        const size_t lds = 1616 + 512;  // tables, U / missing lists, counts, log w_u, log l(x_r)
         hipLaunchKernelGGL(decode_prepare_fft_kernel, dim3(a.count), dim3(256), lds, st, a, a.gf_exp, a.gf_log);
         return hipGetLastError();
     }

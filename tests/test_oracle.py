@@ -276,3 +276,34 @@ def test_reconstruct_roundtrip_property(n, fr, B, seed):
     part = [sh[j] if j in keep else None for j in range(n)]
     out = orc.rbc_interpolate(e, com["root"], part)
     assert out["value"][:B] == value.tobytes()
+
+
+@pytest.mark.parametrize("n,k", [(4, 2), (7, 3), (16, 6), (128, 44), (256, 86)])
+def test_lagrange_decode_matrix_equals_klauspost_inverse(n, k):
+    """decode_prepare_fft_kernel forms the missing-data rows' decode matrix in
+    closed form, D[r][u] = L_u(x_r) (Lagrange basis of the used positions U at
+    the missing data position x_r, positions as field elements).  klauspost's
+    Reconstruct gets the same rows as M[missing] * inv(M[U]); pin the identity
+    on random erasure patterns."""
+    import rbc_oracle as o
+    rng = np.random.default_rng(n * 1000 + k)
+    M = o.encode_matrix(k, n)
+    done = 0
+    while done < 3:
+        pres = np.zeros(n, bool)
+        pres[rng.permutation(n)[: k + int(rng.integers(0, n - k + 1))]] = True
+        U = [p for p in range(n) if pres[p]][:k]
+        miss = [p for p in range(k) if not pres[p]]
+        if len(U) < k or not miss:
+            continue
+        want = o.mat_mul(M[miss], o.mat_invert(M[U]))
+        got = np.zeros_like(want)
+        for r, xr in enumerate(miss):
+            for ui, xu in enumerate(U):
+                num = den = 1
+                for xv in U:
+                    if xv != xu:
+                        num, den = o.gal_mul(num, xr ^ xv), o.gal_mul(den, xu ^ xv)
+                got[r, ui] = o.gal_div(num, den)
+        assert np.array_equal(got, want)
+        done += 1
