@@ -649,14 +649,13 @@ __global__ __launch_bounds__(64) void digest_kernel(const uint8_t *leaves, uint6
 // ============================================================================
 __global__ __launch_bounds__(256) void decode_prepare_kernel(PrepArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int n = a.n, k = a.k, k2 = 2 * a.k;
+    const int n = a.n, k = a.k;
     uint8_t *s_exp = smem;             // 512
     uint8_t *s_log = smem + 512;       // 256
     uint8_t *s_used = smem + 768;      // 256
     uint8_t *s_regen = smem + 1024;    // 256
-    uint8_t *s_fac = smem + 1280;      // 256
     int *s_misc = reinterpret_cast<int *>(smem + 1536);  // 4 ints
-    uint8_t *A = smem + 1552;          // k x 2k
+    uint8_t *A = smem + 1552;          // 512: log w_u, log l(x_r)
     const int inst = blockIdx.x, tid = threadIdx.x;
 
     if (tid == 0) {
@@ -689,9 +688,6 @@ __global__ __launch_bounds__(256) void decode_prepare_kernel(PrepArgs a) {
         s_misc[3] = nm;
     }
     __syncthreads();
-    auto gmul = [&](uint32_t x, uint32_t y) -> uint32_t {
-        return (x && y) ? (uint32_t)s_exp[s_log[x] + s_log[y]] : 0u;
-    };
     const int nu = s_misc[0], nr = s_misc[1];
     if (nu < k) {
         if (tid == 0) a.status[inst] = RBC_ERR_TOO_FEW_SHARDS;
@@ -702,86 +698,34 @@ __global__ __launch_bounds__(256) void decode_prepare_kernel(PrepArgs a) {
         for (int t = tid; t < nm; t += 256) a.list[base + t] = ((uint32_t)inst << 8) | s_regen[t];
         for (int t = tid; t < n; t += 256) a.flags[(size_t)inst * n + t] = 0;
     }
-    __syncthreads();  // s_misc[3] (pivot slot) is reused below
     for (int t = tid; t < k; t += 256) a.used[(size_t)inst * a.used_stride + t] = s_used[t];
     for (int t = tid; t < nr; t += 256) a.regen[(size_t)inst * a.regen_stride + t] = s_regen[t];
-    for (int e = tid; e < k * k2; e += 256) {
-        const int r = e / k2, c = e - r * k2;
-        A[e] = c < k ? a.M[(size_t)s_used[r] * k + c] : (uint8_t)((c - k) == r);
+    // D[r][u] = L_u(x_r): the Lagrange basis of U at every regenerated
+    // position (data or parity).  klauspost's matrix is an evaluation code, so
+    // this equals M[regen] * inv(M[U]) exactly -- no k x k
+    // inversion.  Logs mod 255; x_a ^ x_b != 0 for distinct positions.
+    uint8_t *s_lw = A;          // k: log w_u
+    uint8_t *s_ll = A + 256;    // nr: log l(x_r)
+    for (int u = tid; u < k; u += 256) {
+        const uint32_t xu = s_used[u];
+        uint32_t acc = 0;
+        for (int v = 0; v < k; ++v)
+            if (v != u) acc += s_log[xu ^ s_used[v]];
+        s_lw[u] = (uint8_t)((255u * 255u - acc) % 255u);
+    }
+    for (int r = tid; r < nr; r += 256) {
+        const uint32_t xr = s_regen[r];
+        uint32_t acc = 0;
+        for (int v = 0; v < k; ++v) acc += s_log[xr ^ s_used[v]];
+        s_ll[r] = (uint8_t)(acc % 255u);
     }
     __syncthreads();
-    for (int col = 0; col < k; ++col) {
-        if (tid == 0) {
-            int piv = col;
-            if (A[col * k2 + col] == 0) {
-                piv = -1;
-                for (int b = col + 1; b < k; ++b)
-                    if (A[b * k2 + col]) { piv = b; break; }
-            }
-            s_misc[3] = piv;
-        }
-        __syncthreads();
-        const int piv = s_misc[3];
-        if (piv < 0) {  // cannot happen for an MDS code; report, don't hang
-            if (tid == 0) a.status[inst] = RBC_ERR_SINGULAR;
-            return;
-        }
-        if (piv != col) {
-            for (int c = tid; c < k2; c += 256) {
-                const uint8_t x = A[col * k2 + c];
-                A[col * k2 + c] = A[piv * k2 + c];
-                A[piv * k2 + c] = x;
-            }
-            __syncthreads();
-        }
-        const uint32_t pv = A[col * k2 + col];
-        const uint32_t inv = s_exp[255 - s_log[pv]];
-        __syncthreads();
-        for (int c = tid; c < k2; c += 256) A[col * k2 + c] = (uint8_t)gmul(inv, A[col * k2 + c]);
-        for (int r = tid; r < k; r += 256) s_fac[r] = (r == col) ? 0 : A[r * k2 + col];
-        __syncthreads();
-        for (int e = tid; e < k * k2; e += 256) {
-            const int r = e / k2, c = e - r * k2;
-            const uint32_t f = s_fac[r];
-            if (f) A[e] ^= (uint8_t)gmul(f, A[col * k2 + c]);
-        }
-        __syncthreads();
-    }
-    // D[r][c] = XOR_i M[regen_r][i] * inv[i][c], in the log domain from LDS:
-    // logInvT[c][i] = log inv[i][c], logM[r][i] = log M[regen_r][i] (0xff = zero)
     uint8_t *D = a.dmat + (size_t)inst * a.dmat_stride;
-    if (a.stage_lds) {
-        uint8_t *logInvT = A + (size_t)k * k2;
-        uint8_t *logM = logInvT + (size_t)k * k;
-        for (int e = tid; e < k * k; e += 256) {
-            const int c = e / k, i = e - c * k;
-            const uint32_t x = A[i * k2 + k + c];
-            logInvT[e] = x ? s_log[x] : 0xffu;
-        }
-        for (int e = tid; e < nr * k; e += 256) {
-            const int r = e / k, i = e - r * k;
-            const uint32_t x = a.M[(size_t)s_regen[r] * k + i];
-            logM[e] = x ? s_log[x] : 0xffu;
-        }
-        __syncthreads();
-        for (int e = tid; e < nr * k; e += 256) {
-            const int r = e / k, c = e - r * k;
-            const uint8_t *lm = logM + (size_t)r * k, *li = logInvT + (size_t)c * k;
-            uint32_t acc = 0;
-            for (int i = 0; i < k; ++i) {
-                const uint32_t x = lm[i], y = li[i];
-                acc ^= (x != 0xffu && y != 0xffu) ? (uint32_t)s_exp[x + y] : 0u;
-            }
-            D[e] = (uint8_t)acc;
-        }
-    } else {
-        for (int e = tid; e < nr * k; e += 256) {
-            const int r = e / k, c = e - r * k;
-            const uint8_t *mrow = a.M + (size_t)s_regen[r] * k;
-            uint32_t acc = 0;
-            for (int i = 0; i < k; ++i) acc ^= gmul(mrow[i], A[i * k2 + k + c]);
-            D[e] = (uint8_t)acc;
-        }
+    const int lane = tid & 63, wv = tid >> 6;
+    for (int r = wv; r < nr; r += 4) {
+        const uint32_t xr = s_regen[r], lr = s_ll[r] + 255u;
+        for (int u = lane; u < k; u += 64)
+            D[(size_t)r * k + u] = s_exp[(s_lw[u] + lr - s_log[xr ^ s_used[u]]) % 255u];
     }
     if (tid == 0) a.status[inst] = 0;
 }
@@ -1116,10 +1060,7 @@ hipError_t rbc_launch_decode_prepare(const PrepArgs &a, hipStream_t st) {
         return hipGetLastError();
     }
     PrepArgs b = a;
-    const size_t base = 1552 + (size_t)a.k * 2 * a.k;
-    const size_t staged = base + (size_t)a.k * a.k + (size_t)(a.n - a.k) * a.k;
-    b.stage_lds = staged <= 96 * 1024;
-    const size_t lds = b.stage_lds ? staged : base;
+    const size_t lds = 1552 + 512;
     hipLaunchKernelGGL(decode_prepare_kernel, dim3(a.count), dim3(256), lds, st, b);
     return hipGetLastError();
 }
