@@ -372,29 +372,49 @@ __global__ __launch_bounds__(64) void merkle_kernel(MerkleArgs a) {
             const int inst = inst0 + g;
             if (inst >= a.count) continue;
             const int lc = 2 * i, rc = lc + 1;
-            uint32_t o[8];
+            // one compression body for every node form (fewer live registers):
+            // H(L || R) = [L | R] + a constant pad block; H(L) (right child an
+            // empty padding leaf) = [L | 0x80 .. | 256 bits]; H("") constant
+            uint32_t w[16];
+            bool two = true, none = false;
             if (lc >= W) {  // leaf level: children are leaves lc-W, rc-W (empty past n)
                 const int jl = lc - W, jr = rc - W;
                 const uint8_t *lv = a.leaves + (size_t)inst * a.leaves_inst_pitch;
-                if (jl >= n) {
-                    sha256_empty(o);
-                } else {
-                    uint32_t l[8];
-                    load_digest(lv + 32u * jl, l);
-                    if (jr >= n) {
-                        sha256_node32(l, o);
-                    } else {
-                        uint32_t r[8];
-                        load_digest(lv + 32u * jr, r);
-                        sha256_node64(l, r, o);
-                    }
+                none = jl >= n;
+                uint32_t l[8], r[8];
+                load_digest(lv + 32u * (none ? 0 : jl), l);
+                if (jr < n) load_digest(lv + 32u * jr, r);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    w[q] = l[q];
+                    w[8 + q] = jr < n ? r[q] : 0u;
+                }
+                if (jr >= n) {
+                    w[8] = 0x80000000u;
+                    w[15] = 256u;
+                    two = false;
                 }
             } else {
-                uint32_t l[8], r[8];
                 const uint32_t *nl = nodes + ((size_t)g * W + lc) * 8, *nr = nodes + ((size_t)g * W + rc) * 8;
 #pragma unroll
-                for (int q = 0; q < 8; ++q) { l[q] = nl[q]; r[q] = nr[q]; }
-                sha256_node64(l, r, o);
+                for (int q = 0; q < 8; ++q) { w[q] = nl[q]; w[8 + q] = nr[q]; }
+            }
+            uint32_t o[8];
+            if (none) {
+                sha256_empty(o);
+            } else {
+                Sha256State st;
+                sha256_init(st);
+                sha256_compress(st, w);
+                if (two) {
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) w[q] = 0;
+                    w[0] = 0x80000000u;
+                    w[15] = 512u;
+                    sha256_compress(st, w);
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q) o[q] = st.h[q];
             }
             uint32_t *dst = nodes + ((size_t)g * W + i) * 8;
 #pragma unroll
