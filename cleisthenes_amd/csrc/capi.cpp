@@ -460,6 +460,18 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
         // short rows (C4: 763 B) would leave most of a 4 KiB tile idle
         g.tpb = ((g.rc == 8 || g.rc == 4) && shard_pitch <= 2048) ? 64 : 256;
         g.tiles = (int)((shard_pitch + 16 * g.tpb - 1) / (16 * g.tpb));
+        if (g.tpb == 64) {
+            // 12 bytes per lane when that keeps more lanes busy (C4: S = 763 ->
+            // 64 of 64 lanes instead of 48); rows shorter than a 16-B tile's
+            // share keep the 16-byte form
+            const uint32_t S = shard_lens ? (uint32_t)shard_pitch : uniform_shard_len;
+            const double u16 = (double)S / (1024.0 * ((S + 1023) / 1024));
+            const double u12 = (double)S / (768.0 * ((S + 767) / 768));
+            if (u12 > u16 + 0.05) {
+                g.wpt = 3;
+                g.tiles = (int)((shard_pitch + 767) / 768);
+            }
+        }
         g.mode = GF_MODE_DECODE;
         g.in = shards;
         g.in_inst_pitch = (uint64_t)c->n * shard_pitch;

@@ -12,7 +12,8 @@ struct GfArgs {
     int count;                 // instances
     int tiles;                 // column tiles per instance (ceil(out_row_pitch / (16 * tpb)))
     int rc;                    // rows per chunk (template)
-    int tpb;                   // threads per block (template): 256 (4 KiB tiles) or 64 (1 KiB, rc 8 only); 0 = 256
+    int tpb;                   // threads per block (template): 256 (4 KiB tiles) or 64 (1 KiB, rc 4 / 8); 0 = 256
+    int wpt;                   // tpb 64 only: 3 -> gf_short_kernel (12 B per lane, 768 B tiles); else 16 B
     int R, K;                  // output rows, input rows per instance
     int mode;                  // GF_MODE_*
     const uint8_t *in;         // encode: values [I][value_pitch]; decode: shards [I][N][pitch]

@@ -216,6 +216,95 @@ __global__ __launch_bounds__(TPB, (RC <= 21 ? 3 : 2)) void gf_rows_kernel(GfArgs
 }
 
 // ============================================================================
+// gf_short: interpolate's missing data rows (FFT codec, decode mode, no
+// compare / copy) for SHORT rows: one wave per (instance, 768-byte column
+// tile, RC-row chunk), 12 bytes (3 packed words) per lane.  With 16 bytes per
+// lane a 763-byte C4 row keeps 48 of 64 lanes busy; 12 keeps 64.  Same LDS
+// tables, block -> (item, chunk) mapping and pipelined loads as gf_rows.
+// ============================================================================
+template <int RC>
+__global__ __launch_bounds__(64) void gf_short_kernel(GfArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int TPB = 64;
+    const int KP = (a.K + 1) & ~1;
+    uint4 *s_t01 = reinterpret_cast<uint4 *>(smem);
+    uint32_t *s_t2 = reinterpret_cast<uint32_t *>(smem + (size_t)16 * RC * KP);
+    uint8_t *s_in = reinterpret_cast<uint8_t *>(smem + (size_t)20 * RC * KP);
+    uint8_t *s_out = s_in + 256;
+    const int chunks = (a.R + RC - 1) / RC;
+    const int grp = blockIdx.x / (8 * chunks), rem = blockIdx.x - grp * 8 * chunks;
+    const int c = rem >> 3;
+    const int item = grp * 8 + (rem & 7);
+    if (item >= a.count * a.tiles) return;
+    const int inst = item / a.tiles;
+    const int tile = item - inst * a.tiles;
+    const int tid = threadIdx.x;
+    if (a.status && a.status[inst] != 0) return;
+    const int rlim = a.rcount ? min(a.rcount[inst], a.R) : a.R;
+    if (c * RC >= rlim) return;
+    const uint32_t S = inst_len(a.lens, a.uniform_len, inst);
+    const uint32_t my_off = (uint32_t)tile * (12u * TPB) + 12u * tid;
+    if ((uint32_t)tile * (12u * TPB) >= a.out_row_pitch) return;
+    const uint8_t *in_inst = a.in + (size_t)inst * a.in_inst_pitch;
+    uint8_t *out_inst = a.out + (size_t)inst * a.out_inst_pitch;
+    const rsrc_t rin = make_rsrc(in_inst, a.in_inst_bytes);
+    for (int t = tid; t < a.K; t += TPB) s_in[t] = a.in_idx[(size_t)inst * a.idx_stride + t];
+    for (int t = tid; t < a.R; t += TPB) s_out[t] = a.out_idx[(size_t)inst * a.idx_stride2 + t];
+    const int r0 = c * RC;
+    const int rows = min(RC, rlim - r0);
+    for (int e = tid; e < RC * KP; e += TPB) {
+        const int r = e / KP, j = e - r * KP;
+        uint32_t cf = 0;
+        if (r < rows && j < a.K) cf = a.coef[(size_t)inst * a.coef_inst_stride + (size_t)(r0 + r) * a.K + j];
+        uint4 t01;
+        uint32_t t2;
+        gf_tables(cf, t01, t2);
+        s_t01[j * RC + r] = t01;
+        s_t2[((j >> 1) * RC + r) * 2 + (j & 1)] = t2;
+    }
+    __syncthreads();
+    auto load_row = [&](int j) -> uint3 {
+        if (j >= a.K) return make_uint3(0, 0, 0);
+        auto v = __builtin_amdgcn_raw_buffer_load_b96(rin, (int)(s_in[j] * a.in_row_pitch + my_off), 0, 0);
+        return make_uint3(v[0], v[1], v[2]);
+    };
+    uint32_t acc[RC][3];
+#pragma unroll
+    for (int r = 0; r < RC; ++r) acc[r][0] = acc[r][1] = acc[r][2] = 0;
+    uint3 xa = load_row(0), xb = load_row(1);
+    uint3 pa = load_row(2), pb = load_row(3);
+    for (int j = 0; j < KP; j += 2) {
+        const uint3 na = load_row(j + 4), nb = load_row(j + 5);
+        const GfSel sa0 = gf_sel(xa.x), sa1 = gf_sel(xa.y), sa2 = gf_sel(xa.z);
+        const GfSel sb0 = gf_sel(xb.x), sb1 = gf_sel(xb.y), sb2 = gf_sel(xb.z);
+#pragma unroll
+        for (int r = 0; r < RC; ++r) {
+            const uint4 ta = s_t01[j * RC + r];
+            const uint4 tb = s_t01[(j + 1) * RC + r];
+            const uint2 t2 = *reinterpret_cast<const uint2 *>(&s_t2[((j >> 1) * RC + r) * 2]);
+            acc[r][0] = xor3(acc[r][0], gf_mul4(ta, t2.x, sa0), gf_mul4(tb, t2.y, sb0));
+            acc[r][1] = xor3(acc[r][1], gf_mul4(ta, t2.x, sa1), gf_mul4(tb, t2.y, sb1));
+            acc[r][2] = xor3(acc[r][2], gf_mul4(ta, t2.x, sa2), gf_mul4(tb, t2.y, sb2));
+        }
+        xa = pa;
+        xb = pb;
+        pa = na;
+        pb = nb;
+    }
+    // zero the bytes past S; never write past the row pitch (word granular)
+    const int nvalid = (int)S - (int)my_off;
+#pragma unroll
+    for (int r = 0; r < RC; ++r) {
+        if (r < rows) {
+            uint32_t *dst = reinterpret_cast<uint32_t *>(out_inst + (size_t)s_out[r0 + r] * a.out_row_pitch + my_off);
+#pragma unroll
+            for (int w = 0; w < 3; ++w)
+                if (my_off + 4u * w < a.out_row_pitch) dst[w] = acc[r][w] & keep_bytes(nvalid - 4 * w);
+        }
+    }
+}
+
+// ============================================================================
 // sha_rows: leaf_j = SHA-256(shard_j) for a list of rows, one lane per row;
 // VERIFY additionally walks the Merkle branch (validateMessage,
 // rbc/rbc.go:92-95) and writes valid = present && (root' == root).
@@ -978,6 +1067,18 @@ int rbc_gf_pick_rc(int R, int rcmax) {
 
 hipError_t rbc_launch_gf_rows(const GfArgs &a, hipStream_t st) {
     if (a.count <= 0 || (a.R <= 0 && !a.copy)) return hipSuccess;
+    if (a.tpb == 64 && a.wpt == 3) {  // short rows, 12 bytes per lane (decode, no compare / copy)
+        if (a.mode != GF_MODE_DECODE || a.nmiss || a.copy) return hipErrorInvalidValue;
+        const int KP = (a.K + 1) & ~1;
+        const size_t lds = (size_t)20 * a.rc * KP + 512;
+        const int chunks = (a.R + a.rc - 1) / a.rc;
+        const long items = (long)a.count * a.tiles;
+        dim3 grid((unsigned)(((items + 7) / 8) * 8 * chunks));
+        if (a.rc == 8) hipLaunchKernelGGL(gf_short_kernel<8>, grid, dim3(64), lds, st, a);
+        else if (a.rc == 4) hipLaunchKernelGGL(gf_short_kernel<4>, grid, dim3(64), lds, st, a);
+        else return hipErrorInvalidValue;
+        return hipGetLastError();
+    }
     if (a.tpb == 64) {  // short rows: 1 KiB column tiles (one wave per block)
         if (a.rc == 8) return launch_gf_rc<8, 64>(a, st);
         if (a.rc == 4) return launch_gf_rc<4, 64>(a, st);

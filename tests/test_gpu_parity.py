@@ -697,3 +697,27 @@ def test_host_batch_pinned_direct_copies(gpu, ref, lens):
     assert np.array_equal(res["values"], ref_res["values"]) and np.array_equal(res["digests"], ref_res["digests"])
     for i, v in enumerate(values):
         assert res["values"][i, : len(v)].tobytes() == v.tobytes()
+
+
+@pytest.mark.parametrize("S", [763, 100, 1400, 1500, 2000])
+def test_device_interpolate_short_rows(gpu, S):
+    """Missing-data GF rows for short shards (one-wave tiles: 12 bytes per
+    lane where that keeps more lanes busy -- C4's S = 763 -- including a last
+    tile that straddles the row pitch, S = 1400): interpolate returns the
+    value and rewrites every regenerated row exactly as committed, zero past S."""
+    n, f, I = 256, 85, 6
+    k = n - 2 * f
+    pl = Pipeline(gpu, n, f, k * S, I, seed=S, corrupt_frac=0.3)
+    pl.commit()
+    committed = pl.shards().copy()
+    pl.receive()
+    assert (pl.arr("status", np.int32) == 0).all()
+    out = pl.arr("out", shape=(I, pl.opitch))
+    assert np.array_equal(out[:, : pl.B], pl.values[:, : pl.B])
+    after = pl.shards()
+    for i in range(I):
+        ok = pl.present[i].astype(bool)
+        if pl.corrupt[i] >= 0:
+            ok[pl.corrupt[i]] = False  # verify rejected it, interpolate regenerated it
+        regen = ~ok
+        assert np.array_equal(after[i][regen], committed[i][regen]), i
