@@ -404,11 +404,16 @@ def cpu_baseline(n, f, B, count, threads):
             corrupt[i] = int(rng.choice(pres))
     threads = max(1, min(threads, os.cpu_count() or 1))
     secs, st = rbc_ref.pipeline(n, f, count, B, threads, values, present, corrupt)
+    # one core as well ("1 thread and all cores"), on a 1/16 sample
+    c1 = max(1, count // 16)
+    secs1, st1 = rbc_ref.pipeline(n, f, c1, B, 1, values, present[:c1], corrupt[:c1])
     feats = rbc_ref.lib().rbcref_cpu_features()
     return {"value": round(count * n * S / secs / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
             "sample": f"{count} instances x {B} B (N={n} f={f}), same per-instance pipeline as the GPU step, "
                       f"{secs:.2f} s wall on {threads} threads",
-            "simd": ("avx2 " if feats & 1 else "") + ("sha-ni" if feats & 2 else ""), "status_sum": st}
+            "single_core": {"value": round(c1 * n * S / secs1 / 1e9, 3), "unit": "GB/s", "cores": 1,
+                            "sample": f"{c1} instances, {secs1:.2f} s"},
+            "simd": ("avx2 " if feats & 1 else "") + ("sha-ni" if feats & 2 else ""), "status_sum": st + st1}
 
 
 if __name__ == "__main__":
