@@ -573,88 +573,107 @@ __global__ __launch_bounds__(64) void merkle_kernel(MerkleArgs a) {
 // value its own walk would compute: the result is bit-identical to the
 // per-leaf walk for every input, honest or not.  Per instance that is W-1
 // node hashes plus one per divergent (leaf, level) instead of N*d.
-// G = 256/W instances per 256-thread block (thread t: instance t/W, leaf
-// t%W); the tasks of all G instances are packed onto consecutive threads.
+// One wave per block: lane owns leaves s*64 + lane (s < W/64), or 64/W
+// instances share the wave when W < 64; the hash tasks of a level are packed
+// onto consecutive lanes.
 // Leaves come from sha_rows_kernel<false>; this kernel writes valid[].
 // ============================================================================
-template <int BS>
-__global__ __launch_bounds__(BS) void merkle_path_kernel(PathArgs a) {
-    constexpr int NW = BS / 64;
-    __shared__ uint32_t s_pair[BS][17];  // +1 word: conflict-free per-thread rows; an owner's
-                                          // task digest overwrites words 0..7 of its own row
-    __shared__ uint8_t s_empty[BS];
-    __shared__ uint16_t s_owner[BS];
-    __shared__ uint64_t s_wmask[NW];
-    __shared__ int s_wcnt[NW];
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+template <int L>
+__global__ __launch_bounds__(64) void merkle_path_kernel(PathArgs a) {
+    // one wave per block; lane owns leaf positions p = s*64 + lane (s < L)
+    __shared__ uint32_t s_pair[64 * L][17];  // +1 word: conflict-free rows; an owner's task
+                                              // digest overwrites words 0..7 of its own row
+    __shared__ uint8_t s_empty[64 * L];
+    __shared__ uint16_t s_owner[64 * L];
+    const int lane = threadIdx.x;
     const int W = a.width, lgW = a.lg_width;
-    const int g = t >> lgW, j = t & (W - 1);
-    const int inst = (int)blockIdx.x * a.inst_per_block + g;
-    const bool inst_ok = g < a.inst_per_block && inst < a.count && !(a.status && a.status[inst] != 0);
-    const bool part = inst_ok && j < a.n && (!a.present || a.present[(size_t)inst * a.n + j] != 0);
-    const uint64_t pm = __ballot(part);
-    if (lane == 0) s_wmask[wv] = pm;
-    uint32_t x[8];
-    if (part) load_digest(a.leaves + (size_t)inst * a.leaves_inst_pitch + 32u * j, x);
-    const uint8_t *br = a.branches + (size_t)(inst_ok ? inst : 0) * a.br_inst_pitch + (size_t)j * a.depth * 32u;
     const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    int jj[L], inst_s[L];
+    bool ok_s[L], part[L];
+    uint64_t pm[L];
+    uint32_t x[L][8];
+#pragma unroll
+    for (int s = 0; s < L; ++s) {
+        const int p = s * 64 + lane;
+        const int g = p >> lgW;
+        jj[s] = p & (W - 1);
+        inst_s[s] = (int)blockIdx.x * a.inst_per_block + g;
+        ok_s[s] = g < a.inst_per_block && inst_s[s] < a.count && !(a.status && a.status[inst_s[s]] != 0);
+        part[s] = ok_s[s] && jj[s] < a.n && (!a.present || a.present[(size_t)inst_s[s] * a.n + jj[s]] != 0);
+        pm[s] = __ballot(part[s]);
+        if (part[s]) load_digest(a.leaves + (size_t)inst_s[s] * a.leaves_inst_pitch + 32u * jj[s], x[s]);
+    }
+    auto pmask = [&](int w) -> uint64_t {
+        uint64_t m = pm[0];
+#pragma unroll
+        for (int s = 1; s < L; ++s) m = (w == s) ? pm[s] : m;
+        return m;
+    };
     for (int l = 0; l < a.depth; ++l) {
-        // 1. this leaf's ordered input (left || right) for level l
-        if (part) {
+        // 1. each leaf's ordered input (left || right) for level l
+#pragma unroll
+        for (int s = 0; s < L; ++s) {
+            if (!part[s]) continue;
+            const int p = s * 64 + lane, j = jj[s];
             const bool empty = (l == 0) && ((j ^ 1) >= a.n);
             uint32_t sib[8];
             if (empty) {
 #pragma unroll
                 for (int q = 0; q < 8; ++q) sib[q] = 0;
             } else {
-                load_digest(br + 32u * l, sib);
+                load_digest(a.branches + (size_t)inst_s[s] * a.br_inst_pitch + ((size_t)j * a.depth + l) * 32u, sib);
             }
             const bool right = (j >> l) & 1;
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
-                s_pair[t][q] = right ? sib[q] : x[q];
-                s_pair[t][8 + q] = right ? x[q] : sib[q];
+                s_pair[p][q] = right ? sib[q] : x[s][q];
+                s_pair[p][8 + q] = right ? x[s][q] : sib[q];
             }
-            s_empty[t] = empty ? 1 : 0;
+            s_empty[p] = empty ? 1 : 0;
         }
         __syncthreads();
-        // 2. rep = first participating thread of this leaf's level-(l+1) group
-        int rep = t;
-        bool owner = false;
-        if (part) {
-            const int gs = 2 << l;
-            const int t0 = t & ~(gs - 1), t1 = t0 + gs;
-            for (int w = t0 >> 6; w <= (t1 - 1) >> 6; ++w) {
-                uint64_t m = s_wmask[w];
-                const int lo = t0 - w * 64, hi = t1 - w * 64;
-                if (lo > 0) m &= ~0ull << lo;
-                if (hi < 64) m &= (1ull << hi) - 1ull;
-                if (m) { rep = w * 64 + __builtin_ctzll(m); break; }
-            }
-            bool same = true;
-            if (rep != t) {
-                same = s_empty[t] == s_empty[rep];
+        // 2. rep = first participating leaf of the level-(l+1) group; owners
+        //    are reps and leaves whose input differs from their rep's
+        int rep[L];
+        bool owner[L];
+        int total = 0, base[L];
+        uint64_t om[L];
 #pragma unroll
-                for (int q = 0; q < 16; ++q) same = same && (s_pair[t][q] == s_pair[rep][q]);
+        for (int s = 0; s < L; ++s) {
+            const int p = s * 64 + lane;
+            rep[s] = p;
+            owner[s] = false;
+            if (part[s]) {
+                const int gs = 2 << l;
+                const int t0 = p & ~(gs - 1), t1 = t0 + gs;
+                for (int w = t0 >> 6; w <= (t1 - 1) >> 6; ++w) {
+                    uint64_t m = pmask(w);
+                    const int lo = t0 - w * 64, hi = t1 - w * 64;
+                    if (lo > 0) m &= ~0ull << lo;
+                    if (hi < 64) m &= (1ull << hi) - 1ull;
+                    if (m) { rep[s] = w * 64 + __builtin_ctzll(m); break; }
+                }
+                bool same = true;
+                if (rep[s] != p) {
+                    same = s_empty[p] == s_empty[rep[s]];
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) same = same && (s_pair[p][q] == s_pair[rep[s]][q]);
+                }
+                owner[s] = (rep[s] == p) || !same;
             }
-            owner = (rep == t) || !same;
+            om[s] = __ballot(owner[s]);
+            base[s] = total;
+            total += __popcll(om[s]);
         }
-        // 3. number the hash tasks (owners) across the block
-        const uint64_t om = __ballot(owner);
-        if (lane == 0) s_wcnt[wv] = __popcll(om);
+        // 3. number the hash tasks (owners) on consecutive lanes
+#pragma unroll
+        for (int s = 0; s < L; ++s)
+            if (owner[s]) s_owner[base[s] + __popcll(om[s] & below)] = (uint16_t)(s * 64 + lane);
         __syncthreads();
-        int base = 0, total = 0;
-        for (int w = 0; w < NW; ++w) {
-            if (w < wv) base += s_wcnt[w];
-            total += s_wcnt[w];
-        }
-        if (owner) s_owner[base + __popcll(om & below)] = (uint16_t)t;
-        __syncthreads();
-        // 4. hash the tasks on consecutive threads
-        for (int i = t; i < total; i += BS) {
-            // one compression body for both node forms (fewer live registers):
-            // H(L || R) = two blocks, the second constant; H(L) (empty level-0
-            // sibling) = one block [L | 0x80 .. | 256 bits]
+        // 4. hash the tasks: one compression body for both node forms --
+        //    H(L || R) = two blocks, the second constant; H(L) (empty level-0
+        //    sibling) = one block [L | 0x80 .. | 256 bits]
+        for (int i = lane; i < total; i += 64) {
             const int o = s_owner[i];
             const bool empty = s_empty[o] != 0;
             Sha256State st;
@@ -683,23 +702,27 @@ __global__ __launch_bounds__(BS) void merkle_path_kernel(PathArgs a) {
         __syncthreads();
         // 5. every walk takes the digest of the task with its input (the
         //    rep's task unless it owns one)
-        if (part) {
-            const int o = owner ? t : rep;
 #pragma unroll
-            for (int q = 0; q < 8; ++q) x[q] = s_pair[o][q];
+        for (int s = 0; s < L; ++s) {
+            if (!part[s]) continue;
+            const int o = owner[s] ? s * 64 + lane : rep[s];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) x[s][q] = s_pair[o][q];
         }
         __syncthreads();
     }
-    if (inst_ok && j < a.n) {
+#pragma unroll
+    for (int s = 0; s < L; ++s) {
+        if (!(ok_s[s] && jj[s] < a.n)) continue;
         bool ok = false;
-        if (part) {
+        if (part[s]) {
             uint32_t root[8];
-            load_digest(a.roots + (size_t)inst * 32u, root);
+            load_digest(a.roots + (size_t)inst_s[s] * 32u, root);
             ok = true;
 #pragma unroll
-            for (int q = 0; q < 8; ++q) ok = ok && (x[q] == root[q]);
+            for (int q = 0; q < 8; ++q) ok = ok && (x[s][q] == root[q]);
         }
-        a.valid[(size_t)inst * a.n + j] = ok ? 1 : 0;
+        a.valid[(size_t)inst_s[s] * a.n + jj[s]] = ok ? 1 : 0;
     }
 }
 
@@ -1135,16 +1158,18 @@ hipError_t rbc_launch_merkle_path(const PathArgs &a, hipStream_t st) {
     if (a.count <= 0) return hipSuccess;
     if (a.width < 1 || a.width > 256 || (1 << a.lg_width) != a.width || a.depth != a.lg_width || a.n > a.width)
         return hipErrorInvalidValue;
-    // 256-thread blocks.  Measured (C4, MI355X): 1024-thread blocks that pack
-    // 4x the instances per task list are slower (verify 3.45 -> 3.94 ms): the
-    // 70 KB of LDS per block leaves 2 blocks per CU and every level barrier
-    // then idles 16 waves.
+    // One wave per block: an instance's leaves (L = W / 64 per lane), or
+    // 64 / W instances when W < 64.  Measured (C4, MI355X): 256-thread blocks
+    // (one leaf per thread) kept only 3 blocks per CU resident at 152 VGPRs,
+    // mostly idle at the level barriers (path 1.34 ms); 1024-thread blocks
+    // were slower still (70 KB of LDS per block).
     PathArgs b = a;
-    b.inst_per_block = 256 / a.width;
+    const int L = a.width > 64 ? a.width / 64 : 1;
+    b.inst_per_block = a.width >= 64 ? 1 : 64 / a.width;
     const dim3 grid((unsigned)((a.count + b.inst_per_block - 1) / b.inst_per_block));
-    // (152 VGPRs: 3 blocks per CU.  Forcing 4-5 waves per SIMD spills and
-    // measured slower: C4 verify 3.32 -> 3.50 / 4.50 ms.)
-    hipLaunchKernelGGL(merkle_path_kernel<256>, grid, dim3(256), 0, st, b);
+    if (L == 4) hipLaunchKernelGGL(merkle_path_kernel<4>, grid, dim3(64), 0, st, b);
+    else if (L == 2) hipLaunchKernelGGL(merkle_path_kernel<2>, grid, dim3(64), 0, st, b);
+    else hipLaunchKernelGGL(merkle_path_kernel<1>, grid, dim3(64), 0, st, b);
     return hipGetLastError();
 }
 
