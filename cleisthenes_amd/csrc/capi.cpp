@@ -357,9 +357,9 @@ int stage_verify(rbc_ctx *c, hipStream_t st, int count, const uint8_t *shards, u
     a.valid = valid;
     // Shared-path verification: leaves, then one hash per
     // distinct branch-walk input.  RBC_VERIFY_PATH=0 runs the per-leaf walk.
-    static const bool path_env = [] {
+    static const int path_env = [] {  // 0 never, 1 (default) where it pays, 2 always
         const char *e = getenv("RBC_VERIFY_PATH");
-        return !e || atoi(e) != 0;
+        return e ? atoi(e) : 1;
     }();
     // The per-leaf walk costs 2d compressions per row on top of the leaf's
     // ceil((S+9)/64); the shared-path form pays off where that walk is a real
@@ -367,7 +367,7 @@ int stage_verify(rbc_ctx *c, hipStream_t st, int count, const uint8_t *shards, u
     // 373, measured equal alone and slower beside a second stream).
     const uint32_t blocks_per_row = shard_lens ? 0u : (uniform_shard_len + 9 + 63) / 64;
     const bool path_pays = shard_lens || 16u * (uint32_t)c->depth >= blocks_per_row;
-    if (path_env && path_pays && c->depth >= 1 && c->width <= 256) {
+    if (path_env && (path_pays || path_env == 2) && c->depth >= 1 && c->width <= 256) {
         uint8_t *lv = leaves;
         if (!lv) {
             std::lock_guard<std::mutex> lk(c->mu);
