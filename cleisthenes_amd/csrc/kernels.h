@@ -122,7 +122,6 @@ struct PrepArgs {
     uint32_t cls_stride;
     const uint8_t *gf_exp;     // device exp[512] / log[256] tables (FFT prepare)
     const uint8_t *gf_log;
-    int stage_lds;             // set by the launcher: LDS holds log-domain M rows + inverse
 };
 
 struct JoinArgs {
