@@ -721,3 +721,43 @@ def test_device_interpolate_short_rows(gpu, S):
             ok[pl.corrupt[i]] = False  # verify rejected it, interpolate regenerated it
         regen = ~ok
         assert np.array_equal(after[i][regen], committed[i][regen]), i
+
+
+@pytest.mark.parametrize("n,f", [(16, 5), (256, 85)])
+def test_device_verify_ragged_lengths(gpu, ref, n, f):
+    """rbc_dev_verify with per-instance shard lengths (the shared-path kernel
+    runs whenever lengths are ragged): a ragged batch committed through the
+    host API, a few shards / branch slots corrupted, valid[] and the leaves
+    against the oracle walk."""
+    ctx = gpu.Context(n, f)
+    k, d = ctx.k, ctx.depth
+    rng = np.random.default_rng(n + 17)
+    lens = [1, k, 3 * k + 1, 50 * k, 7, 200 * k + 5]
+    values = [rng.integers(0, 256, L, dtype=np.uint8) for L in lens]
+    out = ctx.shard_commit_batch(values)
+    I, Smax = len(values), out["shards"].shape[2]
+    pitch = rup(Smax, 64)
+    sh = np.zeros((I, n, pitch), np.uint8)
+    sh[:, :, :Smax] = out["shards"]
+    brs = np.ascontiguousarray(out["branches"])
+    roots = out["roots"].copy()
+    for i in range(I):
+        sh[i, rng.integers(n), rng.integers(int(out["shard_lens"][i]))] ^= 0x40
+        brs[i, rng.integers(n), rng.integers(d), rng.integers(32)] ^= 2
+    mb = gpu.DeviceBuffer
+    b = dict(sh=mb(sh.nbytes), br=mb(brs.nbytes), rt=mb(roots.nbytes), ln=mb(4 * I), va=mb(I * n),
+             lv=mb(I * n * 32))
+    b["sh"].upload(sh)
+    b["br"].upload(brs)
+    b["rt"].upload(roots)
+    b["ln"].upload(out["shard_lens"].astype(np.uint32))
+    ctx.dev_verify(None, I, b["sh"], pitch, b["ln"], 0, b["br"], b["rt"], None, b["va"], b["lv"])
+    got = np.frombuffer(b["va"].download().tobytes(), np.uint8).reshape(I, n)
+    leaves = np.frombuffer(b["lv"].download().tobytes(), np.uint8).reshape(I, n, 32)
+    for i in range(I):
+        S = int(out["shard_lens"][i])
+        for j in range(n):
+            want = ref.verify(n, sh[i, j, :S], j, brs[i, j], bytes(roots[i]))
+            assert got[i, j] == int(want), (i, j)
+            assert leaves[i, j].tobytes() == ref.sha256(sh[i, j, :S].tobytes())
+        assert 1 <= (got[i] == 0).sum() <= 2
