@@ -535,27 +535,34 @@ __global__ __launch_bounds__(64) void merkle_kernel(MerkleArgs a) {
             if (a.roots) store_digest(a.roots + (size_t)inst * 32u, root);
         }
     }
-    if (!CHECK && a.branches) {
-        // branch[j][l] = node ((W + j) >> l) ^ 1; one 16-byte half per item.
+    if (!CHECK && a.branches && a.depth > 0) {  // W == 1: no branch bytes
+        // branch[j][l] = node ((W + j) >> l) ^ 1; one 16-byte half per item,
+        // item e of a tree = (jl = j*depth + l, half) at e = 2*jl + half, so a
+        // wave store covers 1 KiB of consecutive branch bytes.  jl advances by
+        // 32 per pass: (j, l) step by (32 / depth, 32 % depth) with a carry,
+        // no integer division inside the loop.
         // Level 0 siblings are leaves (zero slot when past n).
-        const int items = n * a.depth * 2;
-        for (int e = tid; e < G * items; e += 64) {
-            const int g = e / items, r = e - g * items;
+        const int depth = a.depth, items = n * depth * 2;
+        const int qd = 32 / depth, rd = 32 - qd * depth;
+        const int half = tid & 1, j_0 = (tid >> 1) / depth, l_0 = (tid >> 1) - j_0 * depth;
+        for (int g = 0; g < G; ++g) {
             const int inst = inst0 + g;
-            if (inst >= a.count) continue;
-            const int half = r & 1, jl = r >> 1;
-            const int j = jl / a.depth, l = jl - j * a.depth;
-            const int node = ((W + j) >> l) ^ 1;
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (l == 0) {
-                if (node - W < n)
-                    v = *reinterpret_cast<const uint4 *>(a.leaves + (size_t)inst * a.leaves_inst_pitch +
-                                                         32u * (node - W) + 16u * half);
-            } else {
-                const uint32_t *nd = nodes + ((size_t)g * W + node) * 8 + 4 * half;
-                v = make_uint4(bswap32(nd[0]), bswap32(nd[1]), bswap32(nd[2]), bswap32(nd[3]));
+            if (inst >= a.count) break;
+            int jl = tid >> 1, j = j_0, l = l_0;
+            for (int e = tid; e < items; e += 64, jl += 32, j += qd, l += rd) {
+                if (l >= depth) { l -= depth; ++j; }
+                const int node = ((W + j) >> l) ^ 1;
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (l == 0) {
+                    if (node - W < n)
+                        v = *reinterpret_cast<const uint4 *>(a.leaves + (size_t)inst * a.leaves_inst_pitch +
+                                                             32u * (node - W) + 16u * half);
+                } else {
+                    const uint32_t *nd = nodes + ((size_t)g * W + node) * 8 + 4 * half;
+                    v = make_uint4(bswap32(nd[0]), bswap32(nd[1]), bswap32(nd[2]), bswap32(nd[3]));
+                }
+                *reinterpret_cast<uint4 *>(a.branches + (size_t)inst * a.br_inst_pitch + (size_t)jl * 32u + 16u * half) = v;
             }
-            *reinterpret_cast<uint4 *>(a.branches + (size_t)inst * a.br_inst_pitch + (size_t)jl * 32u + 16u * half) = v;
         }
     }
 }
@@ -1180,6 +1187,7 @@ hipError_t rbc_launch_merkle(const MerkleArgs &a, bool check, hipStream_t st) {
     MerkleArgs b = a;
     // up to 512 / W trees per block (<= 64), but keep >= 512 blocks so that a
     // small batch still spreads over every CU (C2 and C4: 2 trees per block)
+    // (C4, W = 256, measured: 1 tree per block 0.68 ms, 2 trees 0.63, 4 trees 0.95)
     int g = a.width >= 512 ? 1 : (512 / a.width < 64 ? 512 / a.width : 64);
     while (g > 1 && (a.count + g - 1) / g < 512) g >>= 1;
     b.trees_per_block = g;
