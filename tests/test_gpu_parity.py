@@ -761,3 +761,24 @@ def test_device_verify_ragged_lengths(gpu, ref, n, f):
             assert got[i, j] == int(want), (i, j)
             assert leaves[i, j].tobytes() == ref.sha256(sh[i, j, :S].tobytes())
         assert 1 <= (got[i] == 0).sum() <= 2
+
+
+# every tree depth 1..8 (W = 2..256), non-power-of-two N, and an odd instance
+# count so the last merkle block holds fewer trees than trees_per_block: the
+# branch-write loop steps (j, l) by (32 / d, 32 % d) with a carry, so each
+# depth exercises a different stepping
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,f", [(2, 0), (3, 1), (6, 1), (11, 3), (17, 5), (32, 10), (33, 10), (100, 33),
+                                 (129, 42), (256, 85)])
+def test_merkle_build_branches_every_depth(gpu, ref, n, f):
+    k = n - 2 * f
+    B = 37 * k + 5
+    I = 5
+    pl = Pipeline(gpu, n, f, B, I, seed=4242 + n)
+    pl.commit()
+    roots = pl.arr("roots", shape=(I, 32))
+    brs = pl.arr("branches", shape=(I, n, max(pl.d, 1), 32))
+    for i in range(I):
+        _, want_root, want_br, _ = ref.encode_commit(n, f, pl.values[i, :B])
+        assert bytes(roots[i]) == want_root, (n, i)
+        assert np.array_equal(brs[i], want_br), (n, i)
