@@ -278,8 +278,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void rs
 #endif
     constexpr int GD = RBC_FFT_GD;  // decode: compare-pipeline group (VGPRs: 1 -> 143, 2 -> 157, 3 -> 181)
     static_assert(K >= 1 && K <= N && N <= W && 2 * N > W, "geometry");
-    const int col = blockIdx.x * 64 + threadIdx.x;  // dword column inside the row
-    const int inst = blockIdx.y;
+    // XCD-aware tile order: the dispatcher deals workgroups round-robin over
+    // the 8 XCDs (linear id % 8), so neighbouring column tiles of one instance
+    // would land on different L2s.  Encode reads data row j at j*S, which is
+    // not line aligned: a 256-B tile touches 3 lines, 2 of them shared with
+    // its neighbours.  Remapping linear id L -> (L % 8) * (T8 / 8) + L / 8
+    // gives each XCD a contiguous run of tiles, so the shared lines hit in
+    // that XCD's L2 instead of being fetched twice from HBM.
+    uint32_t tile_x = blockIdx.x, tile_y = blockIdx.y;
+#ifndef RBC_XCD_REMAP
+#define RBC_XCD_REMAP 1
+#endif
+    if constexpr (MODE == GF_MODE_ENCODE && RBC_XCD_REMAP) {
+        const uint32_t gx = gridDim.x, total = gx * gridDim.y, t8 = total & ~7u;
+        uint32_t lin = blockIdx.y * gx + blockIdx.x;
+        if (lin < t8) lin = (lin & 7u) * (t8 >> 3) + (lin >> 3);
+        tile_y = lin / gx;
+        tile_x = lin - tile_y * gx;
+    }
+    const int col = (int)tile_x * 64 + threadIdx.x;  // dword column inside the row
+    const int inst = (int)tile_y;
     if (inst >= a.count) return;
     if (a.status && a.status[inst] != 0) return;
     const uint32_t off = 4u * (uint32_t)col;
