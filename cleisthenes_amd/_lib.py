@@ -100,6 +100,17 @@ _SIGS = {
     "rbc_comm_init": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "rbc_comm_destroy": (c_int, [c_void_p]),
     "rbc_dev_allgather_roots": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "rbc_dev_allgather_records": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                          c_void_p]),
+    "rbc_comm_info": (c_int, [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_int), c_char_p, c_size_t,
+                              POINTER(c_int), c_char_p, c_size_t]),
+    "rbc_device_pci_bus_id": (c_int, [c_int, c_char_p, c_int]),
+    "rbc_acs_partition": (c_int, [c_int, c_int, c_int, POINTER(c_int), POINTER(c_int)]),
+    "rbc_acs_max_share": (c_int, [c_int, c_int, POINTER(c_int)]),
+    "rbc_acs_assemble": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, POINTER(c_int)]),
+    "rbc_dev_fill_random": (c_int, [c_int, c_void_p, c_void_p, c_uint64, c_uint64, c_uint64, c_uint64]),
+    "rbc_dev_count_mismatch": (c_int, [c_int, c_void_p, c_void_p, c_uint64, c_void_p, c_uint64, c_uint64, c_uint64,
+                                       c_void_p]),
     # include/rbc_protocol.h
     "rbc_pb_encode_rbc": (c_size_t, [c_int, c_void_p, c_size_t, c_void_p, c_size_t]),
     "rbc_pb_decode_rbc": (c_int, [c_void_p, c_size_t, POINTER(c_int), POINTER(c_void_p), szp]),

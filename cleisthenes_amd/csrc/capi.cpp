@@ -5,8 +5,11 @@
 // interpolate at rbc/rbc.go:86-100) and drives the batched HIP kernels in
 // kernels.hip.  Argument checks and error values follow klauspost/reedsolomon
 // v1.9.1 (reedsolomon.go: New, Split, Encode, Verify, Reconstruct, Join).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <limits.h>
 #include <rccl/rccl.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <stdlib.h>
@@ -1178,10 +1181,10 @@ int rbc_validate_batch(rbc_ctx *c, int count, const uint8_t *const *shards, cons
     for (int i = 0; i < count; ++i) {
         const uint32_t j = indices[i];
         // unflatten the Go-form branch (the empty level-0 sibling is omitted)
-        const bool empty0 = d > 0 && (int)(j ^ 1u) >= c->n;
+        const bool empty0 = d > 0 && (j ^ 1u) >= (uint32_t)c->n;
         const size_t want = (size_t)32 * (d - (empty0 ? 1 : 0));
         shape_ok[i] = 1;
-        if ((int)j >= c->n || branch_lens[i] != want || shard_lens[i] == 0 || !shards[i] || !roots[i] ||
+        if (j >= (uint32_t)c->n || branch_lens[i] != want || shard_lens[i] == 0 || !shards[i] || !roots[i] ||
             (want && !branches[i])) {
             shape_ok[i] = 0;
             ln[i] = 1;
@@ -1588,6 +1591,116 @@ int rbc_dev_allgather_roots(rbc_ctx *c, void *stream, int count, const uint8_t *
         RBC_HIP(hipMemset2DAsync(c->d_pack.as<uint8_t>() + 32, 64, 0, 32, count, st));
     if (ncclAllGather(c->d_pack.p, gathered, (size_t)count * 64, ncclUint8, c->comm, st) != ncclSuccess)
         return RBC_ERR_DEVICE;
+    return RBC_OK;
+}
+
+int rbc_dev_allgather_records(rbc_ctx *c, void *stream, int count, int slots, const uint8_t *roots,
+                              const uint8_t *digests, const int32_t *status, uint8_t *gathered) {
+    if (!c || count < 0 || slots < count || (count > 0 && !roots) || (slots > 0 && !gathered))
+        return RBC_ERR_INVALID_ARG;
+    if (!c->comm) return RBC_ERR_NO_COMM;
+    if (slots == 0) return RBC_OK;  // every rank passes the same slots: all skip together
+    std::lock_guard<std::mutex> lk(c->mu);
+    RBC_HIP(hipSetDevice(c->device));
+    hipStream_t st = as_stream(stream);
+    RBC_HIP(c->d_pack.ensure((size_t)slots * 64));
+    RBC_HIP(rbc_launch_pack_records(roots, digests, status, count, slots, c->d_pack.as<uint8_t>(), st));
+    if (ncclAllGather(c->d_pack.p, gathered, (size_t)slots * 64, ncclUint8, c->comm, st) != ncclSuccess)
+        return RBC_ERR_DEVICE;
+    return RBC_OK;
+}
+
+static void copy_path(const void *sym, char *out, size_t cap) {
+    if (!out || cap == 0) return;
+    out[0] = 0;
+    Dl_info info;
+    if (!dladdr(sym, &info) || !info.dli_fname) return;
+    char buf[PATH_MAX];
+    const char *p = realpath(info.dli_fname, buf) ? buf : info.dli_fname;
+    snprintf(out, cap, "%s", p);
+}
+
+int rbc_comm_info(rbc_ctx *c, int *nranks, int *rank, int *rccl_version, char *rccl_path, size_t rccl_cap,
+                  int *hip_runtime_version, char *hip_path, size_t hip_cap) {
+    if (!c) return RBC_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (rccl_version && ncclGetVersion(rccl_version) != ncclSuccess) return RBC_ERR_DEVICE;
+    if (hip_runtime_version && hipRuntimeGetVersion(hip_runtime_version) != hipSuccess) return RBC_ERR_DEVICE;
+    copy_path(reinterpret_cast<const void *>(&ncclAllGather), rccl_path, rccl_cap);
+    copy_path(reinterpret_cast<const void *>(&hipDeviceSynchronize), hip_path, hip_cap);
+    if (nranks || rank) {
+        if (!c->comm) return RBC_ERR_NO_COMM;
+        int nr = 0, r = 0;
+        if (ncclCommCount(c->comm, &nr) != ncclSuccess || ncclCommUserRank(c->comm, &r) != ncclSuccess)
+            return RBC_ERR_DEVICE;
+        if (nranks) *nranks = nr;
+        if (rank) *rank = r;
+    }
+    return RBC_OK;
+}
+
+int rbc_device_pci_bus_id(int device, char *out, int cap) {
+    if (!out || cap < 13) return RBC_ERR_INVALID_ARG;
+    RBC_HIP(hipDeviceGetPCIBusId(out, cap, device));
+    return RBC_OK;
+}
+
+// ---- ACS output-set assembly (host)
+int rbc_acs_partition(int total, int nranks, int rank, int *first, int *count) {
+    if (total < 0 || nranks < 1 || rank < 0 || rank >= nranks || !first || !count) return RBC_ERR_INVALID_ARG;
+    const int64_t a = (int64_t)rank * total / nranks, b = (int64_t)(rank + 1) * total / nranks;
+    *first = (int)a;
+    *count = (int)(b - a);
+    return RBC_OK;
+}
+
+int rbc_acs_max_share(int total, int nranks, int *slots) {
+    if (total < 0 || nranks < 1 || !slots) return RBC_ERR_INVALID_ARG;
+    *slots = (int)(((int64_t)total + nranks - 1) / nranks);  // = the largest contiguous share
+    return RBC_OK;
+}
+
+int rbc_acs_assemble(const uint8_t *gathered, int nranks, int slots, int total, int32_t *instances_out,
+                     uint8_t *records_out, int *out_count) {
+    if (!out_count || nranks < 1 || slots < 0 || total < 0 || (total > 0 && (!gathered || !instances_out)))
+        return RBC_ERR_INVALID_ARG;
+    int m = 0;
+    for (int r = 0; r < nranks; ++r) {
+        int first = 0, cnt = 0;
+        rbc_acs_partition(total, nranks, r, &first, &cnt);
+        if (cnt > slots) return RBC_ERR_INVALID_ARG;  // gather buffer smaller than a share
+        for (int t = 0; t < cnt; ++t) {
+            const uint8_t *rec = gathered + ((size_t)r * slots + t) * 64;
+            uint8_t any = 0;
+            for (int q = 32; q < 64; ++q) any |= rec[q];
+            if (!any) continue;  // zero digest: interpolate failed, not in the set
+            instances_out[m] = first + t;
+            if (records_out) memcpy(records_out + (size_t)m * 64, rec, 64);
+            ++m;
+        }
+    }
+    *out_count = m;
+    return RBC_OK;
+}
+
+// ---- test / bench utilities
+int rbc_dev_fill_random(int device, void *stream, uint8_t *dst, uint64_t first_row, uint64_t rows, uint64_t pitch,
+                        uint64_t seed) {
+    if ((!dst && rows) || pitch % 16) return RBC_ERR_INVALID_ARG;
+    RBC_HIP(hipSetDevice(device));
+    RBC_HIP(rbc_launch_fill_random(dst, first_row, rows, pitch, seed, as_stream(stream)));
+    return RBC_OK;
+}
+
+int rbc_dev_count_mismatch(int device, void *stream, const uint8_t *a, uint64_t a_pitch, const uint8_t *b,
+                           uint64_t b_pitch, uint64_t rows, uint64_t len, uint32_t *mismatch_dev) {
+    if (!mismatch_dev || (rows && len && (!a || !b))) return RBC_ERR_INVALID_ARG;
+    if (a_pitch % 16 || b_pitch % 16 || len > a_pitch || len > b_pitch || ((uintptr_t)a | (uintptr_t)b) % 16)
+        return RBC_ERR_INVALID_ARG;
+    RBC_HIP(hipSetDevice(device));
+    hipStream_t st = as_stream(stream);
+    RBC_HIP(hipMemsetAsync(mismatch_dev, 0, sizeof(uint32_t), st));
+    RBC_HIP(rbc_launch_count_mismatch(a, a_pitch, b, b_pitch, rows, len, mismatch_dev, st));
     return RBC_OK;
 }
 

@@ -1067,8 +1067,104 @@ __global__ void inject_faults_kernel(uint8_t *shards, uint64_t inst_pitch, uint3
 }
 
 // ============================================================================
+// ACS records (rbc_dev_allgather_records): [slots][64] = {root, digest} per
+// instance, zero past `count`; the digest of an instance whose interpolate
+// failed (status != 0) is all-zero, so the record says on its own whether
+// the instance is in the output set.  One thread per 16-byte quarter.
+// ============================================================================
+__global__ void pack_records_kernel(const uint8_t *roots, const uint8_t *digests, const int32_t *status, int count,
+                                    int slots, uint8_t *out) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= slots * 4) return;
+    const int i = t >> 2, q = t & 3;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (i < count) {
+        const bool ok = !status || status[i] == 0;
+        if (q < 2) v = *reinterpret_cast<const uint4 *>(roots + (size_t)i * 32 + 16 * q);
+        else if (digests && ok) v = *reinterpret_cast<const uint4 *>(digests + (size_t)i * 32 + 16 * (q - 2));
+    }
+    *reinterpret_cast<uint4 *>(out + (size_t)i * 64 + 16 * q) = v;
+}
+
+// ============================================================================
+// Synthetic input (bench / tests): row r (global index first_row + local
+// row), 64-bit word w of a [rows][pitch] buffer =
+// splitmix64(seed * golden + r * (pitch / 8) + w), little-endian.
+// The host restates the same function (cleisthenes_amd.synth) to rebuild
+// any row for the oracle check, so multi-GiB inputs never cross PCIe.
+// ============================================================================
+RBC_DEV uint64_t splitmix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void fill_random_kernel(uint8_t *dst, uint64_t first_row, uint64_t rows,
+                                                          uint64_t pitch, uint64_t seed) {
+    const uint64_t chunks = pitch / 16;  // pitch % 16 == 0
+    const uint64_t total = rows * chunks;
+    const uint64_t base = seed * 0x9E3779B97F4A7C15ull + first_row * (pitch / 8);
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < total;
+         c += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t r = c / chunks, q = c - r * chunks;
+        const uint64_t w0 = base + r * (pitch / 8) + 2 * q;
+        const uint64_t a = splitmix64(w0), b = splitmix64(w0 + 1);
+        *reinterpret_cast<uint4 *>(dst + r * pitch + 16 * q) =
+            make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+    }
+}
+
+// Count the 16-byte chunks where rows of a and b differ in their first `len`
+// bytes (both pitches % 16 == 0, 16-byte aligned bases).
+__global__ __launch_bounds__(256) void count_mismatch_kernel(const uint8_t *a, uint64_t a_pitch, const uint8_t *b,
+                                                             uint64_t b_pitch, uint64_t rows, uint64_t len,
+                                                             uint32_t *counter) {
+    const uint64_t chunks = (len + 15) / 16;
+    const uint64_t total = rows * chunks;
+    uint32_t bad = 0;
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < total;
+         c += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t r = c / chunks, q = c - r * chunks;
+        uint4 x = *reinterpret_cast<const uint4 *>(a + r * a_pitch + 16 * q);
+        uint4 y = *reinterpret_cast<const uint4 *>(b + r * b_pitch + 16 * q);
+        const int nv = (int)min((uint64_t)16, len - 16 * q);
+        if (nv < 16) {
+            x = mask16(x, nv);
+            y = mask16(y, nv);
+        }
+        bad += (x.x != y.x || x.y != y.y || x.z != y.z || x.w != y.w) ? 1u : 0u;
+    }
+    if (bad) atomicAdd(counter, bad);
+}
+
+// ============================================================================
 // launchers
 // ============================================================================
+hipError_t rbc_launch_pack_records(const uint8_t *roots, const uint8_t *digests, const int32_t *status, int count,
+                                   int slots, uint8_t *out, hipStream_t st) {
+    if (slots <= 0) return hipSuccess;
+    hipLaunchKernelGGL(pack_records_kernel, dim3((slots * 4 + 255) / 256), dim3(256), 0, st, roots, digests, status,
+                       count, slots, out);
+    return hipGetLastError();
+}
+
+hipError_t rbc_launch_fill_random(uint8_t *dst, uint64_t first_row, uint64_t rows, uint64_t pitch, uint64_t seed,
+                                  hipStream_t st) {
+    if (rows == 0 || pitch == 0) return hipSuccess;
+    if (pitch % 16) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(fill_random_kernel, dim3(8192), dim3(256), 0, st, dst, first_row, rows, pitch, seed);
+    return hipGetLastError();
+}
+
+hipError_t rbc_launch_count_mismatch(const uint8_t *a, uint64_t a_pitch, const uint8_t *b, uint64_t b_pitch,
+                                     uint64_t rows, uint64_t len, uint32_t *counter, hipStream_t st) {
+    if (rows == 0 || len == 0) return hipSuccess;
+    if (a_pitch % 16 || b_pitch % 16 || len > a_pitch || len > b_pitch || ((uintptr_t)a | (uintptr_t)b) % 16)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(count_mismatch_kernel, dim3(8192), dim3(256), 0, st, a, a_pitch, b, b_pitch, rows, len,
+                       counter);
+    return hipGetLastError();
+}
 template <int RC, int TPB = 256>
 static hipError_t launch_gf_rc(const GfArgs &a, hipStream_t st) {
     const int KP = (a.K + 1) & ~1;

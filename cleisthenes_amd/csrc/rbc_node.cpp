@@ -182,7 +182,8 @@ int b64_val(char c) {
 }
 
 // base64.StdEncoding.DecodeString as encoding/json applies it: padding
-// required, '\r' / '\n' ignored, non-zero trailing bits rejected.
+// required, '\r' / '\n' ignored.  StdEncoding is not Strict(), so non-zero
+// trailing bits in the last quantum are ignored ("AB==" decodes to 0x00).
 bool b64_decode(const std::string &in, std::string &out) {
     std::string s;
     s.reserve(in.size());
@@ -198,8 +199,6 @@ bool b64_decode(const std::string &in, std::string &out) {
         for (int j = 0; j < 4 - pad; ++j)
             if ((v[j] = b64_val(s[i + j])) < 0) return false;
         for (int j = 4 - pad; j < 4; ++j) v[j] = 0;
-        if (pad == 2 && (v[1] & 15)) return false;
-        if (pad == 1 && (v[2] & 3)) return false;
         const uint32_t w = (uint32_t)v[0] << 18 | (uint32_t)v[1] << 12 | (uint32_t)v[2] << 6 | (uint32_t)v[3];
         out.push_back((char)(w >> 16));
         if (pad < 2) out.push_back((char)(w >> 8));
@@ -450,10 +449,15 @@ struct Out {
 
 }  // namespace
 
+// The broadcast value is framed as [u64 little-endian length][value] before
+// Split, so delivery returns exactly the proposed bytes: interpolate alone
+// yields k*S bytes with the zero pad (rbc/rbc.go:86-90 carries no length).
+constexpr size_t kFrame = 8;
+
 struct rbc_node {
     rbc_batcher *b = nullptr;
     int n = 0, f = 0, k = 0, depth = 0, self = 0, proposer = 0;
-    bool proposed = false, val_seen = false, ready_sent = false, delivered = false;
+    bool proposed = false, val_seen = false, ready_sent = false, delivered = false, value_ok = false;
     std::vector<char> echo_from, ready_from;  // first message per sender only
     std::map<std::string, RootState> roots;
     std::string delivered_root;
@@ -561,7 +565,15 @@ struct rbc_node {
         if (!delivered && s.have_value && s.readies >= 2 * f + 1 && s.echoes >= n - 2 * f) {
             delivered = true;
             delivered_root = root;
-            value = s.value;
+            // unframe: [u64 LE length][value][Split zero pad].  Every honest
+            // node decodes the same k*S bytes, so a bad length (a Byzantine
+            // proposer's) is seen identically everywhere: delivered, unusable.
+            uint64_t L = 0;
+            if (s.value.size() >= kFrame) {
+                for (int b = 0; b < 8; ++b) L |= (uint64_t)s.value[b] << (8 * b);
+                value_ok = L <= s.value.size() - kFrame;
+            }
+            if (value_ok) value.assign(s.value.begin() + kFrame, s.value.begin() + kFrame + (size_t)L);
         }
     }
 
@@ -666,7 +678,9 @@ int rbc_json_decode_ready(const uint8_t *json, size_t len, uint8_t *root_out) {
 }
 
 int rbc_node_create(rbc_batcher *batcher, int n, int f, int self, int proposer, rbc_node **out) {
-    if (!batcher || !out || n < 1 || f < 0 || n - 2 * f < 1 || self < 0 || self >= n || proposer < 0 ||
+    // n >= 3f + 1: the HBBFT thresholds (N-f ECHO, f+1 / 2f+1 READY) need it
+    // for quorum intersection (the raw data-path context stays permissive)
+    if (!batcher || !out || n < 1 || f < 0 || n < 3 * f + 1 || self < 0 || self >= n || proposer < 0 ||
         proposer >= n)
         return RBC_ERR_INVALID_ARG;
     rbc_node *node = new rbc_node();
@@ -695,11 +709,13 @@ void rbc_node_destroy(rbc_node *node) {
 int rbc_node_propose(rbc_node *node, const uint8_t *value, size_t len) {
     if (!node || (!value && len)) return RBC_ERR_INVALID_ARG;
     if (node->self != node->proposer || node->proposed) return RBC_ERR_PROTOCOL;
-    if (len == 0) return RBC_ERR_SHORT_DATA;
-    node->proposed = true;
+    node->proposed = true;  // an empty value is a valid (framed, 8-byte) proposal
     auto op = std::make_unique<Op>();
     op->kind = OP_SHARD;
-    op->value.assign((const char *)value, len);
+    op->value.resize(kFrame);
+    for (size_t b = 0; b < kFrame; ++b) op->value[b] = (char)((uint64_t)len >> (8 * b));
+    op->value.append((const char *)value, len);
+    len = op->value.size();
     op->S = (len + node->k - 1) / node->k;
     op->shards.resize((size_t)node->n * op->S);
     op->branches.resize((size_t)node->n * (node->depth ? node->depth : 1) * 32);
@@ -790,6 +806,7 @@ int rbc_node_value(rbc_node *node, uint8_t *buf, size_t cap, size_t *len, int *d
     if (!node || !len || !delivered) return RBC_ERR_INVALID_ARG;
     *delivered = node->delivered;
     *len = node->delivered ? node->value.size() : 0;
+    if (node->delivered && !node->value_ok) return RBC_ERR_PROTOCOL;  // agreed on, but badly framed
     if (!node->delivered || (!buf && cap == 0)) return RBC_OK;  // NULL buffer: size query
     if (!buf || node->value.size() > cap) return RBC_ERR_INVALID_ARG;
     memcpy(buf, node->value.data(), node->value.size());

@@ -11,6 +11,7 @@ interpolate work on the GPU through a shared ``Batcher``.
 """
 from __future__ import annotations
 
+import struct
 from ctypes import byref, c_int, c_size_t, c_void_p
 from typing import List, Optional, Tuple
 
@@ -20,6 +21,12 @@ from ._lib import RBC_ERR_INVALID_ARG, RBC_ERR_PROTOCOL, RBCError, check, lib
 from .rbc import Batcher, _bytes_array, _ptr
 
 VAL, ECHO, READY = 0, 1, 2
+
+
+def frame(value: bytes) -> bytes:
+    """The payload a Node broadcasts for `value`: [u64 little-endian len][value]
+    (rbc_node_propose), so delivery can return exactly the proposed bytes."""
+    return struct.pack("<Q", len(value)) + bytes(value)
 
 
 def _buf(x) -> Tuple[np.ndarray, Optional[c_void_p]]:
@@ -136,6 +143,9 @@ class Node:
             out.append((to.value, bytes(buf[:n.value])))
 
     def value(self) -> Optional[bytes]:
+        """The delivered value (exactly the proposer's bytes), None before
+        delivery; RBCError(RBC_ERR_PROTOCOL) if the agreed payload is badly
+        framed (a Byzantine proposer)."""
         n, d = c_size_t(0), c_int(0)
         check(lib.rbc_node_value(self._p, None, 0, byref(n), byref(d)), "rbc_node_value")
         if not d.value:

@@ -34,6 +34,25 @@ def _ptr(a: np.ndarray) -> c_void_p:
     return c_void_p(a.ctypes.data)
 
 
+def pci_bus_id(device: int) -> str:
+    buf = ctypes.create_string_buffer(64)
+    check(lib.rbc_device_pci_bus_id(device, buf, 64), "rbc_device_pci_bus_id")
+    return buf.value.decode().lower()
+
+
+def fill_random(device: int, stream, dst, first_row: int, rows: int, pitch: int, seed: int) -> None:
+    """Synthetic bytes on the device (cleisthenes_amd.synth restates them)."""
+    check(lib.rbc_dev_fill_random(device, _dv(stream), _dv(dst), first_row, rows, pitch, seed),
+          "rbc_dev_fill_random")
+
+
+def count_mismatch(device: int, stream, a, a_pitch: int, b, b_pitch: int, rows: int, length: int, counter) -> None:
+    """Device counter <- 16-byte chunks where rows of a and b differ in
+    their first `length` bytes (read it after the stream completes)."""
+    check(lib.rbc_dev_count_mismatch(device, _dv(stream), _dv(a), a_pitch, _dv(b), b_pitch, rows, length,
+                                     _dv(counter)), "rbc_dev_count_mismatch")
+
+
 def _bytes_array(x) -> np.ndarray:
     if x is None:
         return np.zeros(0, dtype=np.uint8)
@@ -397,6 +416,26 @@ class Context:
     def dev_allgather_roots(self, stream, count, roots, digests, gathered) -> None:
         check(lib.rbc_dev_allgather_roots(self._p, _dv(stream), count, _dv(roots), _dv(digests), _dv(gathered)),
               "rbc_dev_allgather_roots")
+
+    def dev_allgather_records(self, stream, count, slots, roots, digests, status, gathered) -> None:
+        """Ragged-share ACS all-gather: [nranks][slots][64] records, zero
+        padded; a failed instance (status != 0) carries a zero digest."""
+        check(lib.rbc_dev_allgather_records(self._p, _dv(stream), count, slots, _dv(roots), _dv(digests),
+                                            _dv(status), _dv(gathered)), "rbc_dev_allgather_records")
+
+    def comm_info(self, with_comm: bool = True) -> dict:
+        """RCCL as it reports itself: nranks / rank of the communicator, the
+        library version and the files RCCL and the HIP runtime were mapped from."""
+        nr, rk, ver, hver = c_int(0), c_int(0), c_int(0), c_int(0)
+        rp, hp = ctypes.create_string_buffer(4096), ctypes.create_string_buffer(4096)
+        check(lib.rbc_comm_info(self._p, byref(nr) if with_comm else None, byref(rk) if with_comm else None,
+                                byref(ver), rp, 4096, byref(hver), hp, 4096), "rbc_comm_info")
+        v = ver.value
+        out = {"version": v, "version_str": f"{v // 10000}.{(v // 100) % 100}.{v % 100}",
+               "lib": rp.value.decode(), "hip_runtime_version": hver.value, "hip_lib": hp.value.decode()}
+        if with_comm:
+            out.update(nranks=nr.value, rank=rk.value)
+        return out
 
 
 class Encoder:

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define RBC_ABI_VERSION 1
+#define RBC_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------- */
 #define RBC_OK 0
@@ -245,6 +245,46 @@ int rbc_comm_init(rbc_ctx *ctx, int nranks, int rank, const uint8_t id[128]);
 int rbc_comm_destroy(rbc_ctx *ctx);
 int rbc_dev_allgather_roots(rbc_ctx *ctx, void *stream, int count, const uint8_t *roots,
                             const uint8_t *digests, uint8_t *gathered);
+/* Ragged shares (total % nranks != 0): every rank sends `slots` records
+ * (slots = rbc_acs_max_share, the same on every rank); its own `count` <=
+ * slots are packed on the device and the rest are zero.  The digest of an
+ * instance with status[i] != 0 (interpolate failed; status nullable) is sent
+ * as 32 zero bytes, so a record alone says whether the instance is in the ACS
+ * output set.  gathered: [nranks][slots][64]. */
+int rbc_dev_allgather_records(rbc_ctx *ctx, void *stream, int count, int slots, const uint8_t *roots,
+                              const uint8_t *digests, const int32_t *status, uint8_t *gathered);
+/* The communicator as RCCL reports it (ncclCommCount / ncclCommUserRank /
+ * ncclGetVersion) and the files the RCCL and HIP runtimes were mapped from
+ * (lib paths nullable; truncated to cap). */
+int rbc_comm_info(rbc_ctx *ctx, int *nranks, int *rank, int *rccl_version, char *rccl_path, size_t rccl_cap,
+                  int *hip_runtime_version, char *hip_path, size_t hip_cap);
+/* PCI bus id of a device ("0000:xx:yy.z"), for host NUMA placement per rank. */
+int rbc_device_pci_bus_id(int device, char *out, int cap);
+
+/* ---- ACS output-set assembly (host only; the consumer of the all-gather) --
+ * The reference's ACS is absent (honeybadger.go:19-21 TODO, sendBatch panics
+ * at honeybadger.go:57-59): this is the part of it that turns the gathered
+ * RBC outputs into the ordered epoch set.  Instances are partitioned over
+ * ranks in contiguous blocks: rank r owns [r*total/nranks, (r+1)*total/nranks). */
+int rbc_acs_partition(int total, int nranks, int rank, int *first, int *count);
+int rbc_acs_max_share(int total, int nranks, int *slots);
+/* gathered [nranks][slots][64] (rbc_dev_allgather_records output, on the
+ * host) -> the instances with a non-zero digest, in instance order:
+ * instances_out[m] = id, records_out [m][64] (nullable), *out_count = m.
+ * Both outputs need room for `total` entries. */
+int rbc_acs_assemble(const uint8_t *gathered, int nranks, int slots, int total, int32_t *instances_out,
+                     uint8_t *records_out, int *out_count);
+
+/* ---- test / bench utilities (synthetic inputs and result checks) ---------- */
+/* dst [rows][pitch] (pitch % 16 == 0): 64-bit word w of local row i, global
+ * row r = first_row + i, is splitmix64(seed * 0x9E3779B97F4A7C15 + r * pitch / 8
+ * + w), little-endian (restated on the host by cleisthenes_amd.synth). */
+int rbc_dev_fill_random(int device, void *stream, uint8_t *dst, uint64_t first_row, uint64_t rows, uint64_t pitch,
+                        uint64_t seed);
+/* *mismatch_dev (device uint32, zeroed first) = number of 16-byte chunks in
+ * which the first len bytes of rows a[r] and b[r] differ, r < rows. */
+int rbc_dev_count_mismatch(int device, void *stream, const uint8_t *a, uint64_t a_pitch, const uint8_t *b,
+                           uint64_t b_pitch, uint64_t rows, uint64_t len, uint32_t *mismatch_dev);
 
 #ifdef __cplusplus
 }

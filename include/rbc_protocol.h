@@ -83,7 +83,9 @@ typedef struct rbc_node rbc_node;
 /* NewRBC (rbc/rbc.go:38). */
 int rbc_node_create(rbc_batcher *batcher, int n, int f, int self, int proposer, rbc_node **out);
 void rbc_node_destroy(rbc_node *node); /* waits for its outstanding GPU work */
-/* Proposer only: shard + commit `value` (copied), then VAL(h, b_j, s_j) to every j. */
+/* Proposer only: shard + commit `value` (copied), then VAL(h, b_j, s_j) to every j.
+ * The broadcast payload is framed as [u64 little-endian len][value] (len 0 is
+ * allowed), so rbc_node_value returns exactly these bytes. */
 int rbc_node_propose(rbc_node *node, const uint8_t *value, size_t len);
 /* HandleMessage (rbc/rbc.go:47): a marshaled pb.Message from node `sender`.
  * Parses and submits its GPU check; the outcome applies in rbc_node_progress.
@@ -99,9 +101,12 @@ int rbc_node_progress(rbc_node *node, int wait, int *pending_out);
  * its own ECHO/READY locally).  *len = 0: queue empty.  cap too small:
  * returns RBC_ERR_INVALID_ARG with *len = the size needed (message kept). */
 int rbc_node_next_message(rbc_node *node, int *to, uint8_t *buf, size_t cap, size_t *len);
-/* Value (rbc/rbc.go:69): *delivered = 1 once decided; the value is the k data
- * shards concatenated (k*S bytes: the original length is not carried).
- * buf NULL with cap 0: only *len and *delivered are set. */
+/* Value (rbc/rbc.go:69): *delivered = 1 once decided; the value is the
+ * proposer's bytes, unframed from the interpolated k*S bytes.  A delivered
+ * payload whose frame length exceeds it (a Byzantine proposer: every honest
+ * node sees the same bytes) returns RBC_ERR_PROTOCOL with *delivered = 1 and
+ * *len = 0.  buf NULL with cap 0: only *len and *delivered are set.
+ * rbc_node_create requires n >= 3f + 1 (HBBFT quorum intersection). */
 int rbc_node_value(rbc_node *node, uint8_t *buf, size_t cap, size_t *len, int *delivered);
 /* Valid ECHOs and READYs for the leading root, READY sent (0/1), messages
  * rejected (bad proof, wrong sender, malformed, duplicate). */

@@ -323,12 +323,12 @@ void rbcref_merkle_from_leaves(int n, const uint8_t *leaves, uint8_t *root, uint
     free(len);
 }
 
-int rbcref_merkle_verify(int n, const uint8_t *shard, size_t S, uint32_t index, const uint8_t *branch,
-                         const uint8_t *root) {
+/* branch walk from a known leaf digest (the verify half of validateMessage) */
+static int merkle_walk(int n, const uint8_t leaf[32], uint32_t index, const uint8_t *branch, const uint8_t *root) {
     if ((int)index >= n) return 0;
     int d = tree_depth(n);
     uint8_t h[32], buf[64];
-    rbcref_sha256(shard, S, h);
+    memcpy(h, leaf, 32);
     uint32_t t = index;
     for (int l = 0; l < d; l++, t >>= 1) {
         int empty = (l == 0) && ((int)(index ^ 1) >= n);
@@ -342,6 +342,14 @@ int rbcref_merkle_verify(int n, const uint8_t *shard, size_t S, uint32_t index, 
         }
     }
     return memcmp(h, root, 32) == 0;
+}
+
+int rbcref_merkle_verify(int n, const uint8_t *shard, size_t S, uint32_t index, const uint8_t *branch,
+                         const uint8_t *root) {
+    uint8_t h[32];
+    if ((int)index >= n) return 0;
+    rbcref_sha256(shard, S, h);
+    return merkle_walk(n, h, index, branch, root);
 }
 
 /* klauspost builds the encode matrix once in New(); cache it per (k, n) so
@@ -446,6 +454,63 @@ int rbcref_interpolate(int n, int f, const uint8_t *shards, size_t pitch, size_t
     return ok ? 0 : -8;
 }
 
+/* interpolate() as the GPU path runs it: the first k valid shards decode the
+ * rest (Lagrange/inverse D as above); a valid-but-unused shard that equals its
+ * re-encoding keeps the leaf its ECHO was verified with (leaves_in[j]), every
+ * other regenerated row is hashed.  Same result as rbcref_interpolate, which
+ * re-hashes all n rows. */
+int rbcref_interpolate_leaves(int n, int f, const uint8_t *shards, size_t pitch, size_t S, const uint8_t *valid,
+                              const uint8_t *leaves_in, const uint8_t *root, uint8_t *value_out,
+                              uint8_t *digest_out) {
+    gf_init();
+    int k = n - 2 * f;
+    if (k <= 0 || n > 256) return -1;
+    int used[256], regen[256], nu = 0, nr = 0;
+    for (int j = 0; j < n; j++) {
+        if (valid[j] && nu < k) used[nu++] = j;
+        else regen[nr++] = j;
+    }
+    if (nu < k) return -3;
+    const uint8_t *m = cached_matrix(k, n);
+    uint8_t *sub = (uint8_t *)malloc((size_t)k * k),
+            *inv = (uint8_t *)malloc((size_t)k * k), *dm = (uint8_t *)malloc((size_t)(nr ? nr : 1) * k);
+    for (int r = 0; r < k; r++) memcpy(sub + r * k, m + (size_t)used[r] * k, k);
+    int rc = rbcref_invert(k, sub, inv);
+    if (rc) { free(sub); free(inv); free(dm); return rc; }
+    for (int r = 0; r < nr; r++)
+        for (int c = 0; c < k; c++) {
+            uint8_t acc = 0;
+            for (int i = 0; i < k; i++) acc ^= MUL_[m[(size_t)regen[r] * k + i]][inv[i * k + c]];
+            dm[r * k + c] = acc;
+        }
+    uint8_t *full = (uint8_t *)malloc((size_t)n * S);
+    const uint8_t **in = (const uint8_t **)malloc(sizeof(void *) * k);
+    uint8_t **out = (uint8_t **)malloc(sizeof(void *) * (nr ? nr : 1));
+    for (int i = 0; i < k; i++) {
+        in[i] = shards + (size_t)used[i] * pitch;
+        memcpy(full + (size_t)used[i] * S, in[i], S);
+    }
+    for (int r = 0; r < nr; r++) out[r] = full + (size_t)regen[r] * S;
+    rbcref_gf_rows(nr, k, dm, in, out, S);
+    uint8_t *lv = (uint8_t *)malloc((size_t)32 * n), r2[32];
+    for (int i = 0; i < k; i++) memcpy(lv + 32 * used[i], leaves_in + 32 * used[i], 32);
+    for (int r = 0; r < nr; r++) {
+        const int j = regen[r];
+        if (valid[j] && memcmp(full + (size_t)j * S, shards + (size_t)j * pitch, S) == 0)
+            memcpy(lv + 32 * j, leaves_in + 32 * j, 32);
+        else
+            rbcref_sha256(full + (size_t)j * S, S, lv + 32 * j);
+    }
+    rbcref_merkle_from_leaves(n, lv, r2, NULL);
+    int ok = memcmp(r2, root, 32) == 0;
+    if (ok) {
+        if (value_out) memcpy(value_out, full, (size_t)k * S);
+        if (digest_out) rbcref_sha256(lv, (size_t)32 * k, digest_out);
+    }
+    free(lv); free(full); free(in); free(out); free(sub); free(inv); free(dm);
+    return ok ? 0 : -8;
+}
+
 /* ------------------------------------------------- CPU baseline pipeline */
 /* One "step" per instance, the same work bench.py's GPU step does:
  * encode+commit -> (corrupt) -> verify all N echoes -> interpolate from the
@@ -457,7 +522,14 @@ typedef struct {
     const uint8_t *present;     /* count x n */
     const int32_t *corrupt;     /* count: shard index to corrupt or -1 */
     int status_sum;
+    double enc_secs, dec_secs;  /* this thread's encode+commit / verify+decode time */
 } job_t;
+
+static double now_s(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec + 1e-9 * t.tv_nsec;
+}
 
 static void *pipeline_worker(void *arg) {
     job_t *jb = (job_t *)arg;
@@ -466,30 +538,52 @@ static void *pipeline_worker(void *arg) {
     uint8_t *shards = (uint8_t *)malloc((size_t)n * pitch);
     uint8_t *br = (uint8_t *)malloc((size_t)n * (d ? d : 1) * 32);
     uint8_t *value = (uint8_t *)malloc((size_t)k * S);
+    uint8_t *lv = (uint8_t *)malloc((size_t)32 * n);
     uint8_t root[32], dig[32], valid[256];
     for (int i = 0; i < jb->count; i++) {
         const int vi = (jb->first + i) % jb->nvals;
+        const double t0 = now_s();
         rbcref_encode_commit(n, f, jb->values + (size_t)vi * jb->B, jb->B, shards, pitch, root, br, NULL);
+        const double t1 = now_s();
         int cj = jb->corrupt[i];
         if (cj >= 0) shards[(size_t)cj * pitch] ^= 0x5a;
-        for (int j = 0; j < n; j++)
-            valid[j] = jb->present[(size_t)i * n + j] &&
-                       rbcref_merkle_verify(n, shards + (size_t)j * pitch, S, j, br + (size_t)j * d * 32, root);
-        int rc = rbcref_interpolate(n, f, shards, pitch, S, valid, root, value, dig);
+        /* validateMessage for every present ECHO, keeping its leaf digest */
+        for (int j = 0; j < n; j++) {
+            valid[j] = 0;
+            if (!jb->present[(size_t)i * n + j]) continue;
+            rbcref_sha256(shards + (size_t)j * pitch, S, lv + 32 * j);
+            valid[j] = (uint8_t)merkle_walk(n, lv + 32 * j, j, br + (size_t)j * d * 32, root);
+        }
+        int rc = rbcref_interpolate_leaves(n, f, shards, pitch, S, valid, lv, root, value, dig);
         jb->status_sum += rc;
         if (cj >= 0) shards[(size_t)cj * pitch] ^= 0x5a;
+        const double t2 = now_s();
+        jb->enc_secs += t1 - t0;
+        jb->dec_secs += t2 - t1;
     }
-    free(shards); free(br); free(value);
+    free(shards); free(br); free(value); free(lv);
     return NULL;
 }
 
 /* Returns wall seconds for `count` instances split over `threads`. */
+double rbcref_pipeline2(int n, int f, int count, size_t B, int threads, const uint8_t *values, int nvals,
+                        const uint8_t *present, const int32_t *corrupt, int *status_sum, double *enc_secs,
+                        double *dec_secs);
 double rbcref_pipeline(int n, int f, int count, size_t B, int threads, const uint8_t *values, int nvals,
                        const uint8_t *present, const int32_t *corrupt, int *status_sum) {
+    return rbcref_pipeline2(n, f, count, B, threads, values, nvals, present, corrupt, status_sum, NULL, NULL);
+}
+
+/* ... and the summed per-thread time of each phase (encode+commit,
+ * verify+decode), so phase rates are bytes * threads / phase seconds. */
+double rbcref_pipeline2(int n, int f, int count, size_t B, int threads, const uint8_t *values, int nvals,
+                        const uint8_t *present, const int32_t *corrupt, int *status_sum, double *enc_secs,
+                        double *dec_secs) {
     gf_init();
     cpu_detect();
     if (threads < 1) threads = 1;
     if (threads > count) threads = count;
+    if (threads > 256) threads = 256;
     pthread_t th[256];
     job_t jobs[256];
     struct timespec t0, t1;
@@ -497,13 +591,21 @@ double rbcref_pipeline(int n, int f, int count, size_t B, int threads, const uin
     int per = count / threads, extra = count % threads, first = 0;
     for (int t = 0; t < threads; t++) {
         int c = per + (t < extra);
-        jobs[t] = (job_t){n, f, first, c, nvals, B, values, present + (size_t)first * n, corrupt + first, 0};
+        jobs[t] = (job_t){n, f, first, c, nvals, B, values, present + (size_t)first * n, corrupt + first, 0, 0, 0};
         pthread_create(&th[t], NULL, pipeline_worker, &jobs[t]);
         first += c;
     }
     int s = 0;
-    for (int t = 0; t < threads; t++) { pthread_join(th[t], NULL); s += jobs[t].status_sum; }
+    double es = 0, ds = 0;
+    for (int t = 0; t < threads; t++) {
+        pthread_join(th[t], NULL);
+        s += jobs[t].status_sum;
+        es += jobs[t].enc_secs;
+        ds += jobs[t].dec_secs;
+    }
     clock_gettime(CLOCK_MONOTONIC, &t1);
     if (status_sum) *status_sum = s;
+    if (enc_secs) *enc_secs = es;
+    if (dec_secs) *dec_secs = ds;
     return (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
 }

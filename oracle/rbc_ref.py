@@ -34,6 +34,11 @@ def load():
     lib.rbcref_pipeline.argtypes = [c_int, c_int, c_int, c_size_t, c_int, c_void_p, c_int, c_void_p, c_void_p,
                                     POINTER(c_int)]
     lib.rbcref_pipeline.restype = c_double
+    lib.rbcref_pipeline2.argtypes = [c_int, c_int, c_int, c_size_t, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                                     POINTER(c_int), POINTER(c_double), POINTER(c_double)]
+    lib.rbcref_pipeline2.restype = c_double
+    lib.rbcref_interpolate_leaves.argtypes = [c_int, c_int, c_void_p, c_size_t, c_size_t, c_void_p, c_void_p,
+                                              c_void_p, c_void_p, c_void_p]
     lib.rbcref_tree_depth.argtypes = [c_int]
     lib.rbcref_cpu_features.restype = c_int
     lib.rbcref_force_scalar.argtypes = [c_int]
@@ -105,10 +110,29 @@ def interpolate(n: int, f: int, shards: np.ndarray, valid: np.ndarray, root: byt
     return rc, value, bytes(dig)
 
 
-def pipeline(n, f, count, B, threads, values, present, corrupt):
-    """values: [nvals][B]; instance i encodes values[i % nvals]."""
+def interpolate_leaves(n: int, f: int, shards: np.ndarray, valid: np.ndarray, leaves: np.ndarray, root: bytes):
+    """interpolate reusing the verified leaves of valid shards -> (status, value, digest)"""
+    k = n - 2 * f
+    shards = np.ascontiguousarray(shards, dtype=np.uint8)
+    S = shards.shape[1]
+    v = np.ascontiguousarray(valid, dtype=np.uint8)
+    lv = np.ascontiguousarray(leaves, dtype=np.uint8)
+    r = np.frombuffer(root, dtype=np.uint8).copy()
+    value = np.zeros(k * S, dtype=np.uint8)
+    dig = np.zeros(32, dtype=np.uint8)
+    rc = lib().rbcref_interpolate_leaves(n, f, p(shards), S, S, p(v), p(lv), p(r), p(value), p(dig))
+    return rc, value, bytes(dig)
+
+
+def pipeline(n, f, count, B, threads, values, present, corrupt, phases=False):
+    """values: [nvals][B]; instance i encodes values[i % nvals].  -> (wall
+    seconds, status sum[, encode+commit thread-seconds, verify+decode
+    thread-seconds])"""
     st = c_int(0)
+    es, ds = c_double(0), c_double(0)
     values = np.ascontiguousarray(values, dtype=np.uint8)
-    secs = lib().rbcref_pipeline(n, f, count, B, threads, p(values), values.shape[0], p(present), p(corrupt),
-                                 ctypes.byref(st))
+    secs = lib().rbcref_pipeline2(n, f, count, B, threads, p(values), values.shape[0], p(present), p(corrupt),
+                                  ctypes.byref(st), ctypes.byref(es), ctypes.byref(ds))
+    if phases:
+        return secs, st.value, es.value, ds.value
     return secs, st.value

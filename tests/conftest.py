@@ -32,3 +32,10 @@ def gpu():
     import cleisthenes_amd as ca
     assert ca.device_count() > 0, "gpu test run without a visible GPU"
     return ca
+
+
+def pytest_sessionfinish(session, exitstatus):
+    """A GPU session must have run on the ROCm runtime librbc_gpu.so links:
+    torch (if something imported it) maps its own libamdhip64 / librccl."""
+    if "torch" in sys.modules and session.config.getoption("-m") == "gpu":
+        print("\nWARNING: torch was imported in a GPU test session")

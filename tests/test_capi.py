@@ -22,7 +22,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_version_and_strerror():
     from cleisthenes_amd import _lib
-    assert _lib.lib.rbc_abi_version() == 1
+    assert _lib.lib.rbc_abi_version() == 2
     assert _lib.lib.rbc_strerror(-3) == b"too few shards given"
     assert _lib.lib.rbc_strerror(-8).startswith(b"interpolated merkle root")
     assert _lib.lib.rbc_strerror(12345) == b"unknown rbc status"
@@ -52,10 +52,12 @@ def test_acs_partition_covers_all_instances():
                 first, cnt = acs.partition(total, world, r)
                 seen.extend(range(first, first + cnt))
             assert seen == list(range(total))
-            assert acs.max_share(total, world) - min(acs.partition(total, world, r)[1] for r in range(world)) <= 1
+            assert acs.max_share(total, world) == max(acs.partition(total, world, r)[1] for r in range(world))
     g = np.zeros((2, 3, 64), dtype=np.uint8)
     g[0, :2, 0] = [1, 2]
     g[1, :3, 0] = [3, 4, 5]
-    out = acs.assemble_output_set(g, 5, 2, status=[0, 0, 0, -8, 0])
+    g[0, :2, 32] = 1
+    g[1, [0, 2], 40] = 9  # instance 3 (rank 1, slot 1) failed: zero digest
+    out = acs.assemble_output_set(g, 5, 2)
     assert [o["instance"] for o in out] == [0, 1, 2, 4]
     assert [o["root"][0] for o in out] == [1, 2, 3, 5]

@@ -7,8 +7,9 @@ the HBBFT reliable-broadcast properties (docs/RBC-EN.md): every honest node
 delivers the proposer's value with f silent or lying nodes; nothing is
 delivered for a proposal that is not a codeword; an equivocating proposer
 cannot make honest nodes deliver different values.  Delivered values are
-checked against the proposer's input (zero-padded to k*S: interpolate does
-not carry the length, rbc/rbc.go:86-90).
+checked byte-for-byte against the proposer's input: the node frames the
+value with its length before Split (interpolate alone returns k*S bytes with
+the zero pad, rbc/rbc.go:86-90).
 """
 import numpy as np
 import pytest
@@ -71,16 +72,11 @@ def ca(gpu):
     return gpu
 
 
-def padded(v, k):
-    S = (len(v) + k - 1) // k
-    return v + bytes(k * S - len(v))
-
-
 def rand(n, seed):
     return np.random.default_rng(seed).integers(0, 256, n, dtype=np.uint8).tobytes()
 
 
-@pytest.mark.parametrize("n,f,B", [(4, 1, 1000), (7, 2, 333), (16, 5, 65536)])
+@pytest.mark.parametrize("n,f,B", [(4, 1, 1000), (7, 2, 333), (16, 5, 65536), (4, 1, 0), (4, 1, 1)])
 def test_honest_network_delivers(ca, n, f, B):
     net = Net(ca, n, f, proposers=[0])
     try:
@@ -90,7 +86,7 @@ def test_honest_network_delivers(ca, n, f, B):
         k = n - 2 * f
         for i in range(n):
             nd = net.nodes[(0, i)]
-            assert nd.value() == padded(v, k), i
+            assert nd.value() == v, i
             st = nd.stats()
             assert st["ready_sent"] and st["echoes"] == n and st["readies"] == n and st["rejected"] == 0
         assert net.rejected_at_handle == 0
@@ -108,7 +104,7 @@ def test_all_proposers_concurrently_share_launches(ca):
             net.nodes[(p, p)].propose(vals[p])
         net.run()
         for (p, i), nd in net.nodes.items():
-            assert nd.value() == padded(vals[p], n - 2 * f), (p, i)
+            assert nd.value() == vals[p], (p, i)
         batches, requests = net.bt.stats()
         # 16 shards + 16*15 VAL + 16*16*15 ECHO validations + >= 256 interpolations
         assert requests >= 16 + 240 + 3840 + 256
@@ -150,7 +146,7 @@ def test_f_byzantine_nodes_cannot_block_or_forge(ca, mode):
             if i in byz:
                 continue
             nd = net.nodes[(0, i)]
-            assert nd.value() == padded(v, n - 2 * f), (mode, i)
+            assert nd.value() == v, (mode, i)
             st = nd.stats()
             if mode == "bad_echo":
                 assert st["rejected"] == len(byz)  # each lying ECHO failed validateMessage
@@ -172,8 +168,8 @@ def test_equivocating_proposer_cannot_split_honest_nodes(ca):
     try:
         pr = net.protocol
         va, vb = rand(3000, 11), rand(3000, 12)
-        ra, ba, sa = _vals_for(net.ctx, va)
-        rb, bb, sb = _vals_for(net.ctx, vb)
+        ra, ba, sa = _vals_for(net.ctx, pr.frame(va))
+        rb, bb, sb = _vals_for(net.ctx, pr.frame(vb))
         for j in range(n - 1):
             root, br, sh = (ra, ba, sa) if j < n - f else (rb, bb, sb)
             rc = net.nodes[(P, j)].handle_message(P, pr.pb_encode(pr.VAL, pr.json_encode_val(root, br[j],
@@ -181,7 +177,7 @@ def test_equivocating_proposer_cannot_split_honest_nodes(ca):
             assert rc == 0
         net.run()
         got = {net.nodes[(P, j)].value() for j in range(n - 1)}
-        assert got == {padded(va, n - 2 * f)}
+        assert got == {va}
     finally:
         net.close()
 
@@ -233,5 +229,28 @@ def test_out_of_protocol_messages_are_dropped(ca):
         assert st["echoes"] == 2 and st["rejected"] == 5  # own ECHO + node 2's
         with pytest.raises(Exception):
             net.nodes[(0, 2)].propose(b"x")             # only the proposer proposes
+    finally:
+        net.close()
+
+
+def test_badly_framed_proposal_is_agreed_but_unusable(ca):
+    """A Byzantine proposer commits (consistently) to a payload whose length
+    frame exceeds the decoded bytes: every honest node still delivers (RBC
+    agreement holds) and every one reports the same protocol error."""
+    n, f = 4, 1
+    P = 0
+    net = Net(ca, n, f, proposers=[P])
+    try:
+        pr = net.protocol
+        bad = (10 ** 9).to_bytes(8, "little") + rand(500, 31)  # claims 1e9 bytes
+        r, br, sh = _vals_for(net.ctx, bad)
+        for j in range(1, n):
+            net.nodes[(P, j)].handle_message(P, pr.pb_encode(pr.VAL, pr.json_encode_val(r, br[j], bytes(sh[j]))))
+        net.run()
+        for j in range(1, n):
+            with pytest.raises(Exception) as ei:
+                net.nodes[(P, j)].value()
+            assert getattr(ei.value, "code", None) == -20
+            assert net.nodes[(P, j)].stats()["ready_sent"]
     finally:
         net.close()

@@ -149,6 +149,11 @@ def test_json_decode_follows_encoding_json_rules():
     # a later duplicate key wins, as in encoding/json
     js2 = ('{"RootHash":"%s","Block":["AA=="],"Block":["%s"]}' % (r64, blk)).encode()
     assert protocol.json_decode_val(js2)["Block"] == [b"shard"]
+    # base64.StdEncoding is not Strict(): non-zero trailing bits of the last
+    # quantum are ignored ("AB==" -> 0x00, "AAB=" -> 0x00 0x00), as Go decodes them
+    for b64, want in (("AB==", b"\x00"), ("AAB=", b"\x00\x00"), ("/w==", b"\xff"), ("//8=", b"\xff\xff")):
+        js3 = ('{"RootHash":"%s","Block":["%s"]}' % (r64, b64)).encode()
+        assert protocol.json_decode_val(js3)["Block"] == [want], b64
 
 
 @pytest.mark.parametrize("js", [
@@ -156,7 +161,6 @@ def test_json_decode_follows_encoding_json_rules():
     b'[]',
     b'{"RootHash":"AAAA"}',                                  # root not 32 bytes
     b'{"RootHash":"%s","Block":["AA="]}',                    # bad padding
-    b'{"RootHash":"%s","Block":["AB=="]}',                   # non-zero trailing bits
     b'{"RootHash":"%s","Block":["A-=="]}',                   # URL alphabet
     b'{"RootHash":"%s","Block":[]}',                         # no shard
     b'{"RootHash":"%s","Block":["AA==","AA=="]}',            # two shards
@@ -192,4 +196,9 @@ def test_node_create_rejects_bad_arguments_without_gpu():
     import ctypes
     p = ctypes.c_void_p()
     assert _lib.lib.rbc_node_create(None, 4, 1, 0, 0, ctypes.byref(p)) == _lib.RBC_ERR_INVALID_ARG
+    # n < 3f + 1 breaks HBBFT quorum intersection: rejected before the batcher
+    # is touched (a dummy non-NULL handle is never dereferenced on this path)
+    dummy = ctypes.c_void_p(1)
+    for n, f in ((5, 2), (3, 1), (6, 2), (8, 3), (255, 85)):
+        assert _lib.lib.rbc_node_create(dummy, n, f, 0, 0, ctypes.byref(p)) == _lib.RBC_ERR_INVALID_ARG, (n, f)
     assert _lib.lib.rbc_strerror(_lib.RBC_ERR_PROTOCOL).startswith(b"malformed")
