@@ -96,6 +96,7 @@ _SIGS = {
     "rbc_rs_reconstruct_data": (c_int, [c_void_p, c_void_p, szp, c_int]),
     "rbc_rs_split": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, szp]),
     "rbc_rs_join": (c_int, [c_void_p, c_void_p, szp, c_int, c_size_t, c_void_p]),
+    "rbc_rs_update": (c_int, [c_void_p, c_void_p, szp, c_int, c_void_p, szp, c_int]),
     "rbc_comm_unique_id": (c_int, [c_void_p]),
     "rbc_comm_init": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "rbc_comm_destroy": (c_int, [c_void_p]),
@@ -166,6 +167,7 @@ RBC_ERR_DEVICE = -9
 RBC_ERR_INVALID_ARG = -10
 RBC_ERR_SINGULAR = -11
 RBC_ERR_NO_COMM = -12
+RBC_ERR_INVALID_INPUT = -13
 RBC_ERR_PROTOCOL = -20  # include/rbc_protocol.h
 
 # pb.RBC type (pb/message.proto:30-34)

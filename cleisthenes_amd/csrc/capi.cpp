@@ -723,6 +723,7 @@ const char *rbc_strerror(int s) {
         case RBC_ERR_INVALID_ARG: return "invalid argument";
         case RBC_ERR_SINGULAR: return "matrix is singular";
         case RBC_ERR_NO_COMM: return "multi-GPU communicator not initialised";
+        case RBC_ERR_INVALID_INPUT: return "invalid input";
         case -20: return "malformed or out-of-protocol RBC message"; /* RBC_ERR_PROTOCOL */
         default: return "unknown rbc status";
     }
@@ -1385,6 +1386,9 @@ int rbc_validate_message(rbc_ctx *c, const uint8_t *root, const uint8_t *branch,
     return RBC_OK;
 }
 
+// Single-call interpolate: each present shard is copied once, from the
+// caller's pointer straight into the slot's pinned staging row (no
+// intermediate buffer), and the value comes back through pinned memory.
 int rbc_interpolate(rbc_ctx *c, const uint8_t *root, const uint8_t *const *shards, const size_t *lens,
                     uint8_t *value_out, size_t value_cap, size_t *value_len, uint8_t *digest_out) {
     if (!c || !root || !shards || !lens || !value_out) return RBC_ERR_INVALID_ARG;
@@ -1392,22 +1396,68 @@ int rbc_interpolate(rbc_ctx *c, const uint8_t *root, const uint8_t *const *shard
     int rc = check_shards(lens, c->n, true, &S);
     if (rc) return rc;
     int present = 0;
-    for (int i = 0; i < c->n; ++i) present += lens[i] != 0;
+    for (int i = 0; i < c->n; ++i) {
+        present += lens[i] != 0;
+        if (lens[i] && !shards[i]) return RBC_ERR_INVALID_ARG;
+    }
     if (present < c->k) return RBC_ERR_TOO_FEW_SHARDS;  // rbc/rbc.go:87
     if (value_cap < (size_t)c->k * S) return RBC_ERR_INVALID_ARG;
-    std::vector<uint8_t> buf((size_t)c->n * S, 0), pres(c->n, 0);
-    for (int i = 0; i < c->n; ++i)
-        if (lens[i]) {
-            if (!shards[i]) return RBC_ERR_INVALID_ARG;
-            memcpy(buf.data() + (size_t)i * S, shards[i], S);
-            pres[i] = 1;
+    const int n = c->n, k = c->k;
+    const size_t dpitch = round_up(S, 128), vpitch = round_up((size_t)k * S, 16);
+    if ((size_t)n * dpitch > 0x7fffffffULL || vpitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    RBC_HIP(hipSetDevice(c->device));
+    Slot *sp = acquire_slot(c);
+    if (!sp) return RBC_ERR_DEVICE;
+    Slot &s = *sp;
+    hipStream_t st = s.stream;
+    const size_t sh_bytes = (size_t)n * dpitch;
+    RBC_HIP(s.d_shards.ensure(sh_bytes));
+    const size_t npad = round_up((size_t)n, 64);  // root after the present flags, 64-B aligned
+    RBC_HIP(s.d_valid.ensure(npad + 32));
+    RBC_HIP(s.d_leaves.ensure((size_t)n * 32));
+    RBC_HIP(s.d_values.ensure(vpitch));
+    RBC_HIP(s.d_digests.ensure(32));
+    RBC_HIP(s.d_status.ensure(4));
+    RBC_HIP(s.h_in.ensure(sh_bytes + npad + 32));
+    RBC_HIP(s.h_out.ensure(vpitch + 32 + 4));
+    uint8_t *i_sh = s.h_in.as<uint8_t>(), *i_pr = i_sh + sh_bytes, *i_rt = i_pr + npad;
+    memset(i_pr, 0, npad);
+    for (int j = 0; j < n; ++j) {
+        uint8_t *dst = i_sh + (size_t)j * dpitch;
+        if (lens[j]) {
+            memcpy(dst, shards[j], S);
+            memset(dst + S, 0, dpitch - S);
+        } else {
+            memset(dst, 0, dpitch);
         }
+        i_pr[j] = lens[j] ? 1 : 0;
+    }
+    memcpy(i_rt, root, 32);
+    RBC_HIP(hipMemcpyAsync(s.d_shards.p, i_sh, sh_bytes, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(s.d_valid.p, i_pr, npad + 32, hipMemcpyHostToDevice, st));  // present + root
+    const uint8_t *d_root = s.d_valid.as<uint8_t>() + npad;
+    rc = stage_interpolate(c, s.ws, st, 1, s.d_shards.as<uint8_t>(), (uint32_t)dpitch, nullptr, (uint32_t)S,
+                           s.d_valid.as<uint8_t>(), s.d_leaves.as<uint8_t>(), 0, d_root, s.d_values.as<uint8_t>(),
+                           (uint32_t)vpitch, s.d_digests.as<uint8_t>(), s.d_status.as<int32_t>());
+    if (rc) return rc;
+    uint8_t *o_val = s.h_out.as<uint8_t>(), *o_dig = o_val + vpitch;
+    int32_t *o_st = reinterpret_cast<int32_t *>(o_dig + 32);
+    RBC_HIP(hipMemcpyAsync(o_val, s.d_values.p, vpitch, hipMemcpyDeviceToHost, st));
+    RBC_HIP(hipMemcpyAsync(o_dig, s.d_digests.p, 32, hipMemcpyDeviceToHost, st));
+    RBC_HIP(hipMemcpyAsync(o_st, s.d_status.p, 4, hipMemcpyDeviceToHost, st));
     int32_t status = 0;
-    rc = rbc_interpolate_batch(c, 1, buf.data(), S, &S, pres.data(), root, value_out, value_cap, digest_out, &status,
-                               nullptr);
+    rc = submit(c, s, nullptr, [&]() {
+        status = *o_st;
+        if (!status) {
+            memcpy(value_out, o_val, (size_t)k * S);
+            if (digest_out) memcpy(digest_out, o_dig, 32);
+        }
+        return RBC_OK;
+    });
     if (rc) return rc;
     if (status) return status;
-    if (value_len) *value_len = (size_t)c->k * S;
+    if (value_len) *value_len = (size_t)k * S;
     return RBC_OK;
 }
 
@@ -1494,6 +1544,92 @@ int rbc_rs_verify(rbc_rs *rs, const uint8_t *const *shards, const size_t *lens, 
     int good = 1;
     for (int r = 0; r < c->p && good; ++r) good = memcmp(shards[c->k + r], parity.data() + (size_t)r * S, S) == 0;
     *ok = good;
+    return RBC_OK;
+}
+
+// klauspost v1.9.1 Update / updateParityShards (reedsolomon.go): for every
+// changed data shard c (new_lens[c] != 0), delta = old ^ new is left in
+// shards[c] (Go's sliceXor(in, oldin) writes into oldin) and every parity
+// shard gains M[k+r][c] * delta.  The GF(2^8) product runs on the GPU
+// (gf_rows, one launch for all changed shards); the xors are host memory ops.
+int rbc_rs_update(rbc_rs *rs, uint8_t *const *shards, const size_t *lens, int n_shards,
+                  const uint8_t *const *new_data, const size_t *new_lens, int n_new) {
+    if (!rs || !shards || !lens || !new_data || !new_lens) return RBC_ERR_INVALID_ARG;
+    rbc_ctx *c = rs->ctx;
+    if (n_shards < c->n) return RBC_ERR_TOO_FEW_SHARDS;
+    if (n_new < c->k) return RBC_ERR_TOO_FEW_SHARDS;
+    size_t S = 0, S2 = 0;
+    int rc = check_shards(lens, n_shards, true, &S);
+    if (rc) return rc;
+    rc = check_shards(new_lens, n_new, true, &S2);
+    if (rc) return rc;
+    for (int i = 0; i < n_new; ++i)
+        if (new_lens[i] && (i >= n_shards || !lens[i])) return RBC_ERR_INVALID_INPUT;
+    for (int r = c->k; r < c->n; ++r)
+        if (!lens[r]) return RBC_ERR_INVALID_INPUT;
+    std::vector<int> changed;
+    for (int j = 0; j < c->k; ++j)
+        if (new_lens[j]) changed.push_back(j);
+    if (changed.empty() || c->p == 0) return RBC_OK;
+    if (S2 != S) return RBC_ERR_SHARD_SIZE;  // Go would index past the shorter slice
+    for (int j : changed)
+        if (!shards[j] || !new_data[j]) return RBC_ERR_INVALID_ARG;
+    for (int r = c->k; r < c->n; ++r)
+        if (!shards[r]) return RBC_ERR_INVALID_ARG;
+    const int K = (int)changed.size(), P = c->p;
+    const size_t pitch = round_up(S, kAlign);
+    if ((size_t)(K + P) * pitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
+    // delta rows (host xor, written back into the caller's old data shards)
+    for (int j : changed)
+        for (size_t x = 0; x < S; ++x) shards[j][x] ^= new_data[j][x];
+    std::lock_guard<std::mutex> lk(c->mu);
+    RBC_HIP(hipSetDevice(c->device));
+    hipStream_t st = host_stream(c);
+    if (!st) return RBC_ERR_DEVICE;
+    const size_t rows_bytes = (size_t)(K + P) * pitch, meta = (size_t)P * K + 512;
+    RBC_HIP(c->h_stage.ensure(rows_bytes + meta));
+    RBC_HIP(c->d_shards.ensure(rows_bytes));
+    RBC_HIP(c->d_values.ensure(meta));
+    uint8_t *stage = c->h_stage.as<uint8_t>();
+    memset(stage, 0, (size_t)K * pitch);
+    for (int t = 0; t < K; ++t) memcpy(stage + (size_t)t * pitch, shards[changed[t]], S);
+    uint8_t *coef = stage + rows_bytes, *in_idx = coef + (size_t)P * K, *out_idx = in_idx + 256;
+    for (int r = 0; r < P; ++r)
+        for (int t = 0; t < K; ++t) coef[(size_t)r * K + t] = c->h_M[(size_t)(c->k + r) * c->k + changed[t]];
+    for (int t = 0; t < K; ++t) in_idx[t] = (uint8_t)t;
+    for (int r = 0; r < P; ++r) out_idx[r] = (uint8_t)(K + r);
+    RBC_HIP(hipMemcpyAsync(c->d_shards.p, stage, (size_t)K * pitch, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(c->d_values.p, coef, meta, hipMemcpyHostToDevice, st));
+    const uint8_t *d_coef = c->d_values.as<uint8_t>();
+    GfArgs g{};
+    g.count = 1;
+    g.tiles = (int)((pitch + 4095) / 4096);
+    g.R = P;
+    g.K = K;
+    g.rc = rbc_gf_pick_rc(P, gf_rcmax());
+    g.mode = GF_MODE_DECODE;
+    g.in = c->d_shards.as<uint8_t>();
+    g.in_inst_pitch = rows_bytes;
+    g.in_row_pitch = (uint32_t)pitch;
+    g.in_inst_bytes = (uint32_t)rows_bytes;
+    g.out = c->d_shards.as<uint8_t>();
+    g.out_inst_pitch = rows_bytes;
+    g.out_row_pitch = (uint32_t)pitch;
+    g.uniform_len = (uint32_t)S;
+    g.coef = d_coef;
+    g.in_idx = d_coef + (size_t)P * K;
+    g.out_idx = g.in_idx + 256;
+    g.idx_stride = (uint32_t)K;
+    g.idx_stride2 = (uint32_t)P;
+    RBC_HIP(rbc_launch_gf_rows(g, st));
+    RBC_HIP(hipMemcpy2DAsync(stage, S, c->d_shards.as<uint8_t>() + (size_t)K * pitch, pitch, S, P,
+                             hipMemcpyDeviceToHost, st));
+    RBC_HIP(hipStreamSynchronize(st));
+    for (int r = 0; r < P; ++r) {
+        uint8_t *dst = shards[c->k + r];
+        const uint8_t *d = stage + (size_t)r * S;
+        for (size_t x = 0; x < S; ++x) dst[x] ^= d[x];
+    }
     return RBC_OK;
 }
 

@@ -488,6 +488,22 @@ class Encoder:
             if lens[i]:
                 shards[i] = bufs[i][: lens[i]].copy()
 
+    def update(self, shards: List, new_data: List) -> None:
+        """Update(shards, newDatashards): parity shards in `shards` are updated
+        for the changed data shards (None / empty = unchanged); as in Go, each
+        changed old data shard is left holding old ^ new."""
+        arrs = [None if s is None else _bytes_array(s).copy() for s in shards]
+        news = [None if s is None else _bytes_array(s) for s in new_data]
+        n, m = len(arrs), len(news)
+        lens = (c_size_t * n)(*[0 if a is None else len(a) for a in arrs])
+        ptrs = (c_void_p * n)(*[(a.ctypes.data if (a is not None and len(a)) else None) for a in arrs])
+        nlens = (c_size_t * m)(*[0 if a is None else len(a) for a in news])
+        nptrs = (c_void_p * m)(*[(a.ctypes.data if (a is not None and len(a)) else None) for a in news])
+        check(lib.rbc_rs_update(self._p, ptrs, lens, n, nptrs, nlens, m), "Update")
+        for i in range(n):
+            if arrs[i] is not None:
+                shards[i] = arrs[i]
+
     def reconstruct(self, shards: List) -> None:
         self._reconstruct(shards, False)
 

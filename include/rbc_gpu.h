@@ -14,7 +14,7 @@
  *                                                             -> rbc_shard_commit / rbc_dev_merkle_build
  *   rbc/rbc.go:20      enc reedsolomon.Encoder (klauspost v1.9.1, go.mod:10)
  *                                                             -> rbc_rs_* (New/Split/Encode/Verify/
- *                                                                Reconstruct/ReconstructData/Join)
+ *                                                                Reconstruct/ReconstructData/Update/Join)
  *   (BASELINE north_star (5)) ACS output assembly over xGMI  -> rbc_comm_* + rbc_dev_allgather_roots
  *
  * Plain pointers and sizes only.  All functions return an int status
@@ -60,6 +60,7 @@ extern "C" {
 #define RBC_ERR_INVALID_ARG (-10)
 #define RBC_ERR_SINGULAR (-11)            /* internal: singular sub-matrix      */
 #define RBC_ERR_NO_COMM (-12)             /* multi-GPU call before rbc_comm_init */
+#define RBC_ERR_INVALID_INPUT (-13)       /* reedsolomon.ErrInvalidInput (Update) */
 
 const char *rbc_strerror(int status);
 int rbc_abi_version(void);
@@ -232,6 +233,14 @@ int rbc_rs_reconstruct(rbc_rs *rs, uint8_t *const *shards, size_t *lens, int n_s
 int rbc_rs_reconstruct_data(rbc_rs *rs, uint8_t *const *shards, size_t *lens, int n_shards);
 /* Split: out receives n*per bytes (shard i at i*per); *per_shard = per. */
 int rbc_rs_split(rbc_rs *rs, const uint8_t *data, size_t len, uint8_t *out, size_t out_cap, size_t *per_shard);
+/* Update(shards, newDatashards): parity shards += M[k+r][c] * (old_c ^ new_c)
+ * for every changed data shard c (new_lens[c] != 0, first k entries used;
+ * n_new >= k).  As in Go, shards[c] is left holding old_c ^ new_c.  Errors in
+ * Go's order: ErrTooFewShards (n_shards < k+p or n_new < k), checkShards on
+ * both sets, ErrInvalidInput (a changed shard whose old shard is nil, or a
+ * nil parity shard); a new shard of another size is ErrShardSize. */
+int rbc_rs_update(rbc_rs *rs, uint8_t *const *shards, const size_t *lens, int n_shards,
+                  const uint8_t *const *new_data, const size_t *new_lens, int n_new);
 /* Join: first k shards, out_size bytes; a NULL shard pointer is Go `nil`. */
 int rbc_rs_join(rbc_rs *rs, const uint8_t *const *shards, const size_t *lens, int n_shards, size_t out_size,
                 uint8_t *dst);

@@ -103,6 +103,10 @@ class ErrSingular(RSError):
     code = -11
 
 
+class ErrInvalidInput(RSError):
+    code = -13
+
+
 # ----------------------------------------------------------------------------
 # GF(2^8), generating polynomial x^8+x^4+x^3+x^2+1 (0x11D), generator 2.
 # klauspost galois.go: logTable/expTable, galMultiply, galDivide, galExp.
@@ -353,6 +357,38 @@ class Encoder:
             for i, o in zip(missing_par, outs):
                 shards[i] = o
         assert all(len(s) == size for s in shards)
+
+    # Update (reedsolomon.go Update / updateParityShards, v1.9.1): parity +=
+    # M[k+r][c] * (old_c ^ new_c) for every changed data shard c (new_c non-nil).
+    # As in Go, the old data shard in `shards` is left holding old ^ new
+    # (sliceXor(in, oldin) writes into oldin).
+    def update(self, shards, new_data) -> None:
+        if len(shards) < self.shards:
+            raise ErrTooFewShards("too few shards given")
+        if len(new_data) < self.data_shards:
+            raise ErrTooFewShards("too few shards given")
+        _check_shards(shards, True)
+        _check_shards(new_data, True)
+        for i in range(len(new_data)):
+            if new_data[i] is not None and len(new_data[i]) and (
+                    i >= len(shards) or shards[i] is None or len(shards[i]) == 0):
+                raise ErrInvalidInput("invalid input")
+        for pi in range(self.data_shards, self.shards):
+            if shards[pi] is None or len(shards[pi]) == 0:
+                raise ErrInvalidInput("invalid input")
+        size = _shard_size(shards)
+        for c in range(self.data_shards):
+            nd = new_data[c]
+            if nd is None or len(nd) == 0:
+                continue
+            nd = _as_u8(nd)
+            if len(nd) != size:  # Go would index past a shorter shard; reported as a size mismatch
+                raise ErrShardSize("shard sizes do not match")
+            delta = _as_u8(shards[c]) ^ nd
+            shards[c] = delta
+            for r in range(self.parity_shards):
+                (outs,) = gf_rows(self.parity[r:r + 1, c:c + 1], [delta])
+                shards[self.data_shards + r] = _as_u8(shards[self.data_shards + r]) ^ outs
 
     def reconstruct(self, shards) -> None:
         self._reconstruct(shards, False)

@@ -51,6 +51,42 @@ static void TestOneEncode() {
     rbc_rs_free(rs);
 }
 
+// klauspost v1.9.1 Update: parity of the changed data equals a fresh Encode
+// of the new data; the old data shard is left holding old ^ new (Go).
+static void TestUpdate() {
+    const int k = 10, p = 4, n = k + p;
+    const size_t S = 513;
+    rbc_rs *rs = nullptr;
+    CHECK(rbc_rs_new(k, p, 0, &rs) == RBC_OK);
+    std::vector<std::vector<uint8_t>> sh(n), fresh(n);
+    for (int i = 0; i < n; ++i) sh[i] = i < k ? random_bytes(S, 100 + i) : std::vector<uint8_t>(S, 0);
+    std::vector<uint8_t *> ptr(n);
+    std::vector<size_t> lens(n, S);
+    for (int i = 0; i < n; ++i) ptr[i] = sh[i].data();
+    CHECK(rbc_rs_encode(rs, ptr.data(), lens.data(), n) == RBC_OK);
+    std::vector<std::vector<uint8_t>> nd(k);
+    std::vector<const uint8_t *> nptr(k, nullptr);
+    std::vector<size_t> nlens(k, 0);
+    for (int c : {2, 7}) {
+        nd[c] = random_bytes(S, 900 + c);
+        nptr[c] = nd[c].data();
+        nlens[c] = S;
+    }
+    const auto old2 = sh[2];
+    CHECK(rbc_rs_update(rs, ptr.data(), lens.data(), n, nptr.data(), nlens.data(), k) == RBC_OK);
+    for (size_t x = 0; x < S; ++x) CHECK(sh[2][x] == (uint8_t)(old2[x] ^ nd[2][x]));
+    std::vector<uint8_t *> fptr(n);
+    for (int i = 0; i < n; ++i) {
+        fresh[i] = i < k ? (nlens[i] ? nd[i] : sh[i]) : std::vector<uint8_t>(S, 0);
+        fptr[i] = fresh[i].data();
+    }
+    CHECK(rbc_rs_encode(rs, fptr.data(), lens.data(), n) == RBC_OK);
+    for (int r = k; r < n; ++r) CHECK(fresh[r] == sh[r]);
+    lens[k] = 0;  // a nil parity shard
+    CHECK(rbc_rs_update(rs, ptr.data(), lens.data(), n, nptr.data(), nlens.data(), k) == RBC_ERR_INVALID_INPUT);
+    rbc_rs_free(rs);
+}
+
 // Reconstruct / ReconstructData restore exactly what Encode produced and never
 // touch present shards; too few shards is ErrTooFewShards.
 static void TestReconstruct() {
@@ -273,6 +309,7 @@ int main() {
         {"TestOneEncode", TestOneEncode},   {"TestReconstruct", TestReconstruct},
         {"Test_shard", Test_shard},         {"Test_validateMessage", Test_validateMessage},
         {"Test_interpolate", Test_interpolate}, {"TestBatcherConcurrent", TestBatcherConcurrent},
+        {"TestUpdate", TestUpdate},
     };
     for (auto &t : tests) {
         const int before = failures;

@@ -307,3 +307,48 @@ def test_lagrange_decode_matrix_equals_klauspost_inverse(n, k):
                 got[r, ui] = o.gal_div(num, den)
         assert np.array_equal(got, want)
         done += 1
+
+
+# ---- Update (klauspost v1.9.1 reedsolomon.go Update / updateParityShards)
+def test_oracle_update_equals_encode_of_new_data():
+    rng = np.random.default_rng(41)
+    for k, p, S in ((5, 3, 17), (44, 84, 301), (1, 1, 8), (10, 0, 5)):
+        enc = orc.Encoder(k, p)
+        data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)]
+        shards = [d.copy() for d in data] + [np.zeros(S, np.uint8) for _ in range(p)]
+        enc.encode(shards)
+        new = [None] * k
+        for c in rng.choice(k, size=max(1, k // 3), replace=False):
+            new[c] = rng.integers(0, 256, S, dtype=np.uint8)
+        olds = [s.copy() for s in shards]
+        if p == 0:
+            enc.update(shards, new)
+            continue
+        enc.update(shards, new)
+        want = [(new[c] if new[c] is not None else data[c]).copy() for c in range(k)] + \
+               [np.zeros(S, np.uint8) for _ in range(p)]
+        enc.encode(want)
+        for r in range(p):
+            assert np.array_equal(shards[k + r], want[k + r]), (k, p, r)
+        for c in range(k):  # Go's sliceXor leaves old ^ new in the changed old data shard
+            exp = olds[c] ^ new[c] if new[c] is not None else olds[c]
+            assert np.array_equal(shards[c], exp)
+
+
+def test_oracle_update_argument_checks():
+    enc = orc.Encoder(3, 2)
+    S = 4
+    sh = [np.ones(S, np.uint8) for _ in range(5)]
+    new = [np.zeros(S, np.uint8), None, None]
+    with pytest.raises(orc.ErrTooFewShards):
+        enc.update(sh[:4], new)
+    with pytest.raises(orc.ErrTooFewShards):
+        enc.update(sh, new[:2])
+    with pytest.raises(orc.ErrShardNoData):
+        enc.update(sh, [None, None, None])
+    with pytest.raises(orc.ErrShardSize):
+        enc.update(sh, [np.zeros(S, np.uint8), np.zeros(S + 1, np.uint8), None])
+    with pytest.raises(orc.ErrInvalidInput):  # changed shard whose old shard is nil
+        enc.update([None] + sh[1:], new)
+    with pytest.raises(orc.ErrInvalidInput):  # nil parity shard
+        enc.update(sh[:4] + [None], new)
