@@ -92,6 +92,8 @@ def parse_args(argv):
                     help="shard row pitch alignment in bytes (multiple of 64; the C ABI needs 64)")
     ap.add_argument("--force-gather", action="store_true",
                     help="run the RCCL all-gather even with one rank (exercises rbc_comm_*)")
+    ap.add_argument("--no-pcie", action="store_true",
+                    help="skip the PCIe-inclusive host-path measurement (a secondary key, never `value`)")
     ap.add_argument("--oracle-samples", type=int, default=16,
                     help="instances whose root and digest are checked against the C oracle after timing")
     return ap.parse_args(argv)
@@ -100,7 +102,11 @@ def parse_args(argv):
 # --------------------------------------------------------------------------
 # launch: self-spawn of N ranks (no GPU is touched in the parent)
 # --------------------------------------------------------------------------
-def spawn_ranks(n, argv):
+def spawn_ranks(n, argv, script=None):
+    """Start ranks 0..n-1 of `script` (this file) with the torch.distributed.run
+    environment; return the first non-zero exit status (the other ranks are
+    then terminated: they would wait at the rendezvous), else 0."""
+    script = script or os.path.abspath(__file__)
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -110,7 +116,7 @@ def spawn_ranks(n, argv):
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RBC_RDZV_KEY=key)
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env))
     rc = 0
     live = list(procs)
     while live:
@@ -194,18 +200,18 @@ def main(argv):
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(args.gpus, argv)
 
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world != args.gpus:
+        raise SystemExit(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}")
+
     # ONE JSON line on stdout: keep a private handle on the real stdout and
     # point fd 1 at stderr, so banners that native libraries print with
     # printf (RCCL's version block) cannot precede it
     out = os.fdopen(os.dup(1), "w")
     sys.stdout.flush()
     os.dup2(2, 1)
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
-    if world != args.gpus:
-        raise SystemExit(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}")
 
     from cleisthenes_amd.rendezvous import Rendezvous
     rdz = Rendezvous(world, rank)
@@ -459,6 +465,15 @@ def main(argv):
             phases[ph]["cpu_gbs"] = cpu["phases"][ph]
             phases[ph]["gpu_over_cpu"] = round(phases[ph]["gpu_gbs"] / cpu["phases"][ph], 1)
 
+    pcie = None
+    if rank == 0 and world == 1 and not args.no_pcie:
+        # what a Go batcher sees with host buffers in and out (pinned rings,
+        # two submissions in flight): PCIe-bound, reported beside `value`
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import host_bench
+        pcie = host_bench.measure(ca, n, f, B, batch=64, batches=8, inflight=2, pinned=True, device=dev)
+        pcie["unit"] = "GB/s of committed shard bytes (N*S per instance), host memory in and out"
+
     line = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -489,6 +504,7 @@ def main(argv):
         "roofline": roof,
         "roofline_encode": codec_roof,
         "cpu_baseline": cpu,
+        "pcie_inclusive": pcie,
         "rccl": rccl,
         "host": {kk: host[kk] for kk in ("cpu_model", "nproc", "cgroup_cpu_quota", "affinity_cpus")},
     }

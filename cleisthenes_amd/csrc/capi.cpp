@@ -111,6 +111,10 @@ struct DevBuf {
 // work: the context's device API has one, every host-API slot has its own.
 struct Ws {
     DevBuf used, regen, dmat, nmiss, flags, list, counter, rcount, cls, vleaves;
+    // fork the join onto an aux stream (device API); host-API slots keep one
+    // stream each (their concurrency comes from the slots themselves, and
+    // the box has GPU_MAX_HW_QUEUES = 4 hardware queues per process)
+    bool fork = true;
     hipStream_t aux = nullptr;  // created on first use
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool init() {
@@ -580,10 +584,15 @@ int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *sha
     // value assembly (HBM-bound) forks onto the aux stream beside the regen
     // hashing (latency-bound, under-fills the SIMDs); it needs only the
     // regenerated rows.  values_out is defined where status == 0.
+    const bool fork = !fused_join && w.fork;
     if (!fused_join) {
-    if (!aux_stream(w)) return RBC_ERR_DEVICE;
-    RBC_HIP(hipEventRecord(w.ev_fork, st));
-    RBC_HIP(hipStreamWaitEvent(w.aux, w.ev_fork, 0));
+    hipStream_t js = st;
+    if (fork) {
+        if (!aux_stream(w)) return RBC_ERR_DEVICE;
+        RBC_HIP(hipEventRecord(w.ev_fork, st));
+        RBC_HIP(hipStreamWaitEvent(w.aux, w.ev_fork, 0));
+        js = w.aux;
+    }
     {
         JoinArgs j{};
         j.count = count;
@@ -598,9 +607,9 @@ int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *sha
         j.values = values_out;
         j.value_pitch = value_pitch;
         j.status = status;
-        RBC_HIP(rbc_launch_join(j, w.aux));
+        RBC_HIP(rbc_launch_join(j, js));
     }
-    RBC_HIP(hipEventRecord(w.ev_join, w.aux));
+    if (fork) RBC_HIP(hipEventRecord(w.ev_join, w.aux));
     }
     const int nr = c->n - c->k;
     ShaArgs a{};
@@ -638,7 +647,7 @@ int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *sha
     RBC_HIP(rbc_launch_merkle(m, true, st));
     if (digests)
         RBC_HIP(rbc_launch_digest(leaves, (uint64_t)c->n * 32, c->k, status, digests, count, st));
-    if (!fused_join) RBC_HIP(hipStreamWaitEvent(st, w.ev_join, 0));  // join back before returning
+    if (fork) RBC_HIP(hipStreamWaitEvent(st, w.ev_join, 0));  // join back before returning
     return RBC_OK;
 }
 
@@ -1010,6 +1019,7 @@ Slot *acquire_slot(rbc_ctx *c) {
             sl->release();
             return nullptr;
         }
+        sl->ws.fork = false;
         c->slots.push_back(std::move(sl));
         return c->slots.back().get();
     }

@@ -24,6 +24,68 @@ sys.path.insert(0, ROOT)
 CFG = {"c1": (64, 21, 1 << 20), "c2": (128, 42, 1 << 20), "c3": (128, 42, 4 << 20), "c4": (256, 85, 64 << 10)}
 
 
+def measure(ca, n, f, B, batch=64, batches=8, inflight=2, pinned=True, device=0):
+    """Host buffers in and out through rbc_shard_commit / rbc_interpolate_batch;
+    returns GB/s of committed shard bytes (N*S per instance) for each side."""
+    ctx = ca.Context(n, f, device=device)
+    k = ctx.k
+    S = (B + k - 1) // k
+    rng = np.random.default_rng(1)
+    pool = [[rng.integers(0, 256, B, dtype=np.uint8) for _ in range(batch)] for _ in range(2)]
+    outsets = [None] * (inflight + 1)
+    if pinned:
+        for p_ in pool:
+            for i, v in enumerate(p_):
+                pv = ca.pinned_empty(B)
+                pv[:] = v
+                p_[i] = pv
+        outsets = [{"shards": ca.pinned_empty((batch, n, S)), "roots": ca.pinned_empty((batch, 32)),
+                    "branches": ca.pinned_empty((batch, n, max(ctx.depth, 1), 32))}
+                   for _ in range(inflight + 1)]
+
+    # shard + commit (proposer side)
+    warm = [ctx.shard_commit_submit(pool[i % 2], out=outsets[i]) for i in range(inflight)]
+    for w in warm:  # warm every slot's buffers
+        w.wait()
+    t0 = time.perf_counter()
+    live, outs = [], []
+    for b in range(batches):
+        live.append(ctx.shard_commit_submit(pool[b % 2], out=outsets[b % len(outsets)]))
+        if len(live) >= inflight:
+            outs.append(live.pop(0).wait())
+    while live:
+        outs.append(live.pop(0).wait())
+    t_enc = time.perf_counter() - t0
+
+    # interpolate (receiver side) from N-f present shards of the last commit
+    sh = outs[-1]["shards"]
+    present = np.zeros((batch, n), np.uint8)
+    for i in range(batch):
+        present[i, rng.permutation(n)[: n - f]] = 1
+    rx = sh * present[:, :, None]
+    vout = None
+    if pinned:
+        prx = ca.pinned_empty(rx.shape)
+        prx[:] = rx
+        rx = prx
+        vout = ca.pinned_empty((batch, ctx.k * S))
+    lens = outs[-1]["shard_lens"]
+    roots = outs[-1]["roots"].copy()
+    ctx.interpolate_batch(rx, lens, present, roots, values_out=vout)  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(batches):
+        res = ctx.interpolate_batch(rx, lens, present, roots, values_out=vout)
+    t_dec = time.perf_counter() - t0
+    assert (res["status"] == 0).all()
+    ctx.close()
+    shard_bytes = batch * n * S * batches
+    return {"shard_commit_GBps": round(shard_bytes / t_enc / 1e9, 2),
+            "interpolate_GBps": round(shard_bytes / t_dec / 1e9, 2),
+            "shard_commit_ms_per_batch": round(t_enc * 1e3 / batches, 3),
+            "interpolate_ms_per_batch": round(t_dec * 1e3 / batches, 3),
+            "batch": batch, "batches": batches, "inflight": inflight, "pinned": pinned}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2", choices=sorted(CFG))
@@ -37,65 +99,12 @@ def main():
     import cleisthenes_amd as ca
 
     n, f, B = CFG[args.config]
-    ctx = ca.Context(n, f)
-    k = ctx.k
-    S = (B + k - 1) // k
-    rng = np.random.default_rng(1)
-    pool = [[rng.integers(0, 256, B, dtype=np.uint8) for _ in range(args.batch)] for _ in range(2)]
-    outsets = [None] * (args.inflight + 1)
-    if args.pinned:
-        for p_ in pool:
-            for i, v in enumerate(p_):
-                pv = ca.pinned_empty(B)
-                pv[:] = v
-                p_[i] = pv
-        outsets = [{"shards": ca.pinned_empty((args.batch, n, S)), "roots": ca.pinned_empty((args.batch, 32)),
-                    "branches": ca.pinned_empty((args.batch, n, max(ctx.depth, 1), 32))}
-                   for _ in range(args.inflight + 1)]
-
-    # shard + commit (proposer side)
-    warm = [ctx.shard_commit_submit(pool[i % 2], out=outsets[i]) for i in range(args.inflight)]
-    for w in warm:  # warm every slot's buffers
-        w.wait()
-    t0 = time.perf_counter()
-    live, outs = [], []
-    for b in range(args.batches):
-        live.append(ctx.shard_commit_submit(pool[b % 2], out=outsets[b % len(outsets)]))
-        if len(live) >= args.inflight:
-            outs.append(live.pop(0).wait())
-    while live:
-        outs.append(live.pop(0).wait())
-    t_enc = time.perf_counter() - t0
-
-    # interpolate (receiver side) from N-f present shards of the last commit
-    sh = outs[-1]["shards"]
-    present = np.zeros((args.batch, n), np.uint8)
-    for i in range(args.batch):
-        present[i, rng.permutation(n)[: n - f]] = 1
-    rx = sh * present[:, :, None]
-    vout = None
-    if args.pinned:
-        prx = ca.pinned_empty(rx.shape)
-        prx[:] = rx
-        rx = prx
-        vout = ca.pinned_empty((args.batch, ctx.k * S))
-    lens = outs[-1]["shard_lens"]
-    roots = outs[-1]["roots"].copy()
-    ctx.interpolate_batch(rx, lens, present, roots, values_out=vout)  # warm-up
-    t0 = time.perf_counter()
-    for _ in range(args.batches):
-        res = ctx.interpolate_batch(rx, lens, present, roots, values_out=vout)
-    t_dec = time.perf_counter() - t0
-    assert (res["status"] == 0).all()
-    shard_bytes = args.batch * n * S * args.batches
+    r = measure(ca, n, f, B, args.batch, args.batches, args.inflight, args.pinned)
     print(json.dumps({
         "metric": "host-path RBC shard GB/s (PCIe-inclusive, host buffers in and out)",
         "config": {"workload": args.config, "n": n, "f": f, "value_bytes": B, "batch": args.batch,
                    "batches": args.batches, "inflight": args.inflight, "pinned": args.pinned},
-        "shard_commit_GBps": round(shard_bytes / t_enc / 1e9, 2),
-        "interpolate_GBps": round(shard_bytes / t_dec / 1e9, 2),
-        "shard_commit_ms_per_batch": round(t_enc * 1e3 / args.batches, 3),
-        "interpolate_ms_per_batch": round(t_dec * 1e3 / args.batches, 3),
+        **{k_: v for k_, v in r.items() if k_.endswith("GBps") or k_.endswith("batch")},
     }))
 
 
