@@ -84,10 +84,9 @@ def parse_args(argv):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-configs", default="c1,c2,c3,c4",
                     help="configs the CPU port is also timed on (the bench config always is)")
-    ap.add_argument("--pipeline", type=int, default=0,
-                    help="1: overlap batch t's commit (proposer stream) with batch t-1's verify + "
-                         "interpolate (receiver stream), two shard buffer sets; 0 (default): one stream, "
-                         "stages in order, so each kernel's event span is its own")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="1 (default): overlap batch t's commit (proposer stream) with batch t-1's verify + "
+                         "interpolate (receiver stream), two shard buffer sets; 0: one stream, stages in order")
     ap.add_argument("--shard-align", type=int, default=128,
                     help="shard row pitch alignment in bytes (multiple of 64; the C ABI needs 64)")
     ap.add_argument("--force-gather", action="store_true",
@@ -285,9 +284,13 @@ def main(argv):
             raise SystemExit(f"bench: RCCL reports {rccl['nranks']} ranks, expected {world}")
 
     stage_names = ("t0", "enc", "leaf", "tree", "fault", "verify", "interp", "gather")
+    # pipelined schedule: P = proposer stream (t0 .. fault), R = receiver
+    # stream (r0 .. gather); a stage's time is its own stream's event span
+    pipe_spans = (("t0", "enc"), ("enc", "leaf"), ("leaf", "tree"), ("tree", "fault"), ("r0", "verify"),
+                  ("verify", "interp"), ("interp", "gather"))
     # one event set per timed step: stage times are read after the closing
     # barrier, so the timed loop never waits on the host between steps
-    ev_sets = [{name: ca.Event() for name in stage_names} for _ in range(max(args.steps, 3))]
+    ev_sets = [{name: ca.Event() for name in stage_names + ("r0",)} for _ in range(max(args.steps, 3))]
 
     def step(ev, sp=None):
         sp = sp or sets[0]
@@ -316,31 +319,49 @@ def main(argv):
     # A set is reused only after R has finished with it (evR), and R starts a
     # batch only after P committed it (evP): K timed steps = K commits + K
     # decodes, all inside the timed region.
-    rstream = ca.Stream(dev) if pipe else None
+    # RBC_BENCH_PRIO (A/B knob): "R" puts the receiver stream (verify +
+    # interpolate, whose regen-hash tail is latency-bound) at high priority,
+    # "P" the proposer stream
+    prio = os.environ.get("RBC_BENCH_PRIO", "")
+    if pipe and prio == "P":
+        stream.sync()  # the input fill ran on the old stream
+        stream = ca.Stream(dev, priority="high")
+    rstream = ca.Stream(dev, priority="high" if prio == "R" else None) if pipe else None
     evP = [ca.Event() for _ in range(nsets)]
     evR = [ca.Event() for _ in range(nsets)]
     for e in evP + evR:
         e.record(stream)  # recorded once, so every wait below is well defined
 
-    def pstep(t):
+    def pstep(t, ev=None):
         P, R = stream, rstream
+        recP = (lambda name: ev[name].record(P)) if ev is not None else (lambda name: None)
+        recR = (lambda name: ev[name].record(R)) if ev is not None else (lambda name: None)
         sp = sets[t % 2]
         P.wait(evR[t % 2])
+        recP("t0")
         ctx.dev_encode(P.ptr, I, d_values, vpitch, None, B, sp["shards"], spitch)
+        recP("enc")
         ctx.dev_leaves(P.ptr, I, sp["shards"], spitch, None, S, sp["leaves"])
+        recP("leaf")
         ctx.dev_merkle_build(P.ptr, I, sp["leaves"], sp["roots"], sp["branches"])
+        recP("tree")
         ctx.dev_inject_faults(P.ptr, I, sp["shards"], spitch, d_corrupt)
+        recP("fault")
         evP[t % 2].record(P)
         if t == 0:
             return
         sr = sets[(t - 1) % 2]
         R.wait(evP[(t - 1) % 2])
+        recR("r0")
         ctx.dev_verify(R.ptr, I, sr["shards"], spitch, None, S, sr["branches"], sr["roots"], d_present, d_valid,
                        d_leaves_r)
+        recR("verify")
         ctx.dev_interpolate(R.ptr, I, sr["shards"], spitch, None, S, d_valid, d_leaves_r, 1, sr["roots"], d_out,
                             opitch, d_digests, d_status)
+        recR("interp")
         if gather:
             ctx.dev_allgather_records(R.ptr, I, slots, sr["roots"], d_digests, d_status, d_gather)
+        recR("gather")
         evR[(t - 1) % 2].record(R)
 
     def barrier():
@@ -364,7 +385,7 @@ def main(argv):
     t0 = time.perf_counter()
     if pipe:
         for t in range(args.warmup, args.warmup + args.steps):
-            pstep(t)
+            pstep(t, ev_sets[t - args.warmup])
     else:
         for t in range(args.steps):
             step(ev_sets[t])
@@ -372,27 +393,15 @@ def main(argv):
     elapsed = time.perf_counter() - t0
     elapsed_max = rdz.max(elapsed)
     last = sets[(args.warmup + args.steps - 2) % 2] if pipe else sets[0]  # the set the last decode read
-    if not pipe:
-        for ev in ev_sets[: args.steps]:
-            for a, b in zip(stage_names[:-1], stage_names[1:]):
-                stage_ms[b] += ev[a].elapsed_ms(ev[b]) / args.steps
+    for ev in ev_sets[: args.steps]:
+        spans = pipe_spans if pipe else zip(stage_names[:-1], stage_names[1:])
+        for a, b in spans:
+            stage_ms[b] += ev[a].elapsed_ms(ev[b]) / args.steps
 
     # ---- correctness of the timed run's last round (outside the timed region)
     checks = check_results(args, ca, acs, synth, rdz, ctx, dev, stream, world, rank, first, I, total, slots, n, f,
                            k, B, S, vpitch, opitch, d_values, d_out, d_status, d_digests, last["roots"],
                            d_gather, d_count, gather)
-
-    if pipe:
-        # per-stage (and roofline) timings from an isolated serial pass: under
-        # the overlap, one kernel's event span includes the other stream's work
-        iso = 3
-        for it in range(iso):
-            ev = ev_sets[it]
-            step(ev)
-            stream.sync()
-            for a, b in zip(stage_names[:-1], stage_names[1:]):
-                stage_ms[b] += ev[a].elapsed_ms(ev[b]) / iso
-        barrier()
 
     ms_per_step = elapsed_max * 1000.0 / args.steps
     shard_bytes_all = total * n * S
@@ -400,13 +409,15 @@ def main(argv):
 
     # ---- roofline of the dominant kernel ---------------------------------
     blocks_per_shard = (S + 9 + 63) // 64
+    R_rows = int(present_h.sum())  # received ECHO shards over this rank's instances
     enc_kernel = "rs_fft_kernel<encode>" if ctx.codec == "fft" else "gf_rows_kernel<encode>"
     kern = {
         # name: (avg ms, algorithmic HBM bytes per launch, sha compressions per launch)
         enc_kernel: (stage_ms["enc"], I * (k * S + n * S), 0),
         "sha_rows_kernel<leaves>": (stage_ms["leaf"], I * (n * S + n * 32), I * n * blocks_per_shard),
-        "sha_rows_kernel<verify>": (stage_ms["verify"], I * (n * S + n * d * 32 + n * 33 + 32 + n),
-                                    I * n * (blocks_per_shard + 2 * d)),
+        # ECHO verify hashes the received shards only (R = N-f per instance)
+        "sha_rows_kernel<verify>": (stage_ms["verify"], R_rows * (S + d * 32 + 32) + I * (32 + 2 * n),
+                                    R_rows * (blocks_per_shard + 2 * d)),
     }
     pm = {}
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic_r01.json")

@@ -46,6 +46,7 @@ _SIGS = {
     "rbc_host_alloc": (c_int, [c_size_t, POINTER(c_void_p)]),
     "rbc_host_free": (c_int, [c_void_p]),
     "rbc_stream_create": (c_int, [c_int, POINTER(c_void_p)]),
+    "rbc_stream_create_priority": (c_int, [c_int, c_int, POINTER(c_void_p)]),
     "rbc_stream_destroy": (c_int, [c_void_p]),
     "rbc_stream_sync": (c_int, [c_void_p]),
     "rbc_event_create": (c_int, [POINTER(c_void_p)]),

@@ -110,7 +110,7 @@ struct DevBuf {
 // value assembly beside the regen hashing).  One per independent stream of
 // work: the context's device API has one, every host-API slot has its own.
 struct Ws {
-    DevBuf used, regen, dmat, nmiss, flags, list, counter, rcount, cls, vleaves;
+    DevBuf used, regen, dmat, nmiss, flags, list, counter, rcount, cls, vleaves, vlist;
     // fork the join onto an aux stream (device API); host-API slots keep one
     // stream each (their concurrency comes from the slots themselves, and
     // the box has GPU_MAX_HW_QUEUES = 4 hardware queues per process)
@@ -122,7 +122,8 @@ struct Ws {
                hipEventCreateWithFlags(&ev_join, hipEventDisableTiming) == hipSuccess;
     }
     void release() {
-        for (DevBuf *b : {&used, &regen, &dmat, &nmiss, &flags, &list, &counter, &rcount, &cls, &vleaves}) b->release();
+        for (DevBuf *b : {&used, &regen, &dmat, &nmiss, &flags, &list, &counter, &rcount, &cls, &vleaves, &vlist})
+            b->release();
         if (aux) (void)hipStreamDestroy(aux);
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         if (ev_join) (void)hipEventDestroy(ev_join);
@@ -374,6 +375,27 @@ int stage_verify(rbc_ctx *c, hipStream_t st, int count, const uint8_t *shards, u
     // 373, measured equal alone and slower beside a second stream).
     const uint32_t blocks_per_row = shard_lens ? 0u : (uniform_shard_len + 9 + 63) / 64;
     const bool path_pays = shard_lens || 16u * (uint32_t)c->depth >= blocks_per_row;
+    // Only the received ECHOs are validated (validateMessage runs per message):
+    // with a present mask the shards to hash are compacted into a device list
+    // first (N-f of N in the bench: a third fewer SHA rows than hashing all N).
+    // RBC_VERIFY_COMPACT=0 hashes every row and masks the verdict instead.
+    static const int compact_env = [] {
+        const char *e = getenv("RBC_VERIFY_COMPACT");
+        return e ? atoi(e) : 1;
+    }();
+    if (present && compact_env && c->n <= 256) {
+        uint32_t *vl = nullptr, *vc = nullptr;
+        {
+            std::lock_guard<std::mutex> lk(c->mu);
+            RBC_HIP(c->ws.vlist.ensure((size_t)count * c->n * 4 + 64));
+            vl = c->ws.vlist.as<uint32_t>();
+            vc = vl + (size_t)count * c->n;
+        }
+        RBC_HIP(hipMemsetAsync(vc, 0, 4, st));
+        RBC_HIP(rbc_launch_compact_present(present, c->n, count, valid, vl, vc, st));
+        a.list = vl;
+        a.list_count = vc;
+    }
     if (path_env && (path_pays || path_env == 2) && c->depth >= 1 && c->width <= 256) {
         uint8_t *lv = leaves;
         if (!lv) {
@@ -833,6 +855,16 @@ int rbc_stream_create(int device, void **stream) {
     RBC_HIP(hipSetDevice(device));
     hipStream_t s;
     RBC_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *stream = s;
+    return RBC_OK;
+}
+int rbc_stream_create_priority(int device, int high, void **stream) {
+    if (!stream) return RBC_ERR_INVALID_ARG;
+    RBC_HIP(hipSetDevice(device));
+    int least = 0, greatest = 0;
+    RBC_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    hipStream_t s;
+    RBC_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, high ? greatest : least));
     *stream = s;
     return RBC_OK;
 }

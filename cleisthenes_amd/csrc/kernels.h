@@ -198,6 +198,8 @@ hipError_t rbc_launch_digest(const uint8_t *leaves, uint64_t leaves_inst_pitch, 
 hipError_t rbc_launch_join(const JoinArgs &a, hipStream_t st);
 hipError_t rbc_launch_inject_faults(uint8_t *shards, uint64_t inst_pitch, uint32_t row_pitch,
                                     const int32_t *corrupt, int count, hipStream_t st);
+hipError_t rbc_launch_compact_present(const uint8_t *present, int n, int count, uint8_t *valid, uint32_t *list,
+                                     uint32_t *counter, hipStream_t st);
 hipError_t rbc_launch_pack_records(const uint8_t *roots, const uint8_t *digests, const int32_t *status, int count,
                                    int slots, uint8_t *out, hipStream_t st);
 hipError_t rbc_launch_fill_random(uint8_t *dst, uint64_t first_row, uint64_t rows, uint64_t pitch, uint64_t seed,

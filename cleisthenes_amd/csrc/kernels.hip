@@ -1067,6 +1067,40 @@ __global__ void inject_faults_kernel(uint8_t *shards, uint64_t inst_pitch, uint3
 }
 
 // ============================================================================
+// compact_present: the (inst, pos) list of the ECHO shards that were actually
+// received (present[i][pos] != 0), for the ECHO verify to hash only those
+// (validateMessage runs per received message, rbc/rbc.go:92-95); absent rows
+// get valid = 0 here.  One wave per instance, rows of an instance stay
+// contiguous in the list.
+// ============================================================================
+__global__ __launch_bounds__(64) void compact_present_kernel(const uint8_t *present, int n, int count, uint8_t *valid,
+                                                             uint32_t *list, uint32_t *counter) {
+    const int inst = blockIdx.x, lane = threadIdx.x;
+    if (inst >= count) return;
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    bool p[4];
+    uint64_t m[4];
+    int total = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int pos = c * 64 + lane;
+        p[c] = pos < n && present[(size_t)inst * n + pos] != 0;
+        m[c] = __ballot(p[c]);
+        total += __popcll(m[c]);
+        if (pos < n && !p[c]) valid[(size_t)inst * n + pos] = 0;
+    }
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(counter, (uint32_t)total);
+    base = __shfl(base, 0);
+    uint32_t off = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        if (p[c]) list[base + off + __popcll(m[c] & below)] = ((uint32_t)inst << 8) | (uint32_t)(c * 64 + lane);
+        off += __popcll(m[c]);
+    }
+}
+
+// ============================================================================
 // ACS records (rbc_dev_allgather_records): [slots][64] = {root, digest} per
 // instance, zero past `count`; the digest of an instance whose interpolate
 // failed (status != 0) is all-zero, so the record says on its own whether
@@ -1140,6 +1174,14 @@ __global__ __launch_bounds__(256) void count_mismatch_kernel(const uint8_t *a, u
 // ============================================================================
 // launchers
 // ============================================================================
+hipError_t rbc_launch_compact_present(const uint8_t *present, int n, int count, uint8_t *valid, uint32_t *list,
+                                     uint32_t *counter, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    if (n > 256) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(compact_present_kernel, dim3(count), dim3(64), 0, st, present, n, count, valid, list, counter);
+    return hipGetLastError();
+}
+
 hipError_t rbc_launch_pack_records(const uint8_t *roots, const uint8_t *digests, const int32_t *status, int count,
                                    int slots, uint8_t *out, hipStream_t st) {
     if (slots <= 0) return hipSuccess;

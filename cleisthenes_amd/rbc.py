@@ -102,9 +102,15 @@ class DeviceBuffer:
 
 
 class Stream:
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, priority: Optional[str] = None):
+        """priority None: default stream priority; "high" / "low": the device's
+        greatest / least (rbc_stream_create_priority)."""
         p = c_void_p()
-        check(lib.rbc_stream_create(device, byref(p)), "rbc_stream_create")
+        if priority is None:
+            check(lib.rbc_stream_create(device, byref(p)), "rbc_stream_create")
+        else:
+            check(lib.rbc_stream_create_priority(device, 1 if priority == "high" else 0, byref(p)),
+                  "rbc_stream_create_priority")
         self.ptr = p
 
     def sync(self) -> None:

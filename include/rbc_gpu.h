@@ -94,6 +94,9 @@ int rbc_memcpy_d2h(void *dst, const void *src, size_t bytes);
 int rbc_host_alloc(size_t bytes, void **ptr); /* pinned (hipHostMalloc) */
 int rbc_host_free(void *ptr);
 int rbc_stream_create(int device, void **stream);
+/* high != 0: the device's greatest stream priority (its waves are dispatched
+ * ahead of normal-priority streams' when both have work queued), else the least. */
+int rbc_stream_create_priority(int device, int high, void **stream);
 int rbc_stream_destroy(void *stream);
 int rbc_stream_sync(void *stream);
 int rbc_event_create(void **event);
@@ -129,10 +132,12 @@ int rbc_dev_shard_commit(rbc_ctx *ctx, void *stream, int count, const uint8_t *v
                          const uint32_t *value_lens, uint32_t uniform_value_len, uint8_t *shards,
                          uint32_t shard_pitch, const uint32_t *shard_lens, uint8_t *leaves, uint8_t *roots,
                          uint8_t *branches);
-/* ECHO-side validateMessage for every (instance, shard j): hash shard j,
- * walk branch j, compare with roots[i].  valid[i][j] = present[i][j] && ok
- * (present nullable = all).  leaves [count][n][32] (nullable) receives the
- * shard hashes for interpolate's recheck. */
+/* ECHO-side validateMessage for every received (instance, shard j): hash
+ * shard j, walk branch j, compare with roots[i].  valid[i][j] = present[i][j]
+ * && ok (present nullable = all).  Only present shards are hashed (they are
+ * compacted on the device first), so leaves [count][n][32] (nullable)
+ * receives the hashes of the present shards for interpolate's recheck; the
+ * slots of absent shards are left unspecified. */
 int rbc_dev_verify(rbc_ctx *ctx, void *stream, int count, const uint8_t *shards, uint32_t shard_pitch,
                    const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *branches,
                    const uint8_t *roots, const uint8_t *present, uint8_t *valid, uint8_t *leaves);

@@ -559,6 +559,13 @@ def test_two_rows_per_lane_sha_path(gpu, ref, n, f, S):
     leaves_r = pl.arr("leaves_r", shape=(I, n, 32))
     assert np.array_equal(leaves_r[exp == 1], leaves[exp == 1])  # verify's own leaf hashes
     assert (pl.arr("status", np.int32) == 0).all()
+    # with a present mask verify hashes the compacted received rows; without
+    # one every row is hashed, by the two-rows-per-lane kernel at this size
+    c, b = pl.ctx, pl.b
+    c.dev_verify(None, I, b["shards"], pl.spitch, None, S, b["branches"], b["roots"], None, b["valid"], b["leaves_r"])
+    exp_all = np.ones((I, n), np.uint8)  # interpolate rewrote every row with the re-encoding
+    assert np.array_equal(pl.arr("valid", shape=(I, n)), exp_all)
+    assert np.array_equal(pl.arr("leaves_r", shape=(I, n, 32)), leaves)  # = the committed leaves
     out = pl.arr("out", shape=(I, pl.opitch))
     assert np.array_equal(out[:, :B], pl.values[:, :B])
 
@@ -612,7 +619,8 @@ def test_device_verify_shared_paths_adversarial(gpu, ref, n, f, B, I):
                 slots[0] = 0  # device form: an empty level-0 sibling is a zero slot
             want = bool(present[i, j]) and ref.verify(n, sh[i, j, :S], j, slots, bytes(roots[i]))
             assert got[i, j] == int(want), (n, i, j)
-            assert leaves[i, j].tobytes() == ref.sha256(sh[i, j, :S].tobytes()), (n, i, j)
+            if present[i, j]:  # only received shards are hashed (leaves of absent rows: unspecified)
+                assert leaves[i, j].tobytes() == ref.sha256(sh[i, j, :S].tobytes()), (n, i, j)
     assert got[0].all() and not got[4].any()
 
 

@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""Per-kernel-role durations from a rocprofv3 --kernel-trace CSV of bench.py.
+
+usage: tools/trace_summary.py <run_kernel_trace.csv> --config c2 [--instances 1024] [--last K]
+       [--json out.json]
+
+Roles are told apart by kernel name plus grid size: sha_rows_kernel<false>
+is the commit-side leaf hashing when its grid covers every row (I*N threads)
+and interpolate's regen hashing when it covers the N-k regenerated slots per
+instance; rs_fft_kernel<.., 0> is encode and <.., 1> the decode re-encode.
+Only the last `K` launches of each role are averaged (the bench's K timed
+steps; warmup launches come first, and launches on other batch sizes -- the
+PCIe host-path measurement -- have other grids, hence other roles), so the
+averages cover the same launches whose HIP-event spans bench.py reports as
+stage_ms / roofline.avg_ms.
+"""
+import argparse
+import csv
+import json
+from collections import defaultdict
+
+CONFIGS = {"c1": (64, 21), "c2": (128, 42), "c3": (128, 42), "c4": (256, 85)}
+
+
+def base(name):
+    return name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").strip()
+
+
+def role(name, grid, n, k, inst):
+    b = base(name)
+    if b.startswith("rs_fft_kernel<"):
+        return "rs_fft_kernel<encode>" if b.rstrip(">").endswith(", 0") else "rs_fft_kernel<decode>"
+    if b == "sha_rows_kernel<false>":
+        if grid == inst * n:
+            return "sha_rows_kernel<leaves>"
+        if grid == inst * (n - k):
+            return "sha_rows_kernel<regen>"
+        return f"sha_rows_kernel<false>[grid {grid}]"
+    if b == "sha_rows_kernel<true>":
+        return "sha_rows_kernel<verify>"
+    return b
+
+
+def summarize(path, config, inst, last):
+    n, f = CONFIGS[config]
+    k = n - 2 * f
+    durs = defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        grid = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6  # ms
+        durs[(role(r["Kernel_Name"], grid, n, k, inst), int(r["Dispatch_Id"]))].append(d)
+    by_role = defaultdict(list)
+    for (rl, did), ds in sorted(durs.items(), key=lambda x: x[0][1]):
+        by_role[rl].extend(ds)
+    out = {}
+    for rl, ds in by_role.items():
+        kept = ds[-last:] if last else ds
+        out[rl] = {"launches": len(ds), "timed_launches": len(kept), "avg_ms": round(sum(kept) / len(kept), 4),
+                   "min_ms": round(min(kept), 4), "max_ms": round(max(kept), 4)}
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--instances", type=int, default=1024)
+    ap.add_argument("--last", type=int, default=0, help="average only the last K launches per role (timed steps)")
+    ap.add_argument("--json")
+    a = ap.parse_args()
+    res = summarize(a.trace, a.config, a.instances, a.last)
+    for rl, v in sorted(res.items(), key=lambda x: -x[1]["avg_ms"] * x[1]["timed_launches"]):
+        print(f"{rl:46s} {v['timed_launches']:4d} x {v['avg_ms']:8.4f} ms  (min {v['min_ms']:.4f}, max {v['max_ms']:.4f})")
+    if a.json:
+        with open(a.json, "w") as fh:
+            json.dump({"source": a.trace, "config": a.config, "instances": a.instances, "last": a.last,
+                       "roles": res}, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
