@@ -259,6 +259,13 @@ def main(argv):
     corrupt_h = corrupt_all[first:first + I]
 
     pipe = bool(args.pipeline)
+    # the pipeline holds two shard sets; when they do not fit the 288 GB of
+    # HBM (C3 with all 8192 instances on one GPU: 2 x 100 GB + values) run
+    # the serial schedule instead
+    set_bytes = I * n * spitch + I * (n * 32 + 32 + n * max(d, 1) * 32)
+    other_bytes = I * (vpitch + opitch + n * 34 + 64)
+    if pipe and 2 * set_bytes + other_bytes > float(os.environ.get("RBC_BENCH_HBM_BUDGET", 250e9)):
+        pipe = False
     nsets = 2 if pipe else 1
     sets = [dict(shards=mb(I * n * spitch), leaves=mb(I * n * 32), roots=mb(I * 32),
                  branches=mb(I * n * max(d, 1) * 32)) for _ in range(nsets)]
@@ -419,14 +426,19 @@ def main(argv):
         "sha_rows_kernel<verify>": (stage_ms["verify"], R_rows * (S + d * 32 + 32) + I * (32 + 2 * n),
                                     R_rows * (blocks_per_shard + 2 * d)),
     }
-    pm = {}
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic_r01.json")
-    if os.path.exists(pmc_path):
-        try:
-            pm = json.load(open(pmc_path))
-            if pm.get("config") != args.config or I != 1024:
+    # PMC-measured HBM traffic per launch (tools/profile.sh + tools/pmc_summary.py
+    # on this bench's default command), newest round first
+    pm, pmc_path = {}, None
+    for cand in ("pmc_traffic_r02.json", "pmc_traffic_r01.json"):
+        pth = os.path.join(ROOT, "profiles", cand)
+        if os.path.exists(pth):
+            try:
+                pm = json.load(open(pth))
+            except Exception:
                 pm = {}
-        except Exception:
+            if pm.get("config") == args.config and pm.get("instances", 1024) == I:
+                pmc_path = pth
+                break
             pm = {}
 
     def roofline(name):
@@ -456,6 +468,18 @@ def main(argv):
             if pk and pk.get("valu_per_compression"):
                 r["valu"]["valu_instr_per_compression_pmc"] = pk["valu_per_compression"]
         return r
+
+    # chip-level SHA-256 rate of the whole step (all three hashing kernels,
+    # both streams): under the pipelined schedule a kernel's own span also
+    # holds the other stream's work, so this is the utilisation figure
+    regen_rows = int(I * n - present_h.sum() + (corrupt_h >= 0).sum())
+    step_comp = I * n * blocks_per_shard + R_rows * (blocks_per_shard + 2 * d) + regen_rows * blocks_per_shard
+    step_cps = step_comp / (elapsed_max / args.steps)  # per GPU
+    sha_chip = {"compressions_per_step": int(step_comp), "achieved": round(step_cps / 1e9, 2),
+                "unit": "G compressions/s per GPU", "attainable_probe": round(SHA_PROBE_CPS / 1e9, 2),
+                "frac_of_attainable": round(step_cps / SHA_PROBE_CPS, 3),
+                "note": "leaves (all N rows) + ECHO verify (received rows + branch walk) + interpolate's "
+                        "regenerated rows, per ms_per_step"}
 
     dom = max(kern, key=lambda x: kern[x][0])
     roof = roofline(dom)
@@ -514,6 +538,7 @@ def main(argv):
         **checks,
         "roofline": roof,
         "roofline_encode": codec_roof,
+        "sha256_chip": sha_chip,
         "cpu_baseline": cpu,
         "pcie_inclusive": pcie,
         "rccl": rccl,

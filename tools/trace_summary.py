@@ -44,14 +44,20 @@ def role(name, grid, n, k, inst):
 def summarize(path, config, inst, last):
     n, f = CONFIGS[config]
     k = n - 2 * f
-    durs = defaultdict(list)
+    durs = []
     for r in csv.DictReader(open(path)):
         grid = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6  # ms
-        durs[(role(r["Kernel_Name"], grid, n, k, inst), int(r["Dispatch_Id"]))].append(d)
+        durs.append((int(r["Dispatch_Id"]), role(r["Kernel_Name"], grid, n, k, inst), grid, d))
+    # one role may run on several batch sizes (the PCIe host-path measurement
+    # uses small batches): the largest grid is the bench batch, others are
+    # reported apart as role[grid G]
+    biggest = defaultdict(int)
+    for _, rl, grid, _ in durs:
+        biggest[rl] = max(biggest[rl], grid)
     by_role = defaultdict(list)
-    for (rl, did), ds in sorted(durs.items(), key=lambda x: x[0][1]):
-        by_role[rl].extend(ds)
+    for _, rl, grid, d in sorted(durs):
+        by_role[rl if grid == biggest[rl] else f"{rl}[grid {grid}]"].append(d)
     out = {}
     for rl, ds in by_role.items():
         kept = ds[-last:] if last else ds
