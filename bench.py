@@ -93,6 +93,10 @@ def parse_args(argv):
                     help="run the RCCL all-gather even with one rank (exercises rbc_comm_*)")
     ap.add_argument("--no-pcie", action="store_true",
                     help="skip the PCIe-inclusive host-path measurement (a secondary key, never `value`)")
+    ap.add_argument("--rehearse-on-one-gpu", action="store_true",
+                    help="rehearsal of the N-rank path on a 1-GPU box: every rank uses device 0 and the "
+                         "RCCL all-gather is skipped (RCCL needs one device per rank); everything else -- "
+                         "spawn, rendezvous, partition, checks, max-over-ranks -- runs as on N GPUs")
     ap.add_argument("--oracle-samples", type=int, default=16,
                     help="instances whose root and digest are checked against the C oracle after timing")
     return ap.parse_args(argv)
@@ -230,7 +234,7 @@ def main(argv):
         scaling = "weak"
     if I < 1:
         raise SystemExit(f"bench: rank {rank} owns no instances ({total} over {world})")
-    dev = local_rank
+    dev = 0 if args.rehearse_on_one_gpu else local_rank
     placement = numa_place(ca, dev) if world > 1 else None
 
     ctx = ca.Context(n, f, device=dev)
@@ -279,7 +283,7 @@ def main(argv):
     d_digests = mb(I * 32)
     d_status = mb(I * 4)
     d_count = mb(16)
-    gather = world > 1 or args.force_gather
+    gather = (world > 1 or args.force_gather) and not args.rehearse_on_one_gpu
     slots = acs.max_share(total, world)
     d_gather = mb(world * slots * 64) if gather else None
     rccl = None
@@ -532,6 +536,8 @@ def main(argv):
                    "parallelism": f"instances partitioned over {world} GPU(s) in contiguous blocks"
                                   + (", RCCL all-gather of {root,digest} records" if gather else ""),
                    "gf_codec": ctx.codec,
+                   **({"rehearsal": "all ranks on device 0, no RCCL (not a multi-GPU measurement)"}
+                      if args.rehearse_on_one_gpu else {}),
                    "pipeline": "commit(t) || verify+interpolate(t-1) on two streams" if pipe else "serial"},
         "stage_ms": {kk: round(v, 4) for kk, v in stage_ms.items()},
         "phases": phases,
