@@ -1070,33 +1070,52 @@ __global__ void inject_faults_kernel(uint8_t *shards, uint64_t inst_pitch, uint3
 // compact_present: the (inst, pos) list of the ECHO shards that were actually
 // received (present[i][pos] != 0), for the ECHO verify to hash only those
 // (validateMessage runs per received message, rbc/rbc.go:92-95); absent rows
-// get valid = 0 here.  One wave per instance, rows of an instance stay
-// contiguous in the list.
+// get valid = 0 here.  A 256-thread block handles 16 instances, one wave per
+// instance at a time; the block reserves its list range with ONE global
+// atomic (one per instance serialised 16k atomics on one address at C4:
+// 0.19 ms), and the rows of an instance stay contiguous in the list.
 // ============================================================================
-__global__ __launch_bounds__(64) void compact_present_kernel(const uint8_t *present, int n, int count, uint8_t *valid,
-                                                             uint32_t *list, uint32_t *counter) {
-    const int inst = blockIdx.x, lane = threadIdx.x;
-    if (inst >= count) return;
+constexpr int COMPACT_IPB = 16;
+__global__ __launch_bounds__(256) void compact_present_kernel(const uint8_t *present, int n, int count,
+                                                              uint8_t *valid, uint32_t *list, uint32_t *counter) {
+    __shared__ uint32_t s_cnt[COMPACT_IPB];
+    __shared__ uint32_t s_base;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int inst0 = blockIdx.x * COMPACT_IPB;
     const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    bool p[4];
-    uint64_t m[4];
-    int total = 0;
+    bool p[COMPACT_IPB / 4][4];
+    uint64_t m[COMPACT_IPB / 4][4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const int pos = c * 64 + lane;
-        p[c] = pos < n && present[(size_t)inst * n + pos] != 0;
-        m[c] = __ballot(p[c]);
-        total += __popcll(m[c]);
-        if (pos < n && !p[c]) valid[(size_t)inst * n + pos] = 0;
+    for (int q = 0; q < COMPACT_IPB / 4; ++q) {  // wave w owns instances inst0 + 4q + w
+        const int inst = inst0 + 4 * q + w;
+        int total = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int pos = c * 64 + lane;
+            p[q][c] = inst < count && pos < n && present[(size_t)inst * n + pos] != 0;
+            m[q][c] = __ballot(p[q][c]);
+            total += __popcll(m[q][c]);
+            if (inst < count && pos < n && !p[q][c]) valid[(size_t)inst * n + pos] = 0;
+        }
+        if (lane == 0) s_cnt[4 * q + w] = (uint32_t)total;
     }
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(counter, (uint32_t)total);
-    base = __shfl(base, 0);
-    uint32_t off = 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int i = 0; i < COMPACT_IPB; ++i) t += s_cnt[i];
+        s_base = t ? atomicAdd(counter, t) : 0u;
+    }
+    __syncthreads();
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        if (p[c]) list[base + off + __popcll(m[c] & below)] = ((uint32_t)inst << 8) | (uint32_t)(c * 64 + lane);
-        off += __popcll(m[c]);
+    for (int q = 0; q < COMPACT_IPB / 4; ++q) {
+        const int slot = 4 * q + w, inst = inst0 + slot;
+        uint32_t off = s_base;
+        for (int i = 0; i < slot; ++i) off += s_cnt[i];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (p[q][c]) list[off + __popcll(m[q][c] & below)] = ((uint32_t)inst << 8) | (uint32_t)(c * 64 + lane);
+            off += __popcll(m[q][c]);
+        }
     }
 }
 
@@ -1178,7 +1197,8 @@ hipError_t rbc_launch_compact_present(const uint8_t *present, int n, int count, 
                                      uint32_t *counter, hipStream_t st) {
     if (count <= 0) return hipSuccess;
     if (n > 256) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(compact_present_kernel, dim3(count), dim3(64), 0, st, present, n, count, valid, list, counter);
+    hipLaunchKernelGGL(compact_present_kernel, dim3((count + COMPACT_IPB - 1) / COMPACT_IPB), dim3(256), 0, st,
+                       present, n, count, valid, list, counter);
     return hipGetLastError();
 }
 
