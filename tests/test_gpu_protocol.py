@@ -76,7 +76,7 @@ def rand(n, seed):
     return np.random.default_rng(seed).integers(0, 256, n, dtype=np.uint8).tobytes()
 
 
-@pytest.mark.parametrize("n,f,B", [(4, 1, 1000), (7, 2, 333), (16, 5, 65536), (4, 1, 0), (4, 1, 1)])
+@pytest.mark.parametrize("n,f,B", [(4, 1, 1024), (4, 1, 1000), (7, 2, 333), (16, 5, 65536), (4, 1, 0), (4, 1, 1)])
 def test_honest_network_delivers(ca, n, f, B):
     net = Net(ca, n, f, proposers=[0])
     try:
