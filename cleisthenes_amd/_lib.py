@@ -125,6 +125,8 @@ _SIGS = {
     "rbc_dev_marshal_val": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_uint32, c_void_p, c_uint32,
                                     c_void_p, c_void_p, c_void_p, c_uint64, c_void_p]),
     "rbc_val_message_size": (c_size_t, [c_int, c_uint32, c_uint32, c_int]),
+    "rbc_shard_commit_val": (c_int, [c_void_p, c_int, c_void_p, szp, c_void_p, c_size_t, u32p, c_void_p,
+                                     POINTER(c_uint64)]),
     "rbc_node_create": (c_int, [c_void_p, c_int, c_int, c_int, c_int, POINTER(c_void_p)]),
     "rbc_node_destroy": (None, [c_void_p]),
     "rbc_node_propose": (c_int, [c_void_p, c_void_p, c_size_t]),

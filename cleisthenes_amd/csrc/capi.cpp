@@ -1186,6 +1186,85 @@ int rbc_shard_commit(rbc_ctx *c, int count, const uint8_t *const *values, const 
     });
 }
 
+// VAL hand-off: shard + commit on the device, marshal the
+// N per-recipient pb.Message VALs there (marshal_val_kernel) and move the
+// whole batch of finished messages to the caller's ring in one D2H.
+int rbc_shard_commit_val(rbc_ctx *c, int count, const uint8_t *const *values, const size_t *value_lens,
+                         uint8_t *msgs, size_t msg_pitch, uint32_t *msg_lens, uint8_t *roots_out,
+                         uint64_t *ticket) {
+    if (!c || count < 0 || (count > 0 && (!values || !value_lens || !msgs || !msg_lens))) return RBC_ERR_INVALID_ARG;
+    if (count == 0) { if (ticket) *ticket = 0; return RBC_OK; }
+    size_t Smax = 0;
+    for (int i = 0; i < count; ++i) {
+        if (value_lens[i] == 0) return RBC_ERR_SHORT_DATA;  // Split: len(data) == 0
+        if (!values[i]) return RBC_ERR_INVALID_ARG;
+        Smax = std::max(Smax, (value_lens[i] + c->k - 1) / c->k);
+    }
+    const int d = c->depth, n = c->n;
+    const size_t need = round_up(std::max(rbc_val_message_bytes(n, d, (uint32_t)Smax, 0, RBC_MSG_VAL),
+                                          rbc_val_message_bytes(n, d, (uint32_t)Smax, (uint32_t)(n - 1),
+                                                                RBC_MSG_VAL)),
+                                 16);
+    if (msg_pitch < need || msg_pitch % 16) return RBC_ERR_INVALID_ARG;
+    const size_t dpitch = round_up(Smax, 128);
+    const size_t vpitch = round_up((size_t)c->k * Smax + 32, kAlign);
+    if (vpitch > 0x7fffffffULL || (size_t)n * dpitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
+    const size_t sh_bytes = (size_t)count * n * dpitch, br_bytes = (size_t)count * n * std::max(d, 1) * 32;
+    const size_t msg_bytes = (size_t)count * n * msg_pitch;
+    std::lock_guard<std::mutex> lk(c->mu);
+    RBC_HIP(hipSetDevice(c->device));
+    Slot *sp = acquire_slot(c);
+    if (!sp) return RBC_ERR_DEVICE;
+    Slot &s = *sp;
+    hipStream_t st = s.stream;
+    RBC_HIP(s.d_values.ensure((size_t)count * vpitch));
+    RBC_HIP(s.d_shards.ensure(sh_bytes + msg_bytes));  // shards, then the messages
+    RBC_HIP(s.d_leaves.ensure((size_t)count * n * 32));
+    RBC_HIP(s.d_roots.ensure((size_t)count * 32));
+    RBC_HIP(s.d_branches.ensure(br_bytes));
+    RBC_HIP(s.d_lens.ensure((size_t)count * 8 + (size_t)count * n * 4));
+    RBC_HIP(s.h_in.ensure((size_t)count * vpitch + (size_t)count * 8));
+    uint8_t *stage = s.h_in.as<uint8_t>();
+    uint32_t *lens = reinterpret_cast<uint32_t *>(stage + (size_t)count * vpitch);
+    parallel_for(count, vpitch, [&](int i) {
+        memcpy(stage + (size_t)i * vpitch, values[i], value_lens[i]);
+        memset(stage + (size_t)i * vpitch + value_lens[i], 0, vpitch - value_lens[i]);
+        lens[i] = (uint32_t)value_lens[i];
+        lens[count + i] = (uint32_t)((value_lens[i] + c->k - 1) / c->k);
+    });
+    RBC_HIP(hipMemcpyAsync(s.d_values.p, stage, (size_t)count * vpitch, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(s.d_lens.p, lens, (size_t)count * 8, hipMemcpyHostToDevice, st));
+    const uint32_t *d_vlens = s.d_lens.as<uint32_t>(), *d_slens = d_vlens + count;
+    uint32_t *d_mlens = s.d_lens.as<uint32_t>() + 2 * (size_t)count;
+    uint8_t *d_sh = s.d_shards.as<uint8_t>(), *d_msgs = d_sh + sh_bytes;
+    int rc = stage_encode(c, st, count, s.d_values.as<uint8_t>(), vpitch, d_vlens, 0, d_sh, (uint32_t)dpitch);
+    if (!rc) rc = stage_leaves(c, st, count, d_sh, (uint32_t)dpitch, d_slens, 0, s.d_leaves.as<uint8_t>());
+    if (!rc) rc = stage_merkle_build(c, st, count, s.d_leaves.as<uint8_t>(), s.d_roots.as<uint8_t>(),
+                                     s.d_branches.as<uint8_t>());
+    if (rc) return rc;
+    WireArgs a{};
+    a.count = count;
+    a.n = n;
+    a.depth = d;
+    a.type = RBC_MSG_VAL;
+    a.shards = d_sh;
+    a.inst_pitch = (uint64_t)n * dpitch;
+    a.row_pitch = (uint32_t)dpitch;
+    a.lens = d_slens;
+    a.branches = s.d_branches.as<uint8_t>();
+    a.roots = s.d_roots.as<uint8_t>();
+    a.out = d_msgs;
+    a.out_pitch = msg_pitch;
+    a.out_lens = d_mlens;
+    RBC_HIP(rbc_launch_marshal_val(a, st));
+    // one D2H of the finished messages: straight into a pinned ring, else
+    // through HIP's staging (pageable)
+    RBC_HIP(hipMemcpyAsync(msgs, d_msgs, msg_bytes, hipMemcpyDeviceToHost, st));
+    RBC_HIP(hipMemcpyAsync(msg_lens, d_mlens, (size_t)count * n * 4, hipMemcpyDeviceToHost, st));
+    if (roots_out) RBC_HIP(hipMemcpyAsync(roots_out, s.d_roots.p, (size_t)count * 32, hipMemcpyDeviceToHost, st));
+    return submit(c, s, ticket, []() { return RBC_OK; });
+}
+
 int rbc_validate_batch(rbc_ctx *c, int count, const uint8_t *const *shards, const size_t *shard_lens,
                        const uint32_t *indices, const uint8_t *const *branches, const size_t *branch_lens,
                        const uint8_t *const *roots, uint8_t *ok_out, uint64_t *ticket) {

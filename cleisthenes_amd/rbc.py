@@ -320,6 +320,29 @@ class Context:
         out = {"shards": shards, "shard_lens": slens, "roots": roots, "branches": br[:, :, : self.depth]}
         return HostTicket(self, t.value, out, keep=(arrs, vlens, vptrs, br))
 
+    def shard_commit_val(self, values: Sequence[bytes], ring: Optional[np.ndarray] = None) -> dict:
+        """rbc_shard_commit_val: shard + commit and the N per-recipient VAL
+        pb.Messages of every proposal, handed over in one D2H.  `ring` may be
+        a preallocated (e.g. pinned_empty) uint8 array [count][n][msg_pitch]."""
+        count = len(values)
+        arrs = [_bytes_array(v) for v in values]
+        Smax = max((len(a) + self.k - 1) // self.k for a in arrs)
+        need = max(lib.rbc_val_message_size(self.n, Smax, 0, 0), lib.rbc_val_message_size(self.n, Smax, self.n - 1, 0))
+        pitch = (need + 15) // 16 * 16
+        if ring is None:
+            ring = np.zeros((count, self.n, pitch), dtype=np.uint8)
+        assert ring.shape[:2] == (count, self.n) and ring.shape[2] % 16 == 0 and ring.shape[2] >= pitch
+        lens = np.zeros((count, self.n), dtype=np.uint32)
+        roots = np.zeros((count, 32), dtype=np.uint8)
+        vlens = (c_size_t * count)(*[len(a) for a in arrs])
+        vptrs = (c_void_p * count)(*[a.ctypes.data if len(a) else None for a in arrs])
+        t = c_uint64(0)
+        check(lib.rbc_shard_commit_val(self._p, count, vptrs, vlens, _ptr(ring), ring.shape[2],
+                                       lens.ctypes.data_as(_lib.u32p), _ptr(roots), byref(t)), "rbc_shard_commit_val")
+        check(lib.rbc_wait(self._p, t.value), "rbc_wait")
+        return {"msgs": ring, "lens": lens, "roots": roots,
+                "message": lambda i, j: bytes(ring[i, j, : lens[i, j]])}
+
     def validate_batch(self, shards, indices, branches, roots) -> np.ndarray:
         count = len(shards)
         sh = [_bytes_array(s) for s in shards]

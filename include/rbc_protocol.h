@@ -78,6 +78,22 @@ int rbc_dev_marshal_val(rbc_ctx *ctx, void *stream, int count, int type, const u
 /* Size of that message for shard length S at leaf `index` of an n-node tree. */
 size_t rbc_val_message_size(int n, uint32_t shard_len, uint32_t index, int type);
 
+/* The proposer's send path in one call (the gap at
+ * conn.go:182-208, where Broadcaster.Broadcast sends one message to all while
+ * VAL differs per recipient): shard + commit `count` proposals (host values),
+ * marshal every per-recipient VAL on the device, and move the finished
+ * pb.Message bytes to the caller's ring in ONE device-to-host copy:
+ * msgs [count][n][msg_pitch] (message (i, j) for member j at
+ * msgs + (i*n + j)*msg_pitch, msg_lens [count][n] bytes), roots_out
+ * [count][32] (nullable).  msg_pitch % 16 == 0 and >= the largest
+ * rbc_val_message_size(n, S_max, index, RBC_MSG_VAL).  Ring memory from
+ * rbc_host_alloc is written directly by the DMA engine (no staging copy);
+ * a gRPC writer sends msgs[i][j][:len] to member j with a pass-through codec
+ * (INTEGRATION.md).  Asynchronous: complete with rbc_wait / rbc_poll. */
+int rbc_shard_commit_val(rbc_ctx *ctx, int count, const uint8_t *const *values, const size_t *value_lens,
+                         uint8_t *msgs, size_t msg_pitch, uint32_t *msg_lens, uint8_t *roots_out,
+                         uint64_t *ticket);
+
 /* ---- RBC instance (one proposer's broadcast, seen at one node) ----------- */
 typedef struct rbc_node rbc_node;
 /* NewRBC (rbc/rbc.go:38). */

@@ -108,3 +108,32 @@ def test_marshal_round_trips_through_the_state_machine(gpu):
     finally:
         bt.close()
         ctx.close()
+
+
+@pytest.mark.parametrize("n,f,lens,pinned", [(16, 5, [1001, 777, 5000], False), (7, 2, [333, 1, 2000], True),
+                                             (128, 42, [1 << 20, (1 << 20) - 3], True)])
+def test_shard_commit_val_hands_over_every_recipients_message(gpu, n, f, lens, pinned):
+    """rbc_shard_commit_val: every per-recipient VAL is
+    byte-identical to the host codec over the oracle's commitment, handed
+    over in one D2H into a pinned (or pageable) ring."""
+    import rbc_oracle as orc
+    from cleisthenes_amd import protocol
+    ca = gpu
+    ctx = ca.Context(n, f)
+    rng = np.random.default_rng(sum(lens))
+    vals = [rng.integers(0, 256, L, dtype=np.uint8).tobytes() for L in lens]
+    k = n - 2 * f
+    Smax = max((L + k - 1) // k for L in lens)
+    pitch = rup(max(ctx.val_message_size(Smax, 0, 0), ctx.val_message_size(Smax, n - 1, 0)), 16)
+    ring = ca.pinned_empty((len(vals), n, pitch)) if pinned else None
+    out = ctx.shard_commit_val(vals, ring=ring)
+    enc = orc.Encoder(k, 2 * f)
+    for i, v in enumerate(vals):
+        shards = orc.rbc_shard(enc, np.frombuffer(v, np.uint8))
+        com = orc.rbc_commit(shards)
+        assert bytes(out["roots"][i]) == com["root"]
+        for j in range(n):
+            br = orc.flat_branch(com["branches"][j])
+            want = protocol.pb_encode(protocol.VAL, protocol.json_encode_val(com["root"], br, bytes(shards[j])))
+            assert out["message"](i, j) == want, (i, j)
+    ctx.close()

@@ -77,9 +77,23 @@ def measure(ca, n, f, B, batch=64, batches=8, inflight=2, pinned=True, device=0)
         res = ctx.interpolate_batch(rx, lens, present, roots, values_out=vout)
     t_dec = time.perf_counter() - t0
     assert (res["status"] == 0).all()
+    # proposer send path: shard + commit + per-recipient VAL marshal, one D2H of
+    # the finished pb.Message bytes into a pinned ring (rbc_shard_commit_val)
+    vring = None
+    if pinned:
+        need = max(ctx.val_message_size(S, 0, 0), ctx.val_message_size(S, n - 1, 0))
+        vring = ca.pinned_empty((batch, n, (need + 15) // 16 * 16))
+    ctx.shard_commit_val(pool[0], ring=vring)  # warm-up
+    t0 = time.perf_counter()
+    for b in range(batches):
+        vo = ctx.shard_commit_val(pool[b % 2], ring=vring)
+    t_val = time.perf_counter() - t0
+    msg_bytes = int(vo["lens"].sum()) * batches
     ctx.close()
     shard_bytes = batch * n * S * batches
-    return {"shard_commit_GBps": round(shard_bytes / t_enc / 1e9, 2),
+    return {"shard_commit_val_msg_GBps": round(msg_bytes / t_val / 1e9, 2),
+            "shard_commit_val_ms_per_batch": round(t_val * 1e3 / batches, 3),
+            "shard_commit_GBps": round(shard_bytes / t_enc / 1e9, 2),
             "interpolate_GBps": round(shard_bytes / t_dec / 1e9, 2),
             "shard_commit_ms_per_batch": round(t_enc * 1e3 / batches, 3),
             "interpolate_ms_per_batch": round(t_dec * 1e3 / batches, 3),
