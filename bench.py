@@ -86,7 +86,11 @@ def parse_args(argv):
                     help="configs the CPU port is also timed on (the bench config always is)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="1 (default): overlap batch t's commit (proposer stream) with batch t-1's verify + "
-                         "interpolate (receiver stream), two shard buffer sets; 0: one stream, stages in order")
+                         "interpolate (receiver stream); 2: three streams -- commit(t) || verify(t-1) || "
+                         "interpolate(t-2); 0: one stream, stages in order")
+    ap.add_argument("--sets", type=int, default=0,
+                    help="shard buffer sets of the pipelined schedule (0: the minimum, 2 for --pipeline 1, "
+                         "3 for --pipeline 2; more let the proposer run further ahead)")
     ap.add_argument("--shard-align", type=int, default=128,
                     help="shard row pitch alignment in bytes (multiple of 64; the C ABI needs 64)")
     ap.add_argument("--force-gather", action="store_true",
@@ -263,16 +267,23 @@ def main(argv):
     corrupt_h = corrupt_all[first:first + I]
 
     pipe = bool(args.pipeline)
+    pipe3 = args.pipeline == 2
     # the pipeline holds two shard sets; when they do not fit the 288 GB of
     # HBM (C3 with all 8192 instances on one GPU: 2 x 100 GB + values) run
     # the serial schedule instead
     set_bytes = I * n * spitch + I * (n * 32 + 32 + n * max(d, 1) * 32)
     other_bytes = I * (vpitch + opitch + n * 34 + 64)
-    if pipe and 2 * set_bytes + other_bytes > float(os.environ.get("RBC_BENCH_HBM_BUDGET", 250e9)):
-        pipe = False
-    nsets = 2 if pipe else 1
+    if pipe3:
+        set_bytes += I * (n + n * 32)  # per-set valid + verified leaves (verify and interpolate run apart)
+    nsets = max(3 if pipe3 else 2, args.sets) if pipe else 1
+    budget = float(os.environ.get("RBC_BENCH_HBM_BUDGET", 250e9))
+    while pipe and nsets * set_bytes + other_bytes > budget:
+        nsets -= 1
+        if nsets < (3 if pipe3 else 2):
+            pipe, pipe3, nsets = False, False, 1
     sets = [dict(shards=mb(I * n * spitch), leaves=mb(I * n * 32), roots=mb(I * 32),
-                 branches=mb(I * n * max(d, 1) * 32)) for _ in range(nsets)]
+                 branches=mb(I * n * max(d, 1) * 32),
+                 **({"valid": mb(I * n), "leaves_r": mb(I * n * 32)} if pipe3 else {})) for _ in range(nsets)]
     d_present = mb(I * n)
     d_present.upload(present_h)
     d_corrupt = mb(I * 4)
@@ -299,9 +310,11 @@ def main(argv):
     # stream (r0 .. gather); a stage's time is its own stream's event span
     pipe_spans = (("t0", "enc"), ("enc", "leaf"), ("leaf", "tree"), ("tree", "fault"), ("r0", "verify"),
                   ("verify", "interp"), ("interp", "gather"))
+    if pipe3:  # verify on its own stream V: (v0, verify); interpolate on R: (r0, interp)
+        pipe_spans = pipe_spans[:4] + (("v0", "verify"), ("r0", "interp"), ("interp", "gather"))
     # one event set per timed step: stage times are read after the closing
     # barrier, so the timed loop never waits on the host between steps
-    ev_sets = [{name: ca.Event() for name in stage_names + ("r0",)} for _ in range(max(args.steps, 3))]
+    ev_sets = [{name: ca.Event() for name in stage_names + ("r0", "v0")} for _ in range(max(args.steps, 3))]
 
     def step(ev, sp=None):
         sp = sp or sets[0]
@@ -338,17 +351,67 @@ def main(argv):
         stream.sync()  # the input fill ran on the old stream
         stream = ca.Stream(dev, priority="high")
     rstream = ca.Stream(dev, priority="high" if prio == "R" else None) if pipe else None
+    # RBC_BENCH_CU_SPLIT=a/b (A/B knob): the proposer stream gets CUs with
+    # (cu % b) < a, the receiver stream the rest -- disjoint CUs instead of both
+    # stages' kernels sharing every CU (and its instruction cache)
+    split = os.environ.get("RBC_BENCH_CU_SPLIT", "")
+    if pipe and split:
+        a_, b_ = (int(x) for x in split.split("/"))
+        ncu = ca.rbc.cu_count(dev)
+        stream.sync()
+        stream = ca.Stream(dev, cu_mask=[c for c in range(ncu) if c % b_ < a_])
+        rstream = ca.Stream(dev, cu_mask=[c for c in range(ncu) if c % b_ >= a_])
+    vstream = ca.Stream(dev) if pipe3 else None
+    ctxV = ca.Context(n, f, device=dev) if pipe3 else None  # own decode/verify workspace per stream
     evP = [ca.Event() for _ in range(nsets)]
     evR = [ca.Event() for _ in range(nsets)]
-    for e in evP + evR:
+    evV = [ca.Event() for _ in range(nsets)]
+    for e in evP + evR + evV:
         e.record(stream)  # recorded once, so every wait below is well defined
+
+    def pstep3(t, ev=None):
+        """commit(t) on P || verify(t-1) on V || interpolate(t-2) on R; a set
+        is reused by commit(t) only after interpolate(t - nsets) read it."""
+        P, V, R = stream, vstream, rstream
+        rec = (lambda name, st: ev[name].record(st)) if ev is not None else (lambda name, st: None)
+        sp = sets[t % nsets]
+        P.wait(evR[t % nsets])
+        rec("t0", P)
+        ctx.dev_encode(P.ptr, I, d_values, vpitch, None, B, sp["shards"], spitch)
+        rec("enc", P)
+        ctx.dev_leaves(P.ptr, I, sp["shards"], spitch, None, S, sp["leaves"])
+        rec("leaf", P)
+        ctx.dev_merkle_build(P.ptr, I, sp["leaves"], sp["roots"], sp["branches"])
+        rec("tree", P)
+        ctx.dev_inject_faults(P.ptr, I, sp["shards"], spitch, d_corrupt)
+        rec("fault", P)
+        evP[t % nsets].record(P)
+        if t >= 1:
+            sv = sets[(t - 1) % nsets]
+            V.wait(evP[(t - 1) % nsets])
+            rec("v0", V)
+            ctxV.dev_verify(V.ptr, I, sv["shards"], spitch, None, S, sv["branches"], sv["roots"], d_present,
+                            sv["valid"], sv["leaves_r"])
+            rec("verify", V)
+            evV[(t - 1) % nsets].record(V)
+        if t >= 2:
+            sr = sets[(t - 2) % nsets]
+            R.wait(evV[(t - 2) % nsets])
+            rec("r0", R)
+            ctx.dev_interpolate(R.ptr, I, sr["shards"], spitch, None, S, sr["valid"], sr["leaves_r"], 1,
+                                sr["roots"], d_out, opitch, d_digests, d_status)
+            rec("interp", R)
+            if gather:
+                ctx.dev_allgather_records(R.ptr, I, slots, sr["roots"], d_digests, d_status, d_gather)
+            rec("gather", R)
+            evR[(t - 2) % nsets].record(R)
 
     def pstep(t, ev=None):
         P, R = stream, rstream
         recP = (lambda name: ev[name].record(P)) if ev is not None else (lambda name: None)
         recR = (lambda name: ev[name].record(R)) if ev is not None else (lambda name: None)
-        sp = sets[t % 2]
-        P.wait(evR[t % 2])
+        sp = sets[t % nsets]
+        P.wait(evR[t % nsets])
         recP("t0")
         ctx.dev_encode(P.ptr, I, d_values, vpitch, None, B, sp["shards"], spitch)
         recP("enc")
@@ -358,11 +421,11 @@ def main(argv):
         recP("tree")
         ctx.dev_inject_faults(P.ptr, I, sp["shards"], spitch, d_corrupt)
         recP("fault")
-        evP[t % 2].record(P)
+        evP[t % nsets].record(P)
         if t == 0:
             return
-        sr = sets[(t - 1) % 2]
-        R.wait(evP[(t - 1) % 2])
+        sr = sets[(t - 1) % nsets]
+        R.wait(evP[(t - 1) % nsets])
         recR("r0")
         ctx.dev_verify(R.ptr, I, sr["shards"], spitch, None, S, sr["branches"], sr["roots"], d_present, d_valid,
                        d_leaves_r)
@@ -373,19 +436,21 @@ def main(argv):
         if gather:
             ctx.dev_allgather_records(R.ptr, I, slots, sr["roots"], d_digests, d_status, d_gather)
         recR("gather")
-        evR[(t - 1) % 2].record(R)
+        evR[(t - 1) % nsets].record(R)
 
     def barrier():
         if rstream is not None:
             rstream.sync()
+        if vstream is not None:
+            vstream.sync()
         stream.sync()
         ca.rbc.lib.rbc_device_sync(dev)
         rdz.barrier()
 
     if pipe:
-        args.warmup = max(args.warmup, 2)  # fill the pipeline: at least one decode before the guard
+        args.warmup = max(args.warmup, 3 if pipe3 else 2)  # fill the pipeline: a decode before the guard
         for t in range(args.warmup):
-            pstep(t)
+            (pstep3 if pipe3 else pstep)(t)
     else:
         for _ in range(args.warmup):
             step(None)
@@ -396,14 +461,15 @@ def main(argv):
     t0 = time.perf_counter()
     if pipe:
         for t in range(args.warmup, args.warmup + args.steps):
-            pstep(t, ev_sets[t - args.warmup])
+            (pstep3 if pipe3 else pstep)(t, ev_sets[t - args.warmup])
     else:
         for t in range(args.steps):
             step(ev_sets[t])
     barrier()
     elapsed = time.perf_counter() - t0
     elapsed_max = rdz.max(elapsed)
-    last = sets[(args.warmup + args.steps - 2) % 2] if pipe else sets[0]  # the set the last decode read
+    # the set the last decode read
+    last = sets[(args.warmup + args.steps - (3 if pipe3 else 2)) % nsets] if pipe else sets[0]
     for ev in ev_sets[: args.steps]:
         spans = pipe_spans if pipe else zip(stage_names[:-1], stage_names[1:])
         for a, b in spans:
@@ -538,7 +604,10 @@ def main(argv):
                    "gf_codec": ctx.codec,
                    **({"rehearsal": "all ranks on device 0, no RCCL (not a multi-GPU measurement)"}
                       if args.rehearse_on_one_gpu else {}),
-                   "pipeline": "commit(t) || verify+interpolate(t-1) on two streams" if pipe else "serial"},
+                   "pipeline": ((f"commit(t) || verify(t-1) || interpolate(t-2) on three streams, {nsets} shard "
+                                 "sets") if pipe3 else
+                                (f"commit(t) || verify+interpolate(t-1) on two streams, {nsets} shard sets")
+                                if pipe else "serial")},
         "stage_ms": {kk: round(v, 4) for kk, v in stage_ms.items()},
         "phases": phases,
         **checks,

@@ -47,6 +47,8 @@ _SIGS = {
     "rbc_host_free": (c_int, [c_void_p]),
     "rbc_stream_create": (c_int, [c_int, POINTER(c_void_p)]),
     "rbc_stream_create_priority": (c_int, [c_int, c_int, POINTER(c_void_p)]),
+    "rbc_stream_create_cu_mask": (c_int, [c_int, c_void_p, c_int, POINTER(c_void_p)]),
+    "rbc_device_cu_count": (c_int, [c_int, POINTER(c_int)]),
     "rbc_stream_destroy": (c_int, [c_void_p]),
     "rbc_stream_sync": (c_int, [c_void_p]),
     "rbc_event_create": (c_int, [POINTER(c_void_p)]),

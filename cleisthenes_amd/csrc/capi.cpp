@@ -868,6 +868,21 @@ int rbc_stream_create_priority(int device, int high, void **stream) {
     *stream = s;
     return RBC_OK;
 }
+int rbc_stream_create_cu_mask(int device, const uint32_t *mask, int words, void **stream) {
+    if (!stream || !mask || words < 1) return RBC_ERR_INVALID_ARG;
+    RBC_HIP(hipSetDevice(device));
+    hipStream_t s;
+    RBC_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask));
+    *stream = s;
+    return RBC_OK;
+}
+int rbc_device_cu_count(int device, int *cus) {
+    if (!cus) return RBC_ERR_INVALID_ARG;
+    int v = 0;
+    RBC_HIP(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device));
+    *cus = v;
+    return RBC_OK;
+}
 int rbc_stream_destroy(void *stream) { RBC_HIP(hipStreamDestroy(as_stream(stream))); return RBC_OK; }
 int rbc_stream_sync(void *stream) { RBC_HIP(hipStreamSynchronize(as_stream(stream))); return RBC_OK; }
 int rbc_event_create(void **event) {

@@ -34,6 +34,12 @@ def _ptr(a: np.ndarray) -> c_void_p:
     return c_void_p(a.ctypes.data)
 
 
+def cu_count(device: int = 0) -> int:
+    v = c_int(0)
+    check(lib.rbc_device_cu_count(device, byref(v)), "rbc_device_cu_count")
+    return v.value
+
+
 def pci_bus_id(device: int) -> str:
     buf = ctypes.create_string_buffer(64)
     check(lib.rbc_device_pci_bus_id(device, buf, 64), "rbc_device_pci_bus_id")
@@ -102,11 +108,18 @@ class DeviceBuffer:
 
 
 class Stream:
-    def __init__(self, device: int = 0, priority: Optional[str] = None):
+    def __init__(self, device: int = 0, priority: Optional[str] = None, cu_mask: Optional[Sequence[int]] = None):
         """priority None: default stream priority; "high" / "low": the device's
-        greatest / least (rbc_stream_create_priority)."""
+        greatest / least (rbc_stream_create_priority).  cu_mask: the CU ids
+        this stream's kernels may run on (rbc_stream_create_cu_mask)."""
         p = c_void_p()
-        if priority is None:
+        if cu_mask is not None:
+            words = np.zeros((max(cu_mask) // 32) + 1, dtype=np.uint32)
+            for cu in cu_mask:
+                words[cu // 32] |= np.uint32(1 << (cu % 32))
+            check(lib.rbc_stream_create_cu_mask(device, _ptr(words), len(words), byref(p)),
+                  "rbc_stream_create_cu_mask")
+        elif priority is None:
             check(lib.rbc_stream_create(device, byref(p)), "rbc_stream_create")
         else:
             check(lib.rbc_stream_create_priority(device, 1 if priority == "high" else 0, byref(p)),

@@ -97,6 +97,11 @@ int rbc_stream_create(int device, void **stream);
 /* high != 0: the device's greatest stream priority (its waves are dispatched
  * ahead of normal-priority streams' when both have work queued), else the least. */
 int rbc_stream_create_priority(int device, int high, void **stream);
+/* A stream whose kernels run only on the CUs set in mask (bit i of word i/32 =
+ * CU i, `words` 32-bit words; hipExtStreamCreateWithCUMask): lets two
+ * concurrent pipeline stages own disjoint CUs instead of sharing every CU. */
+int rbc_stream_create_cu_mask(int device, const uint32_t *mask, int words, void **stream);
+int rbc_device_cu_count(int device, int *cus);
 int rbc_stream_destroy(void *stream);
 int rbc_stream_sync(void *stream);
 int rbc_event_create(void **event);
