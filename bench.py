@@ -406,12 +406,25 @@ def main(argv):
             rec("gather", R)
             evR[(t - 2) % nsets].record(R)
 
+    # RBC_BENCH_PWAIT=verify (A/B knob, needs >= 3 sets): commit(t) starts when
+    # the receiver finished VERIFYING batch t-2 (which implies decode(t-3),
+    # the last reader of set t % nsets, is done) instead of when it finished
+    # decoding t-2: the commit then overlaps the decode's tail, not its head
+    pwait_verify = os.environ.get("RBC_BENCH_PWAIT", "") == "verify" and nsets >= 3
+    evRV = [ca.Event() for _ in range(nsets)]
+    for e in evRV:
+        e.record(stream)
+
     def pstep(t, ev=None):
         P, R = stream, rstream
         recP = (lambda name: ev[name].record(P)) if ev is not None else (lambda name: None)
         recR = (lambda name: ev[name].record(R)) if ev is not None else (lambda name: None)
         sp = sets[t % nsets]
-        P.wait(evR[t % nsets])
+        if pwait_verify:
+            if t >= 2:
+                P.wait(evRV[(t - 2) % nsets])
+        else:
+            P.wait(evR[t % nsets])
         recP("t0")
         ctx.dev_encode(P.ptr, I, d_values, vpitch, None, B, sp["shards"], spitch)
         recP("enc")
@@ -430,6 +443,7 @@ def main(argv):
         ctx.dev_verify(R.ptr, I, sr["shards"], spitch, None, S, sr["branches"], sr["roots"], d_present, d_valid,
                        d_leaves_r)
         recR("verify")
+        evRV[(t - 1) % nsets].record(R)
         ctx.dev_interpolate(R.ptr, I, sr["shards"], spitch, None, S, d_valid, d_leaves_r, 1, sr["roots"], d_out,
                             opitch, d_digests, d_status)
         recR("interp")
