@@ -87,7 +87,9 @@ def parse_args(argv):
     ap.add_argument("--pipeline", type=int, default=1,
                     help="1 (default): overlap batch t's commit (proposer stream) with batch t-1's verify + "
                          "interpolate (receiver stream); 2: three streams -- commit(t) || verify(t-1) || "
-                         "interpolate(t-2); 0: one stream, stages in order")
+                         "interpolate(t-2); 3: phase-aligned -- every step runs the SHA phases of three batches "
+                         "together (leaves(t) || verify(t-1) || regen hashing(t-2)), then their GF/FFT/tree "
+                         "phases together; 0: one stream, stages in order")
     ap.add_argument("--sets", type=int, default=0,
                     help="shard buffer sets of the pipelined schedule (0: the minimum, 2 for --pipeline 1, "
                          "3 for --pipeline 2; more let the proposer run further ahead)")
@@ -267,7 +269,8 @@ def main(argv):
     corrupt_h = corrupt_all[first:first + I]
 
     pipe = bool(args.pipeline)
-    pipe3 = args.pipeline == 2
+    pipe3 = args.pipeline in (2, 3)  # per-set valid / verified leaves, >= 3 sets
+    phased = args.pipeline == 3
     # the pipeline holds two shard sets; when they do not fit the 288 GB of
     # HBM (C3 with all 8192 instances on one GPU: 2 x 100 GB + values) run
     # the serial schedule instead
@@ -275,6 +278,8 @@ def main(argv):
     other_bytes = I * (vpitch + opitch + n * 34 + 64)
     if pipe3:
         set_bytes += I * (n + n * 32)  # per-set valid + verified leaves (verify and interpolate run apart)
+    if phased:
+        set_bytes += I * (opitch + 32 + 4)  # per-set value / digest / status (decode and check run apart)
     nsets = max(3 if pipe3 else 2, args.sets) if pipe else 1
     budget = float(os.environ.get("RBC_BENCH_HBM_BUDGET", 250e9))
     while pipe and nsets * set_bytes + other_bytes > budget:
@@ -283,7 +288,9 @@ def main(argv):
             pipe, pipe3, nsets = False, False, 1
     sets = [dict(shards=mb(I * n * spitch), leaves=mb(I * n * 32), roots=mb(I * 32),
                  branches=mb(I * n * max(d, 1) * 32),
-                 **({"valid": mb(I * n), "leaves_r": mb(I * n * 32)} if pipe3 else {})) for _ in range(nsets)]
+                 **({"valid": mb(I * n), "leaves_r": mb(I * n * 32)} if pipe3 else {}),
+                 **({"out": mb(I * opitch), "digests": mb(I * 32), "status": mb(I * 4)} if phased else {}))
+            for _ in range(nsets)]
     d_present = mb(I * n)
     d_present.upload(present_h)
     d_corrupt = mb(I * 4)
@@ -314,7 +321,9 @@ def main(argv):
         pipe_spans = pipe_spans[:4] + (("v0", "verify"), ("r0", "interp"), ("interp", "gather"))
     # one event set per timed step: stage times are read after the closing
     # barrier, so the timed loop never waits on the host between steps
-    ev_sets = [{name: ca.Event() for name in stage_names + ("r0", "v0")} for _ in range(max(args.steps, 3))]
+    ev_sets = [{name: ca.Event() for name in stage_names + ("r0", "v0", "l0", "g0", "regen", "t0b", "e0",
+                                                            "d0", "decode", "c0", "check")}
+               for _ in range(max(args.steps, 3))]
 
     def step(ev, sp=None):
         sp = sp or sets[0]
@@ -361,7 +370,7 @@ def main(argv):
         stream.sync()
         stream = ca.Stream(dev, cu_mask=[c for c in range(ncu) if c % b_ < a_])
         rstream = ca.Stream(dev, cu_mask=[c for c in range(ncu) if c % b_ >= a_])
-    vstream = ca.Stream(dev) if pipe3 else None
+    vstream = ca.Stream(dev) if pipe3 else None  # --pipeline 2: verify stream V; 3: stream Z
     ctxV = ca.Context(n, f, device=dev) if pipe3 else None  # own decode/verify workspace per stream
     evP = [ca.Event() for _ in range(nsets)]
     evR = [ca.Event() for _ in range(nsets)]
@@ -452,6 +461,81 @@ def main(argv):
         recR("gather")
         evR[(t - 1) % nsets].record(R)
 
+    # --pipeline 3: phase-aligned schedule on three streams X, Y, Z.  Step k:
+    #   SHA phase     X: leaves(k)        Y: verify(k-1)     Z: rehash(k-2)
+    #   non-SHA phase X: tree+fault(k),   Y: decode(k-1)     Z: check(k-2)
+    #                    encode(k+1)         (prepare, GF,       (+ gather)
+    #                                         FFT, join)
+    # Every stream waits for all three streams' previous phase, so the SHA
+    # kernels of three batches (2048 + 1376 + 672 waves at C2: four per SIMD)
+    # run together and the GF/FFT transforms run together -- two SHA kernels
+    # share CUs well, a transform beside SHA does not.
+    # Set k % nsets is rewritten by encode(k+1)'s set only after rehash(k-2).
+    if phased:
+        X, Y, Z = stream, rstream, vstream
+        evA = {nm: ca.Event() for nm in ("X", "Y", "Z")}  # end of a SHA phase, per stream
+        evB = {nm: ca.Event() for nm in ("X", "Y", "Z")}  # end of a non-SHA phase, per stream
+        for e in list(evA.values()) + list(evB.values()):
+            e.record(stream)
+        # encode(0) before the first step
+        ctx.dev_encode(X.ptr, I, d_values, vpitch, None, B, sets[0]["shards"], spitch)
+        evB["X"].record(X)
+
+    def phase_wait(st, evs):
+        for e in evs.values():
+            st.wait(e)
+
+    def pstep_phased(k, ev=None):
+        rec = (lambda name, st: ev[name].record(st)) if ev is not None else (lambda name, st: None)
+        sk, s1, s2 = sets[k % nsets], sets[(k - 1) % nsets], sets[(k - 2) % nsets]
+        # ---- SHA phase
+        for st in (X, Y, Z):
+            phase_wait(st, evB)
+        rec("l0", X)
+        ctx.dev_leaves(X.ptr, I, sk["shards"], spitch, None, S, sk["leaves"])
+        rec("leaf", X)
+        if k >= 1:
+            rec("v0", Y)
+            ctxV.dev_verify(Y.ptr, I, s1["shards"], spitch, None, S, s1["branches"], s1["roots"], d_present,
+                            s1["valid"], s1["leaves_r"])
+            rec("verify", Y)
+        if k >= 2:
+            rec("g0", Z)
+            ctx.dev_interpolate_phases(Z.ptr, ctx.INTERP_REHASH, I, s2["shards"], spitch, None, S, s2["valid"],
+                                       s2["leaves_r"], 1, s2["roots"], s2["out"], opitch, s2["digests"],
+                                       s2["status"])
+            rec("regen", Z)
+        for nm, st in (("X", X), ("Y", Y), ("Z", Z)):
+            evA[nm].record(st)
+        # ---- non-SHA phase
+        for st in (X, Y, Z):
+            phase_wait(st, evA)
+        rec("t0b", X)
+        ctx.dev_merkle_build(X.ptr, I, sk["leaves"], sk["roots"], sk["branches"])
+        rec("tree", X)
+        ctx.dev_inject_faults(X.ptr, I, sk["shards"], spitch, d_corrupt)
+        rec("fault", X)
+        rec("e0", X)
+        ctx.dev_encode(X.ptr, I, d_values, vpitch, None, B, sets[(k + 1) % nsets]["shards"], spitch)
+        rec("enc", X)
+        if k >= 1:
+            rec("d0", Y)
+            ctx.dev_interpolate_phases(Y.ptr, ctx.INTERP_DECODE, I, s1["shards"], spitch, None, S, s1["valid"],
+                                       s1["leaves_r"], 1, s1["roots"], s1["out"], opitch, s1["digests"],
+                                       s1["status"])
+            rec("decode", Y)
+        if k >= 2:
+            rec("c0", Z)
+            ctx.dev_interpolate_phases(Z.ptr, ctx.INTERP_CHECK, I, s2["shards"], spitch, None, S, s2["valid"],
+                                       s2["leaves_r"], 1, s2["roots"], s2["out"], opitch, s2["digests"],
+                                       s2["status"])
+            rec("check", Z)
+            if gather:
+                ctx.dev_allgather_records(Z.ptr, I, slots, s2["roots"], s2["digests"], s2["status"], d_gather)
+            rec("gather", Z)
+        for nm, st in (("X", X), ("Y", Y), ("Z", Z)):
+            evB[nm].record(st)
+
     def barrier():
         if rstream is not None:
             rstream.sync()
@@ -464,7 +548,7 @@ def main(argv):
     if pipe:
         args.warmup = max(args.warmup, 3 if pipe3 else 2)  # fill the pipeline: a decode before the guard
         for t in range(args.warmup):
-            (pstep3 if pipe3 else pstep)(t)
+            (pstep_phased if phased else pstep3 if pipe3 else pstep)(t)
     else:
         for _ in range(args.warmup):
             step(None)
@@ -475,7 +559,7 @@ def main(argv):
     t0 = time.perf_counter()
     if pipe:
         for t in range(args.warmup, args.warmup + args.steps):
-            (pstep3 if pipe3 else pstep)(t, ev_sets[t - args.warmup])
+            (pstep_phased if phased else pstep3 if pipe3 else pstep)(t, ev_sets[t - args.warmup])
     else:
         for t in range(args.steps):
             step(ev_sets[t])
@@ -484,14 +568,22 @@ def main(argv):
     elapsed_max = rdz.max(elapsed)
     # the set the last decode read
     last = sets[(args.warmup + args.steps - (3 if pipe3 else 2)) % nsets] if pipe else sets[0]
+    if phased:
+        pipe_spans = (("e0", "enc"), ("l0", "leaf"), ("t0b", "tree"), ("tree", "fault"), ("v0", "verify"),
+                      ("d0", "decode"), ("g0", "regen"), ("c0", "check"), ("check", "gather"))
+        stage_ms.update(decode=0.0, regen=0.0, check=0.0)
     for ev in ev_sets[: args.steps]:
         spans = pipe_spans if pipe else zip(stage_names[:-1], stage_names[1:])
         for a, b in spans:
             stage_ms[b] += ev[a].elapsed_ms(ev[b]) / args.steps
+    if phased:  # interpolate = its three phases
+        stage_ms["interp"] = stage_ms.pop("decode") + stage_ms.pop("regen") + stage_ms.pop("check")
 
     # ---- correctness of the timed run's last round (outside the timed region)
+    res_out, res_status, res_dig = ((last["out"], last["status"], last["digests"]) if phased
+                                    else (d_out, d_status, d_digests))
     checks = check_results(args, ca, acs, synth, rdz, ctx, dev, stream, world, rank, first, I, total, slots, n, f,
-                           k, B, S, vpitch, opitch, d_values, d_out, d_status, d_digests, last["roots"],
+                           k, B, S, vpitch, opitch, d_values, res_out, res_status, res_dig, last["roots"],
                            d_gather, d_count, gather)
 
     ms_per_step = elapsed_max * 1000.0 / args.steps
@@ -618,7 +710,9 @@ def main(argv):
                    "gf_codec": ctx.codec,
                    **({"rehearsal": "all ranks on device 0, no RCCL (not a multi-GPU measurement)"}
                       if args.rehearse_on_one_gpu else {}),
-                   "pipeline": ((f"commit(t) || verify(t-1) || interpolate(t-2) on three streams, {nsets} shard "
+                   "pipeline": ((f"phase-aligned: SHA of leaves(t) || verify(t-1) || rehash(t-2), then tree/encode "
+                                 f"|| decode(t-1) || check(t-2), three streams, {nsets} shard sets") if phased else
+                                (f"commit(t) || verify(t-1) || interpolate(t-2) on three streams, {nsets} shard "
                                  "sets") if pipe3 else
                                 (f"commit(t) || verify+interpolate(t-1) on two streams, {nsets} shard sets")
                                 if pipe else "serial")},

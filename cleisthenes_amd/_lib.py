@@ -67,6 +67,9 @@ _SIGS = {
                                c_void_p, c_void_p, c_void_p, c_void_p]),
     "rbc_dev_interpolate": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_uint32, c_void_p, c_uint32, c_void_p,
                                     c_void_p, c_int, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p]),
+    "rbc_dev_interpolate_phases": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_uint32, c_void_p, c_uint32,
+                                           c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_uint32, c_void_p,
+                                           c_void_p]),
     "rbc_dev_inject_faults": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_uint32, c_void_p]),
     "rbc_shard_commit": (c_int, [c_void_p, c_int, c_void_p, szp, c_void_p, c_size_t, u32p, c_void_p, c_void_p,
                                  POINTER(c_uint64)]),

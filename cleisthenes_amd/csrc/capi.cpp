@@ -579,10 +579,17 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
     return RBC_OK;
 }
 
+// interpolate phases: 1 = decode (prepare, missing-data GF, FFT re-encode +
+// compare, value join), 2 = rehash (SHA of the regenerated rows), 4 = check
+// (Merkle root recheck + batch digest).  All three (7) is rbc_dev_interpolate;
+// the join then forks onto the aux stream beside the rehash.
+constexpr int kPhaseDecode = 1, kPhaseRehash = 2, kPhaseCheck = 4, kPhaseAll = 7;
+
 int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shards, uint32_t shard_pitch,
                       const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *valid, uint8_t *leaves,
                       int leaves_verified, const uint8_t *roots, uint8_t *values_out, uint32_t value_pitch,
-                      uint8_t *digests, int32_t *status) {
+                      uint8_t *digests, int32_t *status, int phases = kPhaseAll) {
+    if (phases < 1 || phases > kPhaseAll) return RBC_ERR_INVALID_ARG;
     if (count < 0 || (count > 0 && (!shards || !valid || !leaves || !roots || !values_out || !status)))
         return RBC_ERR_INVALID_ARG;
     if (shard_pitch % kAlign || value_pitch % 16) return RBC_ERR_INVALID_ARG;
@@ -600,13 +607,14 @@ int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *sha
         return e && atoi(e) != 0;
     }();
     const bool fused_join = fuse_env && c->fft && c->n > c->k;
-    int rc = stage_regenerate(c, w, st, count, shards, shard_pitch, shard_lens, uniform_shard_len, valid, status,
-                              leaves_verified, fused_join ? values_out : nullptr, value_pitch);
-    if (rc) return rc;
     // value assembly (HBM-bound) forks onto the aux stream beside the regen
     // hashing (latency-bound, under-fills the SIMDs); it needs only the
     // regenerated rows.  values_out is defined where status == 0.
-    const bool fork = !fused_join && w.fork;
+    const bool fork = !fused_join && w.fork && phases == kPhaseAll;
+    if (phases & kPhaseDecode) {
+    int rc = stage_regenerate(c, w, st, count, shards, shard_pitch, shard_lens, uniform_shard_len, valid, status,
+                              leaves_verified, fused_join ? values_out : nullptr, value_pitch);
+    if (rc) return rc;
     if (!fused_join) {
     hipStream_t js = st;
     if (fork) {
@@ -633,6 +641,7 @@ int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *sha
     }
     if (fork) RBC_HIP(hipEventRecord(w.ev_join, w.aux));
     }
+    }  // decode phase
     const int nr = c->n - c->k;
     ShaArgs a{};
     a.count = count;
@@ -655,7 +664,8 @@ int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *sha
     } else {
         a.rows_per_inst = c->n;
     }
-    if (a.rows_per_inst > 0) RBC_HIP(rbc_launch_sha_rows(a, false, st));
+    if ((phases & kPhaseRehash) && a.rows_per_inst > 0) RBC_HIP(rbc_launch_sha_rows(a, false, st));
+    if (phases & kPhaseCheck) {
     MerkleArgs m{};
     m.count = count;
     m.n = c->n;
@@ -669,6 +679,7 @@ int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *sha
     RBC_HIP(rbc_launch_merkle(m, true, st));
     if (digests)
         RBC_HIP(rbc_launch_digest(leaves, (uint64_t)c->n * 32, c->k, status, digests, count, st));
+    }  // check phase
     if (fork) RBC_HIP(hipStreamWaitEvent(st, w.ev_join, 0));  // join back before returning
     return RBC_OK;
 }
@@ -966,11 +977,20 @@ int rbc_dev_interpolate(rbc_ctx *c, void *stream, int count, uint8_t *shards, ui
                         const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *valid,
                         uint8_t *leaves, int leaves_verified, const uint8_t *roots, uint8_t *values_out,
                         uint32_t value_pitch, uint8_t *digests, int32_t *status) {
+    return rbc_dev_interpolate_phases(c, stream, kPhaseAll, count, shards, shard_pitch, shard_lens,
+                                      uniform_shard_len, valid, leaves, leaves_verified, roots, values_out,
+                                      value_pitch, digests, status);
+}
+
+int rbc_dev_interpolate_phases(rbc_ctx *c, void *stream, int phases, int count, uint8_t *shards,
+                               uint32_t shard_pitch, const uint32_t *shard_lens, uint32_t uniform_shard_len,
+                               const uint8_t *valid, uint8_t *leaves, int leaves_verified, const uint8_t *roots,
+                               uint8_t *values_out, uint32_t value_pitch, uint8_t *digests, int32_t *status) {
     if (!c) return RBC_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(c->mu);  // shared decode workspace
     RBC_HIP(hipSetDevice(c->device));
-    return stage_interpolate(c, c->ws, as_stream(stream), count, shards, shard_pitch, shard_lens, uniform_shard_len, valid,
-                             leaves, leaves_verified, roots, values_out, value_pitch, digests, status);
+    return stage_interpolate(c, c->ws, as_stream(stream), count, shards, shard_pitch, shard_lens, uniform_shard_len,
+                             valid, leaves, leaves_verified, roots, values_out, value_pitch, digests, status, phases);
 }
 
 size_t rbc_val_message_size(int n, uint32_t shard_len, uint32_t index, int type) {

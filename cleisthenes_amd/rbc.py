@@ -430,6 +430,15 @@ class Context:
                                       _dv(values_out), value_pitch, _dv(digests), _dv(status)),
               "rbc_dev_interpolate")
 
+    INTERP_DECODE, INTERP_REHASH, INTERP_CHECK = 1, 2, 4
+
+    def dev_interpolate_phases(self, stream, phases, count, shards, shard_pitch, shard_lens, uniform_len, valid,
+                               leaves, leaves_verified, roots, values_out, value_pitch, digests, status):
+        check(lib.rbc_dev_interpolate_phases(self._p, _dv(stream), phases, count, _dv(shards), shard_pitch,
+                                             _dv(shard_lens), uniform_len, _dv(valid), _dv(leaves),
+                                             int(leaves_verified), _dv(roots), _dv(values_out), value_pitch,
+                                             _dv(digests), _dv(status)), "rbc_dev_interpolate_phases")
+
     def dev_marshal_val(self, stream, count, msg_type, shards, shard_pitch, shard_lens, uniform_len, branches,
                         roots, out, out_pitch, out_lens):
         """Per-recipient VAL / ECHO pb.Message bytes in HBM (include/rbc_protocol.h)."""

@@ -160,6 +160,22 @@ int rbc_dev_interpolate(rbc_ctx *ctx, void *stream, int count, uint8_t *shards, 
                         const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *valid,
                         uint8_t *leaves, int leaves_verified, const uint8_t *roots, uint8_t *values_out,
                         uint32_t value_pitch, uint8_t *digests, int32_t *status);
+/* The same interpolate split into its three phases, for schedulers that
+ * interleave batches (bench.py --pipeline 3 runs every SHA phase of three
+ * batches together): phases is a mask of RBC_INTERP_DECODE (decode_prepare,
+ * missing-data GF, FFT re-encode + compare of the valid-but-unused rows, value
+ * join), RBC_INTERP_REHASH (SHA-256 of the regenerated rows) and
+ * RBC_INTERP_CHECK (Merkle root recheck + batch digest).  A batch's phases
+ * run in that order; between its DECODE and REHASH no other DECODE may run on
+ * this context (they share its decode workspace).  status / values_out /
+ * leaves are per batch and must stay untouched by other batches in between. */
+#define RBC_INTERP_DECODE 1
+#define RBC_INTERP_REHASH 2
+#define RBC_INTERP_CHECK 4
+int rbc_dev_interpolate_phases(rbc_ctx *ctx, void *stream, int phases, int count, uint8_t *shards,
+                               uint32_t shard_pitch, const uint32_t *shard_lens, uint32_t uniform_shard_len,
+                               const uint8_t *valid, uint8_t *leaves, int leaves_verified, const uint8_t *roots,
+                               uint8_t *values_out, uint32_t value_pitch, uint8_t *digests, int32_t *status);
 /* Synthetic Byzantine input for tests/bench: shards[i][corrupt[i]][0] ^= 0x5a
  * for every i with corrupt[i] >= 0 (corrupt: device int32[count]). */
 int rbc_dev_inject_faults(rbc_ctx *ctx, void *stream, int count, uint8_t *shards, uint32_t shard_pitch,
