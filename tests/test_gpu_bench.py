@@ -1,0 +1,32 @@
+"""bench.py end to end on the GPU at a small batch: every schedule
+(--pipeline 0 serial, 1 two-stream default, 2 three-stream, 3 phase-aligned)
+must pass the bench's own correctness guard (all instances decode, every
+decoded value equals its input, sampled roots / digests equal the C oracle;
+the bench exits 3 otherwise) and print exactly one JSON line with the
+contract keys."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("pipeline", [0, 1, 2, 3])
+def test_bench_schedules_pass_their_guard(pipeline):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "3", "--instances", "96",
+           "--pipeline", str(pipeline), "--no-cpu-baseline", "--no-pcie", "--oracle-samples", "4"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert key in d, key
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["value"] > 0
+    assert d["decoded_ok"] == 96 and d["values_ok"] and d["oracle_sample_ok"] and d["oracle_samples_checked"] == 4
+    assert 0 < d["roofline"]["frac"] < 1 and d["roofline"]["avg_ms"] > 0

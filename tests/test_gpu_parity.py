@@ -790,3 +790,42 @@ def test_merkle_build_branches_every_depth(gpu, ref, n, f):
         _, want_root, want_br, _ = ref.encode_commit(n, f, pl.values[i, :B])
         assert bytes(roots[i]) == want_root, (n, i)
         assert np.array_equal(brs[i], want_br), (n, i)
+
+
+@pytest.mark.parametrize("n,f,B,I", [(128, 42, 1 << 16, 96), (16, 5, 3001, 64), (256, 85, 86 * 40, 48)])
+def test_interpolate_phases_equal_one_shot(gpu, ref, n, f, B, I):
+    """rbc_dev_interpolate_phases (decode, rehash, check as three calls,
+    as --pipeline 3 schedules them) produces exactly the one-shot
+    rbc_dev_interpolate's values, digests, statuses and leaves, corrupted
+    ECHO shards and wrong committed roots included; sampled instances are
+    also checked against the C oracle."""
+    outs = []
+    for phased in (False, True):
+        pl = Pipeline(gpu, n, f, B, I, seed=n + B, corrupt_frac=0.3)
+        pl.commit()
+        b, c = pl.b, pl.ctx
+        c.dev_inject_faults(None, I, b["shards"], pl.spitch, b["corrupt"])
+        c.dev_verify(None, I, b["shards"], pl.spitch, None, pl.S, b["branches"], b["roots"], b["present"],
+                     b["valid"], b["leaves_r"])
+        roots = pl.arr("roots", shape=(I, 32)).copy()
+        roots[::7, 0] ^= 0x80  # interpolate's recheck against a wrong root every 7th instance
+        b["roots"].upload(roots)
+        args = (I, b["shards"], pl.spitch, None, pl.S, b["valid"], b["leaves_r"], 1, b["roots"], b["out"],
+                pl.opitch, b["digests"], b["status"])
+        if phased:
+            for ph in (c.INTERP_DECODE, c.INTERP_REHASH, c.INTERP_CHECK):
+                c.dev_interpolate_phases(None, ph, *args)
+        else:
+            c.dev_interpolate(None, *args)
+        gpu.rbc.lib.rbc_device_sync(0)
+        st = pl.arr("status", np.int32)
+        ok = st == 0
+        outs.append((st, pl.arr("out", shape=(I, pl.opitch))[:, : pl.k * pl.S][ok],
+                     pl.arr("digests", shape=(I, 32))[ok], pl.arr("leaves_r", shape=(I, n, 32)), pl))
+    (s0, v0, d0, l0, pl), (s1, v1, d1, l1, _) = outs
+    assert np.array_equal(s0, s1) and set(s0[::7]) == {-8} and (s0[np.arange(I) % 7 != 0] == 0).all()
+    assert np.array_equal(v0, v1) and np.array_equal(d0, d1) and np.array_equal(l0, l1)
+    for i in (1, 2, I - 1):
+        if i % 7 == 0:
+            continue
+        assert bytes(pl.values[i, :B]) == bytes(v1[np.cumsum(s1 == 0)[i] - 1][:B])
