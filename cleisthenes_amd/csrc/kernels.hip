@@ -175,6 +175,7 @@ __global__ __launch_bounds__(TPB, (RC <= 21 ? 3 : 2)) void gf_rows_kernel(GfArgs
             const GfSel sb0 = gf_sel(xb.x), sb1 = gf_sel(xb.y), sb2 = gf_sel(xb.z), sb3 = gf_sel(xb.w);
 #pragma unroll
             for (int r = 0; r < RC; ++r) {
+                if (r >= rows) break;  // block-uniform: a short last chunk skips its padding rows
                 const uint4 ta = s_t01[j * RC + r];
                 const uint4 tb = s_t01[(j + 1) * RC + r];
                 const uint2 t2 = *reinterpret_cast<const uint2 *>(&s_t2[((j >> 1) * RC + r) * 2]);
@@ -279,6 +280,7 @@ __global__ __launch_bounds__(64) void gf_short_kernel(GfArgs a) {
         const GfSel sb0 = gf_sel(xb.x), sb1 = gf_sel(xb.y), sb2 = gf_sel(xb.z);
 #pragma unroll
         for (int r = 0; r < RC; ++r) {
+            if (r >= rows) break;  // block-uniform (see gf_rows_kernel)
             const uint4 ta = s_t01[j * RC + r];
             const uint4 tb = s_t01[(j + 1) * RC + r];
             const uint2 t2 = *reinterpret_cast<const uint2 *>(&s_t2[((j >> 1) * RC + r) * 2]);
