@@ -12,6 +12,9 @@
   S < 16, S % 64 == 0 and SHA-256 padding boundaries, N = 1, f = 0,
   non-power-of-two N, too few shards, Byzantine non-codeword commitments.
 All comparisons are bit-exact (integer/byte work)."""
+import os
+import zlib
+
 import numpy as np
 import pytest
 
@@ -247,7 +250,7 @@ FULL = [
 
 @pytest.mark.parametrize("name,n,f,B,I", FULL, ids=[x[0] for x in FULL])
 def test_device_pipeline_full_size_vs_c_oracle(gpu, ref, name, n, f, B, I):
-    pl = Pipeline(gpu, n, f, B, I, seed=hash(name) & 0xffff)
+    pl = Pipeline(gpu, n, f, B, I, seed=zlib.crc32(name.encode()))
     pl.commit()
     sh = pl.shards()
     roots = pl.arr("roots", shape=(I, 32))
@@ -282,6 +285,56 @@ def test_device_pipeline_full_size_vs_c_oracle(gpu, ref, name, n, f, B, I):
         # round-trip property: the decoded value is the proposer's input
         assert out[i, :B].tobytes() == pl.values[i, :B].tobytes()
         assert not out[i, B: pl.k * S].any()
+
+
+BATCH = [
+    ("c1", 64, 21, 1 << 20, 1024),
+    ("c2", 128, 42, 1 << 20, 1024),
+    ("c3", 128, 42, 4 << 20, 256),
+    ("c4", 256, 85, 64 << 10, 4096),
+]
+
+
+@pytest.mark.parametrize("name,n,f,B,I", BATCH, ids=[x[0] for x in BATCH])
+def test_device_pipeline_every_instance_of_a_bench_batch_vs_c_oracle(gpu, ref, name, n, f, B, I):
+    """Every instance of a bench-sized batch against the C restatement: root,
+    leaves and the branch of a rotating leaf after commit; valid mask, status,
+    value (k*S bytes) and digest after receive (one corrupted ECHO shard in
+    10% of instances).  The oracle runs on a thread pool (ctypes releases the
+    GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    pl = Pipeline(gpu, n, f, B, I, seed=zlib.crc32(name.encode()))
+    pl.commit()
+    sh = pl.shards()
+    roots = pl.arr("roots", shape=(I, 32))
+    leaves = pl.arr("leaves", shape=(I, n, 32))
+    brs = pl.arr("branches", shape=(I, n, max(pl.d, 1), 32))
+    pl.receive()
+    valid = pl.arr("valid", shape=(I, n))
+    status = pl.arr("status", np.int32)
+    out = pl.arr("out", shape=(I, pl.opitch))
+    digests = pl.arr("digests", shape=(I, 32))
+    S, k = pl.S, pl.k
+
+    def check(i):
+        _, want_root, want_br, want_leaves = ref.encode_commit(n, f, pl.values[i, :B])
+        j = i % n
+        ok = (bytes(roots[i]) == want_root and np.array_equal(leaves[i], want_leaves) and
+              np.array_equal(brs[i, j, :pl.d], want_br[j]))
+        exp_valid = pl.present[i].copy()
+        rx = sh[i, :, :S].copy()
+        if pl.corrupt[i] >= 0:
+            exp_valid[pl.corrupt[i]] = 0
+            rx[pl.corrupt[i], 0] ^= 0x5A
+        rc, value, dig = ref.interpolate(n, f, rx, exp_valid, want_root)
+        ok = ok and np.array_equal(valid[i], exp_valid) and status[i] == rc == 0
+        ok = ok and np.array_equal(out[i, :k * S], value) and bytes(digests[i]) == dig
+        return ok
+
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+        bad = [i for i, ok in enumerate(ex.map(check, range(I))) if not ok]
+    assert not bad, (name, bad[:10])
+    assert np.array_equal(out[:, :B], pl.values[:, :B])
 
 
 def test_device_pipeline_many_instances_properties(gpu, ref):
