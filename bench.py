@@ -97,6 +97,9 @@ def parse_args(argv):
                     help="shard row pitch alignment in bytes (multiple of 64; the C ABI needs 64)")
     ap.add_argument("--force-gather", action="store_true",
                     help="run the RCCL all-gather even with one rank (exercises rbc_comm_*)")
+    ap.add_argument("--no-isolated", action="store_true",
+                    help="skip the 5 serial steps before the warmup that time each kernel alone on the chip "
+                         "(roofline.isolated)")
     ap.add_argument("--no-pcie", action="store_true",
                     help="skip the PCIe-inclusive host-path measurement (a secondary key, never `value`)")
     ap.add_argument("--rehearse-on-one-gpu", action="store_true",
@@ -545,6 +548,21 @@ def main(argv):
         ca.rbc.lib.rbc_device_sync(dev)
         rdz.barrier()
 
+    # the same kernels alone on the chip (serial schedule, events per stage),
+    # BEFORE the warmup so that the timed launches stay the last ones a
+    # rocprof trace holds: under the pipeline a kernel's span also holds the
+    # other stream's work, so the roofline carries both figures
+    iso_ms = None
+    if pipe and not phased and not args.no_isolated:
+        for _ in range(2):
+            step(None)
+        iso_ev = ev_sets[:3]
+        for ev in iso_ev:
+            step(ev)
+        stream.sync()
+        iso_ms = {b_: sum(ev[a_].elapsed_ms(ev[b_]) for ev in iso_ev) / len(iso_ev)
+                  for a_, b_ in zip(stage_names[:-1], stage_names[1:])}
+
     if pipe:
         args.warmup = max(args.warmup, 3 if pipe3 else 2)  # fill the pipeline: a decode before the guard
         for t in range(args.warmup):
@@ -660,6 +678,20 @@ def main(argv):
     dom = max(kern, key=lambda x: kern[x][0])
     roof = roofline(dom)
     codec_roof = roofline(enc_kernel)  # north_star: encode against the HBM peak
+    if iso_ms is not None:
+        stage_of = {enc_kernel: "enc", "sha_rows_kernel<leaves>": "leaf", "sha_rows_kernel<verify>": "verify"}
+        for r in (roof, codec_roof):
+            ms_i = iso_ms[stage_of[r["kernel"]]]
+            _, nbytes, ncomp = kern[r["kernel"]]
+            iso = {"avg_ms": round(ms_i, 4), "achieved": round(nbytes / (ms_i / 1e3) / 1e9, 1),
+                   "frac": round(nbytes / (ms_i / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                   "note": "same kernel and batch alone on the chip (3 serial steps before the warmup); "
+                           "avg_ms above is its span under the two-stream pipeline, shared with the other "
+                           "stream's kernels"}
+            if ncomp:
+                cps = ncomp / (ms_i / 1e3)
+                iso["valu_frac_of_attainable"] = round(cps / SHA_PROBE_CPS, 4)
+            r["isolated"] = iso
 
     # GPU phase rates (per rank, from the stage events): encode+commit =
     # N*S shard bytes per instance; verify+decode = k*S value bytes
