@@ -146,6 +146,13 @@ struct Slot {
     uint64_t ticket = 0;
     bool busy = false;
     std::function<int()> finish;
+    // Device-to-host copies of a submission, enqueued only when the NEXT
+    // submission has enqueued its host-to-device copies (or at wait / poll):
+    // the copy engine serves the streams' copies in enqueue order, so a D2H
+    // queued at submit time (it waits on this submission's kernels) would hold
+    // the next submission's H2D behind it and serialise the slots.
+    std::function<int()> d2h;
+    int d2h_rc = 0;
     void release() {
         for (DevBuf *b : {&d_values, &d_shards, &d_leaves, &d_roots, &d_branches, &d_valid, &d_status, &d_digests,
                           &d_lens, &d_slens, &d_idx, &h_in, &h_out})
@@ -791,6 +798,11 @@ void rbc_ctx_destroy(rbc_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     for (auto &sl : c->slots) {
+        if (sl->busy && sl->d2h) {
+            (void)sl->d2h();
+            sl->d2h = nullptr;
+            (void)hipEventRecord(sl->done, sl->stream);
+        }
         if (sl->busy) (void)hipEventSynchronize(sl->done);
         sl->release();
     }
@@ -1064,11 +1076,23 @@ void parallel_for(int count, size_t bytes_per_item, F &&f) {
     for (auto &x : th) x.join();
 }
 
+// Enqueue a submission's deferred device-to-host copies and its completion
+// event (see Slot::d2h).
+void flush_d2h(Slot &s) {
+    if (!s.d2h) return;
+    s.d2h_rc = s.d2h();
+    s.d2h = nullptr;
+    if (hipEventRecord(s.done, s.stream) != hipSuccess && !s.d2h_rc) s.d2h_rc = RBC_ERR_DEVICE;
+}
+
 // Free slot for the next submission: create one while fewer than
 // host_slots() exist, else reuse an idle one, else retire the oldest
 // in-flight submission (its status is kept until the caller waits on it).
 int retire(rbc_ctx *c, Slot &s) {
     int st = RBC_OK;
+    flush_d2h(s);
+    if (s.d2h_rc) st = s.d2h_rc;
+    s.d2h_rc = 0;
     if (hipEventSynchronize(s.done) != hipSuccess) st = RBC_ERR_DEVICE;
     if (st == RBC_OK && s.finish) st = s.finish();
     s.finish = nullptr;
@@ -1098,12 +1122,23 @@ Slot *acquire_slot(rbc_ctx *c) {
 }
 
 // Seal a submission: record its completion event and hand out a ticket, or
-// (ticket == NULL) complete it before returning.
-int submit(rbc_ctx *c, Slot &s, uint64_t *ticket, std::function<int()> finish) {
+// (ticket == NULL) complete it before returning.  With `d2h` the submission's
+// device-to-host copies are deferred (Slot::d2h); the other slots' deferred
+// copies are enqueued now, behind this submission's host-to-device copies.
+int submit(rbc_ctx *c, Slot &s, uint64_t *ticket, std::function<int()> finish,
+           std::function<int()> d2h = nullptr) {
     s.finish = std::move(finish);
-    if (hipEventRecord(s.done, s.stream) != hipSuccess) {
-        s.finish = nullptr;
-        return RBC_ERR_DEVICE;
+    for (auto &o : c->slots)
+        if (o.get() != &s && o->busy) flush_d2h(*o);
+    s.d2h_rc = 0;
+    if (d2h && ticket) {
+        s.d2h = std::move(d2h);
+    } else {
+        const int rc = d2h ? d2h() : RBC_OK;
+        if (rc || hipEventRecord(s.done, s.stream) != hipSuccess) {
+            s.finish = nullptr;
+            return rc ? rc : RBC_ERR_DEVICE;
+        }
     }
     s.ticket = c->next_ticket++;
     s.busy = true;
@@ -1162,12 +1197,18 @@ int rbc_shard_commit(rbc_ctx *c, int count, const uint8_t *const *values, const 
     RBC_HIP(s.d_roots.ensure((size_t)count * 32));
     RBC_HIP(s.d_branches.ensure(br_bytes));
     RBC_HIP(s.d_lens.ensure((size_t)count * 8));
-    RBC_HIP(s.h_in.ensure((size_t)count * vpitch + (size_t)count * 8));
-    RBC_HIP(s.h_out.ensure(sh_bytes + (size_t)count * 32 + br_bytes));
-    uint8_t *stage = s.h_in.as<uint8_t>();
-    uint32_t *lens = reinterpret_cast<uint32_t *>(stage + (size_t)count * vpitch);
+    // pinned staging only for what is not already pinned caller memory
     bool in_direct = true;
     for (int i = 0; i < count && in_direct; ++i) in_direct = host_pinned(values[i], value_lens[i]);
+    const size_t in_stage = in_direct ? 0 : (size_t)count * vpitch;
+    const bool sh_direct = host_pinned(shards_out, ((size_t)count * n - 1) * shard_pitch + Smax);
+    const bool rt_direct = host_pinned(roots_out, (size_t)count * 32);
+    const size_t br_out = (size_t)count * n * d * 32;
+    const bool br_direct = branches_out && d > 0 && host_pinned(branches_out, br_out);
+    RBC_HIP(s.h_in.ensure(in_stage + (size_t)count * 8));
+    RBC_HIP(s.h_out.ensure((sh_direct ? 0 : sh_bytes) + (size_t)count * 32 + br_bytes));
+    uint8_t *stage = s.h_in.as<uint8_t>();
+    uint32_t *lens = reinterpret_cast<uint32_t *>(stage + in_stage);
     if (in_direct) {
         // the encode kernel masks the Split pad (bytes past len are never used)
         for (int i = 0; i < count; ++i) {
@@ -1194,19 +1235,20 @@ int rbc_shard_commit(rbc_ctx *c, int count, const uint8_t *const *values, const 
     if (!rc) rc = stage_merkle_build(c, st, count, s.d_leaves.as<uint8_t>(), s.d_roots.as<uint8_t>(),
                                      s.d_branches.as<uint8_t>());
     if (rc) return rc;
-    uint8_t *o_sh = s.h_out.as<uint8_t>(), *o_rt = o_sh + sh_bytes, *o_br = o_rt + (size_t)count * 32;
-    const size_t br_out = (size_t)count * n * d * 32;
-    const bool sh_direct = host_pinned(shards_out, ((size_t)count * n - 1) * shard_pitch + Smax);
-    const bool rt_direct = host_pinned(roots_out, (size_t)count * 32);
-    const bool br_direct = branches_out && d > 0 && host_pinned(branches_out, br_out);
-    if (sh_direct)  // Smax bytes per row: the device rows are zero past S_i
-        RBC_HIP(hipMemcpy2DAsync(shards_out, shard_pitch, s.d_shards.p, dpitch, Smax, (size_t)count * n,
-                                 hipMemcpyDeviceToHost, st));
-    else
-        RBC_HIP(hipMemcpyAsync(o_sh, s.d_shards.p, sh_bytes, hipMemcpyDeviceToHost, st));
-    RBC_HIP(hipMemcpyAsync(rt_direct ? roots_out : o_rt, s.d_roots.p, (size_t)count * 32, hipMemcpyDeviceToHost, st));
-    if (branches_out && d > 0)
-        RBC_HIP(hipMemcpyAsync(br_direct ? branches_out : o_br, s.d_branches.p, br_bytes, hipMemcpyDeviceToHost, st));
+    uint8_t *o_sh = s.h_out.as<uint8_t>(), *o_rt = o_sh + (sh_direct ? 0 : sh_bytes),
+            *o_br = o_rt + (size_t)count * 32;
+    void *d_sh = s.d_shards.p, *d_rt = s.d_roots.p, *d_br = s.d_branches.p;
+    auto d2h = [=]() -> int {
+        if (sh_direct)  // Smax bytes per row: the device rows are zero past S_i
+            RBC_HIP(hipMemcpy2DAsync(shards_out, shard_pitch, d_sh, dpitch, Smax, (size_t)count * n,
+                                     hipMemcpyDeviceToHost, st));
+        else
+            RBC_HIP(hipMemcpyAsync(o_sh, d_sh, sh_bytes, hipMemcpyDeviceToHost, st));
+        RBC_HIP(hipMemcpyAsync(rt_direct ? roots_out : o_rt, d_rt, (size_t)count * 32, hipMemcpyDeviceToHost, st));
+        if (branches_out && d > 0)
+            RBC_HIP(hipMemcpyAsync(br_direct ? branches_out : o_br, d_br, br_bytes, hipMemcpyDeviceToHost, st));
+        return RBC_OK;
+    };
     return submit(c, s, ticket, [=]() {
         parallel_for(count, sh_direct ? 0 : (size_t)n * Smax, [&](int i) {
             const size_t S = lens[count + i];
@@ -1218,7 +1260,7 @@ int rbc_shard_commit(rbc_ctx *c, int count, const uint8_t *const *values, const 
         if (!rt_direct) memcpy(roots_out, o_rt, (size_t)count * 32);
         if (branches_out && d > 0 && !br_direct) memcpy(branches_out, o_br, br_out);
         return RBC_OK;
-    });
+    }, d2h);
 }
 
 // VAL hand-off: shard + commit on the device, marshal the
@@ -1261,13 +1303,24 @@ int rbc_shard_commit_val(rbc_ctx *c, int count, const uint8_t *const *values, co
     RBC_HIP(s.h_in.ensure((size_t)count * vpitch + (size_t)count * 8));
     uint8_t *stage = s.h_in.as<uint8_t>();
     uint32_t *lens = reinterpret_cast<uint32_t *>(stage + (size_t)count * vpitch);
-    parallel_for(count, vpitch, [&](int i) {
-        memcpy(stage + (size_t)i * vpitch, values[i], value_lens[i]);
-        memset(stage + (size_t)i * vpitch + value_lens[i], 0, vpitch - value_lens[i]);
-        lens[i] = (uint32_t)value_lens[i];
-        lens[count + i] = (uint32_t)((value_lens[i] + c->k - 1) / c->k);
-    });
-    RBC_HIP(hipMemcpyAsync(s.d_values.p, stage, (size_t)count * vpitch, hipMemcpyHostToDevice, st));
+    bool in_direct = true;
+    for (int i = 0; i < count && in_direct; ++i) in_direct = host_pinned(values[i], value_lens[i]);
+    if (in_direct) {  // pinned values: one DMA each, the encode kernel masks the Split pad
+        for (int i = 0; i < count; ++i) {
+            lens[i] = (uint32_t)value_lens[i];
+            lens[count + i] = (uint32_t)((value_lens[i] + c->k - 1) / c->k);
+            RBC_HIP(hipMemcpyAsync(s.d_values.as<uint8_t>() + (size_t)i * vpitch, values[i], value_lens[i],
+                                   hipMemcpyHostToDevice, st));
+        }
+    } else {
+        parallel_for(count, vpitch, [&](int i) {
+            memcpy(stage + (size_t)i * vpitch, values[i], value_lens[i]);
+            memset(stage + (size_t)i * vpitch + value_lens[i], 0, vpitch - value_lens[i]);
+            lens[i] = (uint32_t)value_lens[i];
+            lens[count + i] = (uint32_t)((value_lens[i] + c->k - 1) / c->k);
+        });
+        RBC_HIP(hipMemcpyAsync(s.d_values.p, stage, (size_t)count * vpitch, hipMemcpyHostToDevice, st));
+    }
     RBC_HIP(hipMemcpyAsync(s.d_lens.p, lens, (size_t)count * 8, hipMemcpyHostToDevice, st));
     const uint32_t *d_vlens = s.d_lens.as<uint32_t>(), *d_slens = d_vlens + count;
     uint32_t *d_mlens = s.d_lens.as<uint32_t>() + 2 * (size_t)count;
@@ -1293,11 +1346,15 @@ int rbc_shard_commit_val(rbc_ctx *c, int count, const uint8_t *const *values, co
     a.out_lens = d_mlens;
     RBC_HIP(rbc_launch_marshal_val(a, st));
     // one D2H of the finished messages: straight into a pinned ring, else
-    // through HIP's staging (pageable)
-    RBC_HIP(hipMemcpyAsync(msgs, d_msgs, msg_bytes, hipMemcpyDeviceToHost, st));
-    RBC_HIP(hipMemcpyAsync(msg_lens, d_mlens, (size_t)count * n * 4, hipMemcpyDeviceToHost, st));
-    if (roots_out) RBC_HIP(hipMemcpyAsync(roots_out, s.d_roots.p, (size_t)count * 32, hipMemcpyDeviceToHost, st));
-    return submit(c, s, ticket, []() { return RBC_OK; });
+    // through HIP's staging (pageable); deferred behind the next submission's H2D
+    void *d_rt = s.d_roots.p;
+    auto d2h = [=]() -> int {
+        RBC_HIP(hipMemcpyAsync(msgs, d_msgs, msg_bytes, hipMemcpyDeviceToHost, st));
+        RBC_HIP(hipMemcpyAsync(msg_lens, d_mlens, (size_t)count * n * 4, hipMemcpyDeviceToHost, st));
+        if (roots_out) RBC_HIP(hipMemcpyAsync(roots_out, d_rt, (size_t)count * 32, hipMemcpyDeviceToHost, st));
+        return RBC_OK;
+    };
+    return submit(c, s, ticket, []() { return RBC_OK; }, d2h);
 }
 
 int rbc_validate_batch(rbc_ctx *c, int count, const uint8_t *const *shards, const size_t *shard_lens,
@@ -1422,15 +1479,18 @@ int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t s
     RBC_HIP(s.d_digests.ensure((size_t)count * 32));
     RBC_HIP(s.d_status.ensure((size_t)count * 4));
     RBC_HIP(s.d_slens.ensure((size_t)count * 4));
-    RBC_HIP(s.h_in.ensure(sh_bytes + (size_t)count * (n + 32 + 4)));
-    RBC_HIP(s.h_out.ensure((size_t)count * (vpitch + 32 + 4)));
-    uint8_t *i_sh = s.h_in.as<uint8_t>(), *i_pr = i_sh + sh_bytes, *i_rt = i_pr + (size_t)count * n;
-    uint32_t *ln = reinterpret_cast<uint32_t *>(i_rt + (size_t)count * 32);
     // direct H2D of a pinned, uniform-length batch (bytes past S must arrive
-    // as zero: the rows are zeroed on the device first)
+    // as zero: the rows are zeroed on the device first); pinned staging only
+    // for what is not already pinned caller memory
     bool uniform = true;
     for (int i = 0; i < count && uniform; ++i) uniform = shard_lens[i] == Smax;
     const bool in_direct = uniform && host_pinned(shards, ((size_t)count * n - 1) * shard_pitch + Smax);
+    const bool out_direct = host_pinned(values_out, (size_t)(count - 1) * value_pitch + (size_t)k * Smax);
+    const size_t in_stage = in_direct ? 0 : sh_bytes, out_stage = out_direct ? 0 : (size_t)count * vpitch;
+    RBC_HIP(s.h_in.ensure(in_stage + (size_t)count * (n + 32 + 4)));
+    RBC_HIP(s.h_out.ensure(out_stage + (size_t)count * (32 + 4)));
+    uint8_t *i_sh = s.h_in.as<uint8_t>(), *i_pr = i_sh + in_stage, *i_rt = i_pr + (size_t)count * n;
+    uint32_t *ln = reinterpret_cast<uint32_t *>(i_rt + (size_t)count * 32);
     if (in_direct) {
         for (int i = 0; i < count; ++i) ln[i] = (uint32_t)shard_lens[i];
         if (dpitch > Smax) RBC_HIP(hipMemsetAsync(s.d_shards.p, 0, sh_bytes, st));
@@ -1460,16 +1520,19 @@ int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t s
                                s.d_roots.as<uint8_t>(), s.d_values.as<uint8_t>(), (uint32_t)vpitch,
                                s.d_digests.as<uint8_t>(), s.d_status.as<int32_t>());
     if (rc) return rc;
-    uint8_t *o_val = s.h_out.as<uint8_t>(), *o_dig = o_val + (size_t)count * vpitch;
+    uint8_t *o_val = s.h_out.as<uint8_t>(), *o_dig = o_val + out_stage;
     int32_t *o_st = reinterpret_cast<int32_t *>(o_dig + (size_t)count * 32);
-    const bool out_direct = host_pinned(values_out, (size_t)(count - 1) * value_pitch + (size_t)k * Smax);
-    if (out_direct)
-        RBC_HIP(hipMemcpy2DAsync(values_out, value_pitch, s.d_values.p, vpitch, (size_t)k * Smax, (size_t)count,
-                                 hipMemcpyDeviceToHost, st));
-    else
-        RBC_HIP(hipMemcpyAsync(o_val, s.d_values.p, (size_t)count * vpitch, hipMemcpyDeviceToHost, st));
-    RBC_HIP(hipMemcpyAsync(o_dig, s.d_digests.p, (size_t)count * 32, hipMemcpyDeviceToHost, st));
-    RBC_HIP(hipMemcpyAsync(o_st, s.d_status.p, (size_t)count * 4, hipMemcpyDeviceToHost, st));
+    void *d_val = s.d_values.p, *d_dig = s.d_digests.p, *d_st = s.d_status.p;
+    auto d2h = [=]() -> int {
+        if (out_direct)
+            RBC_HIP(hipMemcpy2DAsync(values_out, value_pitch, d_val, vpitch, (size_t)k * Smax, (size_t)count,
+                                     hipMemcpyDeviceToHost, st));
+        else
+            RBC_HIP(hipMemcpyAsync(o_val, d_val, (size_t)count * vpitch, hipMemcpyDeviceToHost, st));
+        RBC_HIP(hipMemcpyAsync(o_dig, d_dig, (size_t)count * 32, hipMemcpyDeviceToHost, st));
+        RBC_HIP(hipMemcpyAsync(o_st, d_st, (size_t)count * 4, hipMemcpyDeviceToHost, st));
+        return RBC_OK;
+    };
     return submit(c, s, ticket, [=]() {
         memcpy(status_out, o_st, (size_t)count * 4);
         if (!out_direct)
@@ -1478,7 +1541,7 @@ int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t s
             });
         if (digests_out) memcpy(digests_out, o_dig, (size_t)count * 32);
         return RBC_OK;
-    });
+    }, d2h);
 }
 
 // A ticket completes (its outputs land in the caller's buffers) in rbc_wait,
@@ -1504,6 +1567,7 @@ int rbc_poll(rbc_ctx *c, uint64_t ticket, int *done) {
     *done = 1;
     for (auto &sl : c->slots)
         if (sl->busy && sl->ticket == ticket) {
+            flush_d2h(*sl);  // nothing completes while its copies are unqueued
             const hipError_t q = hipEventQuery(sl->done);
             if (q == hipErrorNotReady) {
                 *done = 0;

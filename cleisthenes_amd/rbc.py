@@ -337,8 +337,13 @@ class Context:
         """rbc_shard_commit_val: shard + commit and the N per-recipient VAL
         pb.Messages of every proposal, handed over in one D2H.  `ring` may be
         a preallocated (e.g. pinned_empty) uint8 array [count][n][msg_pitch]."""
+        return self.shard_commit_val_submit(values, ring).wait()
+
+    def shard_commit_val_submit(self, values: Sequence[bytes], ring: Optional[np.ndarray] = None) -> "HostTicket":
+        """Asynchronous rbc_shard_commit_val (see shard_commit_submit)."""
         count = len(values)
-        arrs = [_bytes_array(v) for v in values]
+        arrs = [v if isinstance(v, np.ndarray) and v.dtype == np.uint8 and v.flags.c_contiguous
+                else _bytes_array(v) for v in values]
         Smax = max((len(a) + self.k - 1) // self.k for a in arrs)
         need = max(lib.rbc_val_message_size(self.n, Smax, 0, 0), lib.rbc_val_message_size(self.n, Smax, self.n - 1, 0))
         pitch = (need + 15) // 16 * 16
@@ -352,9 +357,8 @@ class Context:
         t = c_uint64(0)
         check(lib.rbc_shard_commit_val(self._p, count, vptrs, vlens, _ptr(ring), ring.shape[2],
                                        lens.ctypes.data_as(_lib.u32p), _ptr(roots), byref(t)), "rbc_shard_commit_val")
-        check(lib.rbc_wait(self._p, t.value), "rbc_wait")
-        return {"msgs": ring, "lens": lens, "roots": roots,
-                "message": lambda i, j: bytes(ring[i, j, : lens[i, j]])}
+        out = {"msgs": ring, "lens": lens, "roots": roots, "message": lambda i, j: bytes(ring[i, j, : lens[i, j]])}
+        return HostTicket(self, t.value, out, keep=(arrs, vlens, vptrs))
 
     def validate_batch(self, shards, indices, branches, roots) -> np.ndarray:
         count = len(shards)
@@ -376,6 +380,12 @@ class Context:
 
     def interpolate_batch(self, shards: np.ndarray, shard_lens, present: np.ndarray, roots: np.ndarray,
                           values_out: Optional[np.ndarray] = None) -> dict:
+        return self.interpolate_submit(shards, shard_lens, present, roots, values_out).wait()
+
+    def interpolate_submit(self, shards: np.ndarray, shard_lens, present: np.ndarray, roots: np.ndarray,
+                           values_out: Optional[np.ndarray] = None) -> "HostTicket":
+        """Asynchronous rbc_interpolate_batch: returns at once; .wait()
+        completes it (values, digests, status land in the returned arrays)."""
         shards = np.ascontiguousarray(shards, dtype=np.uint8)
         count, n, pitch = shards.shape
         assert n == self.n
@@ -395,8 +405,8 @@ class Context:
         check(lib.rbc_interpolate_batch(self._p, count, _ptr(shards), pitch, sl, _ptr(present), _ptr(roots),
                                         _ptr(values), values.shape[1], _ptr(digests),
                                         status.ctypes.data_as(_lib.i32p), byref(t)), "rbc_interpolate_batch")
-        check(lib.rbc_wait(self._p, t.value))
-        return {"values": values, "digests": digests, "status": status}
+        out = {"values": values, "digests": digests, "status": status}
+        return HostTicket(self, t.value, out, keep=(shards, present, roots, sl))
 
     # ---- device-resident stages --------------------------------------------
     def dev_encode(self, stream, count, values, value_pitch, value_lens, uniform_len, shards, shard_pitch):

@@ -71,22 +71,37 @@ def measure(ca, n, f, B, batch=64, batches=8, inflight=2, pinned=True, device=0)
         vout = ca.pinned_empty((batch, ctx.k * S))
     lens = outs[-1]["shard_lens"]
     roots = outs[-1]["roots"].copy()
-    ctx.interpolate_batch(rx, lens, present, roots, values_out=vout)  # warm-up
+    vouts = [vout] + [ca.pinned_empty(vout.shape) if pinned else None for _ in range(inflight)]
+    warm = [ctx.interpolate_submit(rx, lens, present, roots, values_out=vouts[i]) for i in range(inflight)]
+    for w in warm:  # warm every slot's buffers
+        w.wait()
     t0 = time.perf_counter()
-    for _ in range(batches):
-        res = ctx.interpolate_batch(rx, lens, present, roots, values_out=vout)
+    live, res = [], None
+    for b in range(batches):
+        live.append(ctx.interpolate_submit(rx, lens, present, roots, values_out=vouts[b % len(vouts)]))
+        if len(live) >= inflight:
+            res = live.pop(0).wait()
+    while live:
+        res = live.pop(0).wait()
     t_dec = time.perf_counter() - t0
     assert (res["status"] == 0).all()
     # proposer send path: shard + commit + per-recipient VAL marshal, one D2H of
     # the finished pb.Message bytes into a pinned ring (rbc_shard_commit_val)
-    vring = None
+    vrings = [None] * (inflight + 1)
     if pinned:
         need = max(ctx.val_message_size(S, 0, 0), ctx.val_message_size(S, n - 1, 0))
-        vring = ca.pinned_empty((batch, n, (need + 15) // 16 * 16))
-    ctx.shard_commit_val(pool[0], ring=vring)  # warm-up
+        vrings = [ca.pinned_empty((batch, n, (need + 15) // 16 * 16)) for _ in range(inflight + 1)]
+    warm = [ctx.shard_commit_val_submit(pool[i % 2], ring=vrings[i]) for i in range(inflight)]
+    for w in warm:
+        w.wait()
     t0 = time.perf_counter()
+    live = []
     for b in range(batches):
-        vo = ctx.shard_commit_val(pool[b % 2], ring=vring)
+        live.append(ctx.shard_commit_val_submit(pool[b % 2], ring=vrings[b % len(vrings)]))
+        if len(live) >= inflight:
+            vo = live.pop(0).wait()
+    while live:
+        vo = live.pop(0).wait()
     t_val = time.perf_counter() - t0
     msg_bytes = int(vo["lens"].sum()) * batches
     ctx.close()
