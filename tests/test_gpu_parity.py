@@ -581,6 +581,67 @@ def test_host_api_pipelined_submissions(gpu, ref):
     assert tickets[0].wait() is tickets[0].result  # waiting twice is harmless
 
 
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_api_mixed_submissions_deferred_copies(gpu, ref, pinned):
+    """The three host batch entry points interleaved with more tickets in
+    flight than slots: each submission's device-to-host copies are deferred
+    until the next submission (or a poll / wait), so polls, waits in reverse
+    order and slot reuse must all still land bit-exact outputs, pinned or
+    pageable caller memory alike."""
+    n, f = 16, 5
+    k = n - 2 * f
+    ctx = gpu.Context(n, f)
+    rng = np.random.default_rng(7 + pinned)
+    B, count = 6000, 5
+    S = (B + k - 1) // k
+    alloc = (lambda shape: gpu.pinned_empty(shape)) if pinned else (lambda shape: np.zeros(shape, np.uint8))
+    vals = []
+    for _ in range(3):
+        vv = []
+        for _ in range(count):
+            a = alloc(B)
+            a[:] = rng.integers(0, 256, B, dtype=np.uint8)
+            vv.append(a)
+        vals.append(vv)
+    want = [[ref.encode_commit(n, f, v) for v in vv] for vv in vals]
+    # receiver inputs from the oracle's codewords: N-f present, one absent-by-zero row each
+    rx = alloc((count, n, S))
+    present = np.zeros((count, n), np.uint8)
+    roots = np.zeros((count, 32), np.uint8)
+    for i in range(count):
+        sh, root, _, _ = want[2][i]
+        pres = rng.permutation(n)[: n - f]
+        present[i, pres] = 1
+        rx[i] = sh * present[i, :, None]
+        roots[i] = np.frombuffer(root, np.uint8)
+    outs = {"shards": alloc((count, n, S)), "roots": alloc((count, 32)),
+            "branches": alloc((count, n, max(ctx.depth, 1), 32))} if pinned else None
+    t1 = ctx.shard_commit_submit(vals[0], out=outs)
+    t2 = ctx.interpolate_submit(rx, [S] * count, present, roots, values_out=alloc((count, k * S)))
+    t3 = ctx.shard_commit_val_submit(vals[1])
+    t4 = ctx.shard_commit_submit(vals[2])
+    assert isinstance(t3.done(), bool)  # a poll enqueues t3's deferred copies
+    r4, r3, r2, r1 = t4.wait(), t3.wait(), t2.wait(), t1.wait()
+    for r, w in ((r1, want[0]), (r4, want[2])):
+        for i in range(count):
+            sh, root, br, _ = w[i]
+            assert np.array_equal(r["shards"][i, :, :S], sh) and bytes(r["roots"][i]) == root
+            assert np.array_equal(r["branches"][i], br)
+    assert (r2["status"] == 0).all()
+    for i in range(count):
+        rc, value, dig = ref.interpolate(n, f, rx[i], present[i], bytes(roots[i]))
+        assert rc == 0 and np.array_equal(r2["values"][i], value) and bytes(r2["digests"][i]) == dig
+        assert bytes(r3["roots"][i]) == want[1][i][1]
+    # the VAL messages equal the host codec's bytes for (root, branch j, shard j)
+    from cleisthenes_amd import protocol
+    for i in (0, count - 1):
+        sh, root, br, _ = want[1][i]
+        for j in (0, n - 1):
+            flat = b"".join(bytes(br[j, lvl]) for lvl in range(ctx.depth) if not (lvl == 0 and (j ^ 1) >= n))
+            assert r3["message"](i, j) == protocol.pb_encode(protocol.VAL, protocol.json_encode_val(root, flat,
+                                                                                                   bytes(sh[j])))
+
+
 @pytest.mark.parametrize("n,f,S", [(64, 21, 187), (64, 21, 192), (128, 42, 200)])
 def test_two_rows_per_lane_sha_path(gpu, ref, n, f, S):
     """ECHO verify grids of >= 262,144 rows take sha_rows2_kernel (two rows
