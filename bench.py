@@ -89,7 +89,8 @@ def parse_args(argv):
                          "interpolate (receiver stream); 2: three streams -- commit(t) || verify(t-1) || "
                          "interpolate(t-2); 3: phase-aligned -- every step runs the SHA phases of three batches "
                          "together (leaves(t) || verify(t-1) || regen hashing(t-2)), then their GF/FFT/tree "
-                         "phases together; 0: one stream, stages in order")
+                         "phases together; 4: as 1 with verify(t-1) split by instances over both streams; "
+                         "0: one stream, stages in order")
     ap.add_argument("--sets", type=int, default=0,
                     help="shard buffer sets of the pipelined schedule (0: the minimum, 2 for --pipeline 1, "
                          "3 for --pipeline 2; more let the proposer run further ahead)")
@@ -464,6 +465,65 @@ def main(argv):
         recR("gather")
         evR[(t - 1) % nsets].record(R)
 
+    # --pipeline 4 (A/B option): the two-stream schedule with ECHO verify of
+    # batch t-1 split by instances over both streams, so that the proposer
+    # stream P (encode + leaves + tree, the shorter one) takes half of the
+    # receiver stream's SHA work: P verifies the first half of t-1 (its own
+    # context's workspace) then commits t; R verifies the second half, waits
+    # for P's half and interpolates t-1.
+    vsplit = args.pipeline == 4
+    if vsplit:
+        h1 = I // 2
+        ctxS = ca.Context(n, f, device=dev)
+        evVa = [ca.Event() for _ in range(nsets)]
+        for e in evVa:
+            e.record(stream)
+
+    def vhalf(c, st, sr, lo, hi):
+        if hi <= lo:
+            return
+        c.dev_verify(st.ptr, hi - lo, sr["shards"].ptr.value + lo * n * spitch, spitch, None, S,
+                     sr["branches"].ptr.value + lo * n * max(d, 1) * 32, sr["roots"].ptr.value + lo * 32,
+                     d_present.ptr.value + lo * n, d_valid.ptr.value + lo * n, d_leaves_r.ptr.value + lo * n * 32)
+
+    def pstep_split(t, ev=None):
+        P, R = stream, rstream
+        recP = (lambda name: ev[name].record(P)) if ev is not None else (lambda name: None)
+        recR = (lambda name: ev[name].record(R)) if ev is not None else (lambda name: None)
+        sp = sets[t % nsets]
+        sr = sets[(t - 1) % nsets] if t >= 1 else None
+        if t >= 1:  # P's half of verify(t-1): commit(t-1) ran on P already
+            if t >= 2:
+                P.wait(evR[(t - 2) % nsets])  # interpolate(t-2) is done with d_valid / d_leaves_r
+            recP("v0")
+            vhalf(ctxS, P, sr, 0, h1)
+            evVa[(t - 1) % nsets].record(P)
+        P.wait(evR[t % nsets])
+        recP("t0")
+        ctx.dev_encode(P.ptr, I, d_values, vpitch, None, B, sp["shards"], spitch)
+        recP("enc")
+        ctx.dev_leaves(P.ptr, I, sp["shards"], spitch, None, S, sp["leaves"])
+        recP("leaf")
+        ctx.dev_merkle_build(P.ptr, I, sp["leaves"], sp["roots"], sp["branches"])
+        recP("tree")
+        ctx.dev_inject_faults(P.ptr, I, sp["shards"], spitch, d_corrupt)
+        recP("fault")
+        evP[t % nsets].record(P)
+        if t == 0:
+            return
+        R.wait(evP[(t - 1) % nsets])
+        recR("r0")
+        vhalf(ctx, R, sr, h1, I)
+        recR("verify")
+        R.wait(evVa[(t - 1) % nsets])
+        ctx.dev_interpolate(R.ptr, I, sr["shards"], spitch, None, S, d_valid, d_leaves_r, 1, sr["roots"], d_out,
+                            opitch, d_digests, d_status)
+        recR("interp")
+        if gather:
+            ctx.dev_allgather_records(R.ptr, I, slots, sr["roots"], d_digests, d_status, d_gather)
+        recR("gather")
+        evR[(t - 1) % nsets].record(R)
+
     # --pipeline 3: phase-aligned schedule on three streams X, Y, Z.  Step k:
     #   SHA phase     X: leaves(k)        Y: verify(k-1)     Z: rehash(k-2)
     #   non-SHA phase X: tree+fault(k),   Y: decode(k-1)     Z: check(k-2)
@@ -566,7 +626,7 @@ def main(argv):
     if pipe:
         args.warmup = max(args.warmup, 3 if pipe3 else 2)  # fill the pipeline: a decode before the guard
         for t in range(args.warmup):
-            (pstep_phased if phased else pstep3 if pipe3 else pstep)(t)
+            (pstep_phased if phased else pstep3 if pipe3 else pstep_split if vsplit else pstep)(t)
     else:
         for _ in range(args.warmup):
             step(None)
@@ -577,7 +637,8 @@ def main(argv):
     t0 = time.perf_counter()
     if pipe:
         for t in range(args.warmup, args.warmup + args.steps):
-            (pstep_phased if phased else pstep3 if pipe3 else pstep)(t, ev_sets[t - args.warmup])
+            (pstep_phased if phased else pstep3 if pipe3 else pstep_split if vsplit else pstep)(
+                t, ev_sets[t - args.warmup])
     else:
         for t in range(args.steps):
             step(ev_sets[t])
@@ -746,6 +807,8 @@ def main(argv):
                                  f"|| decode(t-1) || check(t-2), three streams, {nsets} shard sets") if phased else
                                 (f"commit(t) || verify(t-1) || interpolate(t-2) on three streams, {nsets} shard "
                                  "sets") if pipe3 else
+                                (f"verify(t-1) first half || second half, then commit(t) || interpolate(t-1), "
+                                 f"two streams, {nsets} shard sets") if vsplit else
                                 (f"commit(t) || verify+interpolate(t-1) on two streams, {nsets} shard sets")
                                 if pipe else "serial")},
         "stage_ms": {kk: round(v, 4) for kk, v in stage_ms.items()},
