@@ -1167,6 +1167,19 @@ static bool host_pinned(const void *p, size_t bytes) {
     return true;
 }
 
+// The device address of pinned caller memory when it is the host address itself
+// (hipHostMalloc / rbc_host_alloc under unified addressing), else NULL: a
+// kernel may then read it directly over PCIe.
+static const uint8_t *host_zero_copy(const void *p, size_t bytes) {
+    if (!host_pinned(p, bytes)) return nullptr;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return a.devicePointer == p ? static_cast<const uint8_t *>(p) : nullptr;
+}
+
 int rbc_shard_commit(rbc_ctx *c, int count, const uint8_t *const *values, const size_t *value_lens,
                      uint8_t *shards_out, size_t shard_pitch, uint32_t *shard_lens_out, uint8_t *roots_out,
                      uint8_t *branches_out, uint64_t *ticket) {
@@ -1491,7 +1504,21 @@ int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t s
     RBC_HIP(s.h_out.ensure(out_stage + (size_t)count * (32 + 4)));
     uint8_t *i_sh = s.h_in.as<uint8_t>(), *i_pr = i_sh + in_stage, *i_rt = i_pr + (size_t)count * n;
     uint32_t *ln = reinterpret_cast<uint32_t *>(i_rt + (size_t)count * 32);
-    if (in_direct) {
+    // present mask first: the zero-copy gather reads it
+    memcpy(i_pr, present, (size_t)count * n);
+    RBC_HIP(hipMemcpyAsync(s.d_valid.p, i_pr, (size_t)count * n, hipMemcpyHostToDevice, st));
+    static const bool zc_env = [] {
+        const char *e = getenv("RBC_HOST_ZERO_COPY");
+        return !e || atoi(e) != 0;
+    }();
+    const uint8_t *zc = in_direct && zc_env ? host_zero_copy(shards, ((size_t)count * n - 1) * shard_pitch + Smax)
+                                            : nullptr;
+    if (zc) {
+        // only the received rows cross PCIe (N-f of N at the bench shape)
+        for (int i = 0; i < count; ++i) ln[i] = (uint32_t)shard_lens[i];
+        RBC_HIP(rbc_launch_gather_present(zc, shard_pitch, (uint32_t)Smax, s.d_valid.as<uint8_t>(),
+                                          s.d_shards.as<uint8_t>(), (uint32_t)dpitch, (uint32_t)(count * n), st));
+    } else if (in_direct) {
         for (int i = 0; i < count; ++i) ln[i] = (uint32_t)shard_lens[i];
         if (dpitch > Smax) RBC_HIP(hipMemsetAsync(s.d_shards.p, 0, sh_bytes, st));
         RBC_HIP(hipMemcpy2DAsync(s.d_shards.p, dpitch, shards, shard_pitch, Smax, (size_t)count * n,
@@ -1508,9 +1535,7 @@ int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t s
         });
         RBC_HIP(hipMemcpyAsync(s.d_shards.p, i_sh, sh_bytes, hipMemcpyHostToDevice, st));
     }
-    memcpy(i_pr, present, (size_t)count * n);
     memcpy(i_rt, roots, (size_t)count * 32);
-    RBC_HIP(hipMemcpyAsync(s.d_valid.p, i_pr, (size_t)count * n, hipMemcpyHostToDevice, st));
     RBC_HIP(hipMemcpyAsync(s.d_roots.p, i_rt, (size_t)count * 32, hipMemcpyHostToDevice, st));
     RBC_HIP(hipMemcpyAsync(s.d_slens.p, ln, (size_t)count * 4, hipMemcpyHostToDevice, st));
     // ragged batch: bytes past k*S_i of a value row are returned as zero
@@ -1524,7 +1549,10 @@ int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t s
     int32_t *o_st = reinterpret_cast<int32_t *>(o_dig + (size_t)count * 32);
     void *d_val = s.d_values.p, *d_dig = s.d_digests.p, *d_st = s.d_status.p;
     auto d2h = [=]() -> int {
-        if (out_direct)
+        if (out_direct && value_pitch == vpitch)  // one contiguous DMA (a 2-D copy runs as a blit kernel)
+            RBC_HIP(hipMemcpyAsync(values_out, d_val, (size_t)(count - 1) * vpitch + (size_t)k * Smax,
+                                   hipMemcpyDeviceToHost, st));
+        else if (out_direct)
             RBC_HIP(hipMemcpy2DAsync(values_out, value_pitch, d_val, vpitch, (size_t)k * Smax, (size_t)count,
                                      hipMemcpyDeviceToHost, st));
         else

@@ -204,5 +204,8 @@ hipError_t rbc_launch_pack_records(const uint8_t *roots, const uint8_t *digests,
                                    int slots, uint8_t *out, hipStream_t st);
 hipError_t rbc_launch_fill_random(uint8_t *dst, uint64_t first_row, uint64_t rows, uint64_t pitch, uint64_t seed,
                                   hipStream_t st);
+// present rows of a pinned host batch -> device rows (zero-copy reads), absent rows zeroed
+hipError_t rbc_launch_gather_present(const uint8_t *host, uint64_t hpitch, uint32_t S, const uint8_t *present,
+                                     uint8_t *dev, uint32_t dpitch, uint32_t rows, hipStream_t st);
 hipError_t rbc_launch_count_mismatch(const uint8_t *a, uint64_t a_pitch, const uint8_t *b, uint64_t b_pitch,
                                      uint64_t rows, uint64_t len, uint32_t *counter, hipStream_t st);

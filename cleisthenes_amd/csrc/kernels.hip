@@ -1192,6 +1192,43 @@ __global__ __launch_bounds__(256) void count_mismatch_kernel(const uint8_t *a, u
     if (bad) atomicAdd(counter, bad);
 }
 
+// Host batch API, receiver side: move only the PRESENT shard rows of a pinned
+// caller batch into the device rows, reading the host memory directly over
+// PCIe (zero-copy; measured at the DMA engine's rate, tools/probes/
+// zerocopy_probe.hip).  Bytes [S, dpitch) of a present row and every absent
+// row are written as zero.  Blocks stride over the rows (r = instance * N +
+// row): a few blocks per CU keep enough PCIe reads in flight and leave the
+// CUs to the other slot's decode kernels; the host read is bounded to the
+// row's S bytes.
+__global__ __launch_bounds__(256) void gather_present_kernel(const uint8_t *host, uint64_t hpitch, uint32_t S,
+                                                             const uint8_t *present, uint8_t *dev, uint32_t dpitch,
+                                                             uint32_t rows) {
+    for (uint32_t r = blockIdx.x; r < rows; r += gridDim.x) {
+    uint4 *dst = reinterpret_cast<uint4 *>(dev + (size_t)r * dpitch);
+    const uint32_t chunks = dpitch / 16;
+    if (!present[r]) {
+        for (uint32_t c = threadIdx.x; c < chunks; c += blockDim.x) dst[c] = make_uint4(0, 0, 0, 0);
+        continue;
+    }
+    const uint8_t *row = host + (size_t)r * hpitch;
+    const rsrc_t src = make_rsrc(row, S);
+    for (uint32_t c = threadIdx.x; c < chunks; c += blockDim.x) {
+        const int nv = (int)S - (int)(16u * c);
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (nv >= 16) {
+            v = bload16(src, 16u * c);
+        } else if (nv > 0) {
+            // a 16-byte buffer load that crosses num_records returns zero as a
+            // whole: the row's last bytes are read one by one (never past S)
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+            for (int b = 0; b < nv; ++b) w[b >> 2] |= (uint32_t)row[16u * c + b] << (8 * (b & 3));
+            v = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        dst[c] = v;
+    }
+    }
+}
+
 // ============================================================================
 // launchers
 // ============================================================================
@@ -1217,6 +1254,20 @@ hipError_t rbc_launch_fill_random(uint8_t *dst, uint64_t first_row, uint64_t row
     if (rows == 0 || pitch == 0) return hipSuccess;
     if (pitch % 16) return hipErrorInvalidValue;
     hipLaunchKernelGGL(fill_random_kernel, dim3(8192), dim3(256), 0, st, dst, first_row, rows, pitch, seed);
+    return hipGetLastError();
+}
+
+hipError_t rbc_launch_gather_present(const uint8_t *host, uint64_t hpitch, uint32_t S, const uint8_t *present,
+                                     uint8_t *dev, uint32_t dpitch, uint32_t rows, hipStream_t st) {
+    if (rows == 0) return hipSuccess;
+    if (dpitch % 16 || S > dpitch) return hipErrorInvalidValue;
+    static const uint32_t blocks_env = [] {
+        const char *e = getenv("RBC_GATHER_BLOCKS");
+        return e ? (uint32_t)atoi(e) : 64u;
+    }();
+    const uint32_t blocks = blocks_env ? std::min(rows, blocks_env) : rows;
+    hipLaunchKernelGGL(gather_present_kernel, dim3(blocks), dim3(256), 0, st, host, hpitch, S, present, dev, dpitch,
+                       rows);
     return hipGetLastError();
 }
 

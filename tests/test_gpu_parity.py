@@ -821,6 +821,40 @@ def test_host_batch_pinned_direct_copies(gpu, ref, lens):
         assert res["values"][i, : len(v)].tobytes() == v.tobytes()
 
 
+@pytest.mark.parametrize("n,f,B,pad", [(16, 5, 6000, 0), (16, 5, 5999, 13), (128, 42, 1 << 20, 0),
+                                        (256, 85, 64 << 10, 5), (4, 1, 1, 3)])
+def test_host_interpolate_zero_copy_reads_present_rows_only(gpu, ref, n, f, B, pad):
+    """A pinned, uniform-length receive batch is gathered on the device
+    straight from host memory, present rows only: absent rows and the bytes
+    of a row past S (a host pitch > S) hold garbage here and must not change
+    status, value or digest -- equal to the C oracle on the zeroed input."""
+    k = n - 2 * f
+    S = (B + k - 1) // k
+    count = 3
+    ctx = gpu.Context(n, f)
+    rng = np.random.default_rng(n + pad)
+    rx = gpu.pinned_empty((count, n, S + pad))
+    rx[:] = rng.integers(0, 256, rx.shape, dtype=np.uint8)  # garbage everywhere first
+    present = np.zeros((count, n), np.uint8)
+    roots = np.zeros((count, 32), np.uint8)
+    clean = np.zeros((count, n, S), np.uint8)
+    for i in range(count):
+        v = rng.integers(0, 256, B, dtype=np.uint8)
+        sh, root, _, _ = ref.encode_commit(n, f, v)
+        roots[i] = np.frombuffer(root, np.uint8)
+        pres = rng.permutation(n)[: n - f]
+        present[i, pres] = 1
+        rx[i, pres, :S] = sh[pres]
+        clean[i] = sh * present[i, :, None]
+    vout = gpu.pinned_empty((count, k * S))
+    # the host row stride is S + pad; the lengths give S
+    res = ctx.interpolate_submit(rx, [S] * count, present, roots, values_out=vout).wait()
+    assert (res["status"] == 0).all()
+    for i in range(count):
+        rc, value, dig = ref.interpolate(n, f, clean[i], present[i], bytes(roots[i]))
+        assert rc == 0 and np.array_equal(res["values"][i], value) and bytes(res["digests"][i]) == dig, i
+
+
 @pytest.mark.parametrize("S", [763, 100, 1400, 1500, 2000])
 def test_device_interpolate_short_rows(gpu, S):
     """Missing-data GF rows for short shards (one-wave tiles: 12 bytes per
