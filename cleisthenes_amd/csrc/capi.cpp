@@ -165,12 +165,13 @@ struct Slot {
     }
 };
 
-// host-API submissions in flight per context (RBC_HOST_SLOTS, default 2)
+// host-API submissions in flight per context (RBC_HOST_SLOTS, default 4: the
+// batcher keeps 4 launches in flight, tools/batcher_bench.cpp)
 int host_slots() {
     static const int v = [] {
         const char *e = getenv("RBC_HOST_SLOTS");
         int x = e ? atoi(e) : 0;
-        return (x >= 1 && x <= 8) ? x : 2;
+        return (x >= 1 && x <= 8) ? x : 4;
     }();
     return v;
 }
@@ -1404,8 +1405,10 @@ int rbc_validate_batch(rbc_ctx *c, int count, const uint8_t *const *shards, cons
     uint32_t *ln = reinterpret_cast<uint32_t *>(rt + (size_t)count * 32);
     uint8_t *ix = reinterpret_cast<uint8_t *>(ln + count);
     uint8_t *shape_ok = s.h_out.as<uint8_t>() + count;  // host-side shape verdicts
-    memset(sh, 0, stage_bytes);
-    for (int i = 0; i < count; ++i) {
+    // No blanket zeroing: the kernel reads a row only up to its length (the
+    // bytes past it inside the last 64-byte block are masked), and a
+    // malformed entry hashes one staged byte whose verdict is discarded.
+    parallel_for(count, pitch, [&](int i) {
         const uint32_t j = indices[i];
         // unflatten the Go-form branch (the empty level-0 sibling is omitted)
         const bool empty0 = d > 0 && (j ^ 1u) >= (uint32_t)c->n;
@@ -1416,19 +1419,25 @@ int rbc_validate_batch(rbc_ctx *c, int count, const uint8_t *const *shards, cons
             shape_ok[i] = 0;
             ln[i] = 1;
             ix[i] = 0;
-            continue;
+            memset(sh + (size_t)i * pitch, 0, 64);
+            memset(br + (size_t)i * bslot, 0, bslot);
+            memset(rt + 32 * i, 0, 32);
+            return;
         }
         memcpy(sh + (size_t)i * pitch, shards[i], shard_lens[i]);
         size_t off = 0;
         for (int l = 0; l < d; ++l) {
-            if (l == 0 && empty0) continue;
+            if (l == 0 && empty0) {
+                memset(br + (size_t)i * bslot, 0, 32);  // the device form keeps a zero level-0 slot
+                continue;
+            }
             memcpy(br + (size_t)i * bslot + 32 * l, branches[i] + off, 32);
             off += 32;
         }
         memcpy(rt + 32 * i, roots[i], 32);
         ln[i] = (uint32_t)shard_lens[i];
         ix[i] = (uint8_t)j;
-    }
+    });
     RBC_HIP(hipMemcpyAsync(s.d_shards.p, sh, (size_t)count * pitch, hipMemcpyHostToDevice, st));
     RBC_HIP(hipMemcpyAsync(s.d_branches.p, br, (size_t)count * bslot, hipMemcpyHostToDevice, st));
     RBC_HIP(hipMemcpyAsync(s.d_roots.p, rt, (size_t)count * 32, hipMemcpyHostToDevice, st));
