@@ -90,6 +90,7 @@ def parse_args(argv):
                          "interpolate(t-2); 3: phase-aligned -- every step runs the SHA phases of three batches "
                          "together (leaves(t) || verify(t-1) || regen hashing(t-2)), then their GF/FFT/tree "
                          "phases together; 4: as 1 with verify(t-1) split by instances over both streams; "
+                         "5: balanced two streams -- commit(t) then rehash+check(t-2) || verify+decode(t-1); "
                          "0: one stream, stages in order")
     ap.add_argument("--sets", type=int, default=0,
                     help="shard buffer sets of the pipelined schedule (0: the minimum, 2 for --pipeline 1, "
@@ -273,8 +274,9 @@ def main(argv):
     corrupt_h = corrupt_all[first:first + I]
 
     pipe = bool(args.pipeline)
-    pipe3 = args.pipeline in (2, 3)  # per-set valid / verified leaves, >= 3 sets
-    phased = args.pipeline == 3
+    pipe3 = args.pipeline in (2, 3, 5)  # per-set valid / verified leaves, >= 3 sets
+    phased = args.pipeline in (3, 5)    # per-set value / digest / status
+    bal = args.pipeline == 5
     # the pipeline holds two shard sets; when they do not fit the 288 GB of
     # HBM (C3 with all 8192 instances on one GPU: 2 x 100 GB + values) run
     # the serial schedule instead
@@ -524,6 +526,60 @@ def main(argv):
         recR("gather")
         evR[(t - 1) % nsets].record(R)
 
+    # --pipeline 5 (A/B option): balanced two-stream schedule.  P commits t,
+    # then rehashes the regenerated rows of t-2 and checks its root; R
+    # verifies and decodes t-1.  Isolated work per stream: P 4.0 ms (encode,
+    # leaves, tree, regen hashing, root check), R 4.1 (verify, prepare, GF,
+    # FFT, join) instead of 2.9 / 4.9.  The decode and rehash of one batch
+    # share a context's regen list, so batches alternate between two contexts.
+    if bal:
+        evD = [ca.Event() for _ in range(nsets)]
+        for e in evD:
+            e.record(stream)
+
+    def pstep_bal(t, ev=None):
+        P, R = stream, rstream
+        recP = (lambda name: ev[name].record(P)) if ev is not None else (lambda name: None)
+        recR = (lambda name: ev[name].record(R)) if ev is not None else (lambda name: None)
+        cxo = (ctx, ctxV)
+        sp = sets[t % nsets]
+        # set t % 3 last held batch t-3, whose check ran on P (step t-1) after
+        # waiting for its decode on R: P's own order frees it
+        recP("t0")
+        ctx.dev_encode(P.ptr, I, d_values, vpitch, None, B, sp["shards"], spitch)
+        recP("enc")
+        ctx.dev_leaves(P.ptr, I, sp["shards"], spitch, None, S, sp["leaves"])
+        recP("leaf")
+        ctx.dev_merkle_build(P.ptr, I, sp["leaves"], sp["roots"], sp["branches"])
+        recP("tree")
+        ctx.dev_inject_faults(P.ptr, I, sp["shards"], spitch, d_corrupt)
+        recP("fault")
+        evP[t % nsets].record(P)
+        if t >= 2:
+            s2, c2 = sets[(t - 2) % nsets], cxo[(t - 2) % 2]
+            P.wait(evD[(t - 2) % nsets])
+            recP("g0")
+            c2.dev_interpolate_phases(P.ptr, ctx.INTERP_REHASH, I, s2["shards"], spitch, None, S, s2["valid"],
+                                      s2["leaves_r"], 1, s2["roots"], s2["out"], opitch, s2["digests"], s2["status"])
+            recP("regen")
+            c2.dev_interpolate_phases(P.ptr, ctx.INTERP_CHECK, I, s2["shards"], spitch, None, S, s2["valid"],
+                                      s2["leaves_r"], 1, s2["roots"], s2["out"], opitch, s2["digests"], s2["status"])
+            recP("check")
+            if gather:
+                ctx.dev_allgather_records(P.ptr, I, slots, s2["roots"], s2["digests"], s2["status"], d_gather)
+            recP("gather")
+        if t >= 1:
+            s1, c1 = sets[(t - 1) % nsets], cxo[(t - 1) % 2]
+            R.wait(evP[(t - 1) % nsets])
+            recR("v0")
+            c1.dev_verify(R.ptr, I, s1["shards"], spitch, None, S, s1["branches"], s1["roots"], d_present,
+                          s1["valid"], s1["leaves_r"])
+            recR("verify")
+            c1.dev_interpolate_phases(R.ptr, ctx.INTERP_DECODE, I, s1["shards"], spitch, None, S, s1["valid"],
+                                      s1["leaves_r"], 1, s1["roots"], s1["out"], opitch, s1["digests"], s1["status"])
+            recR("decode")
+            evD[(t - 1) % nsets].record(R)
+
     # --pipeline 3: phase-aligned schedule on three streams X, Y, Z.  Step k:
     #   SHA phase     X: leaves(k)        Y: verify(k-1)     Z: rehash(k-2)
     #   non-SHA phase X: tree+fault(k),   Y: decode(k-1)     Z: check(k-2)
@@ -534,7 +590,7 @@ def main(argv):
     # run together and the GF/FFT transforms run together -- two SHA kernels
     # share CUs well, a transform beside SHA does not.
     # Set k % nsets is rewritten by encode(k+1)'s set only after rehash(k-2).
-    if phased:
+    if phased and not bal:
         X, Y, Z = stream, rstream, vstream
         evA = {nm: ca.Event() for nm in ("X", "Y", "Z")}  # end of a SHA phase, per stream
         evB = {nm: ca.Event() for nm in ("X", "Y", "Z")}  # end of a non-SHA phase, per stream
@@ -626,7 +682,8 @@ def main(argv):
     if pipe:
         args.warmup = max(args.warmup, 3 if pipe3 else 2)  # fill the pipeline: a decode before the guard
         for t in range(args.warmup):
-            (pstep_phased if phased else pstep3 if pipe3 else pstep_split if vsplit else pstep)(t)
+            (pstep_bal if bal else pstep_phased if phased else pstep3 if pipe3 else pstep_split if vsplit
+             else pstep)(t)
     else:
         for _ in range(args.warmup):
             step(None)
@@ -637,8 +694,8 @@ def main(argv):
     t0 = time.perf_counter()
     if pipe:
         for t in range(args.warmup, args.warmup + args.steps):
-            (pstep_phased if phased else pstep3 if pipe3 else pstep_split if vsplit else pstep)(
-                t, ev_sets[t - args.warmup])
+            (pstep_bal if bal else pstep_phased if phased else pstep3 if pipe3 else pstep_split if vsplit
+             else pstep)(t, ev_sets[t - args.warmup])
     else:
         for t in range(args.steps):
             step(ev_sets[t])
@@ -647,7 +704,11 @@ def main(argv):
     elapsed_max = rdz.max(elapsed)
     # the set the last decode read
     last = sets[(args.warmup + args.steps - (3 if pipe3 else 2)) % nsets] if pipe else sets[0]
-    if phased:
+    if bal:
+        pipe_spans = (("t0", "enc"), ("enc", "leaf"), ("leaf", "tree"), ("tree", "fault"), ("v0", "verify"),
+                      ("verify", "decode"), ("g0", "regen"), ("regen", "check"), ("check", "gather"))
+        stage_ms.update(decode=0.0, regen=0.0, check=0.0)
+    elif phased:
         pipe_spans = (("e0", "enc"), ("l0", "leaf"), ("t0b", "tree"), ("tree", "fault"), ("v0", "verify"),
                       ("d0", "decode"), ("g0", "regen"), ("c0", "check"), ("check", "gather"))
         stage_ms.update(decode=0.0, regen=0.0, check=0.0)
@@ -803,7 +864,9 @@ def main(argv):
                    "gf_codec": ctx.codec,
                    **({"rehearsal": "all ranks on device 0, no RCCL (not a multi-GPU measurement)"}
                       if args.rehearse_on_one_gpu else {}),
-                   "pipeline": ((f"phase-aligned: SHA of leaves(t) || verify(t-1) || rehash(t-2), then tree/encode "
+                   "pipeline": ((f"balanced: commit(t) then rehash+check(t-2) || verify+decode(t-1), two streams, "
+                                 f"{nsets} shard sets") if bal else
+                                (f"phase-aligned: SHA of leaves(t) || verify(t-1) || rehash(t-2), then tree/encode "
                                  f"|| decode(t-1) || check(t-2), three streams, {nsets} shard sets") if phased else
                                 (f"commit(t) || verify(t-1) || interpolate(t-2) on three streams, {nsets} shard "
                                  "sets") if pipe3 else
