@@ -75,21 +75,31 @@ bool skip_field(const uint8_t *&p, const uint8_t *e, int wire) {
     }
 }
 
+size_t varint_len(uint64_t v) {
+    size_t n = 1;
+    while (v >= 0x80) {
+        v >>= 7;
+        ++n;
+    }
+    return n;
+}
+
 std::string pb_rbc(int type, const uint8_t *payload, size_t len) {
-    std::string rbc;
-    if (len) {  // proto3: default (empty / zero) scalars are not emitted
-        rbc.push_back(0x0a);
-        put_varint(rbc, len);
-        rbc.append((const char *)payload, len);
+    // proto3: default (empty / zero) scalars are not emitted
+    const size_t body = (len ? 1 + varint_len(len) + len : 0) + (type ? 1 + varint_len((uint64_t)type) : 0);
+    std::string m;
+    m.reserve(1 + varint_len(body) + body);
+    m.push_back(0x1a);  // field 3, length-delimited: the oneof is set even when RBC is empty
+    put_varint(m, body);
+    if (len) {
+        m.push_back(0x0a);
+        put_varint(m, len);
+        m.append((const char *)payload, len);
     }
     if (type) {
-        rbc.push_back(0x10);
-        put_varint(rbc, (uint64_t)type);
+        m.push_back(0x10);
+        put_varint(m, (uint64_t)type);
     }
-    std::string m;
-    m.push_back(0x1a);  // field 3, length-delimited: the oneof is set even when RBC is empty
-    put_varint(m, rbc.size());
-    m += rbc;
     return m;
 }
 
@@ -149,63 +159,77 @@ int pb_parse(const uint8_t *msg, size_t len, int *type, const uint8_t **payload,
 // ---------------------------------------------------------------------------
 const char B64[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
 
+// Written straight into pre-sized storage: a VAL / ECHO carries a whole shard
+// (tens of KiB) as base64, so the codec is the per-message host cost.
 void b64_encode(std::string &s, const uint8_t *p, size_t n) {
+    const size_t at = s.size();
+    s.resize(at + 4 * ((n + 2) / 3));
+    char *o = &s[at];
     size_t i = 0;
-    for (; i + 3 <= n; i += 3) {
+    for (; i + 3 <= n; i += 3, o += 4) {
         const uint32_t v = (uint32_t)p[i] << 16 | (uint32_t)p[i + 1] << 8 | p[i + 2];
-        s.push_back(B64[v >> 18]);
-        s.push_back(B64[(v >> 12) & 63]);
-        s.push_back(B64[(v >> 6) & 63]);
-        s.push_back(B64[v & 63]);
+        o[0] = B64[v >> 18];
+        o[1] = B64[(v >> 12) & 63];
+        o[2] = B64[(v >> 6) & 63];
+        o[3] = B64[v & 63];
     }
     if (n - i == 1) {
         const uint32_t v = (uint32_t)p[i] << 16;
-        s.push_back(B64[v >> 18]);
-        s.push_back(B64[(v >> 12) & 63]);
-        s += "==";
+        o[0] = B64[v >> 18];
+        o[1] = B64[(v >> 12) & 63];
+        o[2] = o[3] = '=';
     } else if (n - i == 2) {
         const uint32_t v = (uint32_t)p[i] << 16 | (uint32_t)p[i + 1] << 8;
-        s.push_back(B64[v >> 18]);
-        s.push_back(B64[(v >> 12) & 63]);
-        s.push_back(B64[(v >> 6) & 63]);
-        s.push_back('=');
+        o[0] = B64[v >> 18];
+        o[1] = B64[(v >> 12) & 63];
+        o[2] = B64[(v >> 6) & 63];
+        o[3] = '=';
     }
 }
 
-int b64_val(char c) {
-    if (c >= 'A' && c <= 'Z') return c - 'A';
-    if (c >= 'a' && c <= 'z') return c - 'a' + 26;
-    if (c >= '0' && c <= '9') return c - '0' + 52;
-    if (c == '+') return 62;
-    if (c == '/') return 63;
-    return -1;
-}
+// alphabet value of every byte, -1 outside the standard alphabet
+struct B64Table {
+    int8_t v[256];
+    B64Table() {
+        memset(v, -1, sizeof v);
+        for (int i = 0; i < 64; ++i) v[(uint8_t)B64[i]] = (int8_t)i;
+    }
+};
+const B64Table kB64;
 
 // base64.StdEncoding.DecodeString as encoding/json applies it: padding
 // required, '\r' / '\n' ignored.  StdEncoding is not Strict(), so non-zero
 // trailing bits in the last quantum are ignored ("AB==" decodes to 0x00).
-bool b64_decode(const std::string &in, std::string &out) {
-    std::string s;
-    s.reserve(in.size());
-    for (char c : in)
-        if (c != '\r' && c != '\n') s.push_back(c);
-    if (s.size() % 4) return false;
-    out.clear();
-    for (size_t i = 0; i < s.size(); i += 4) {
-        const bool last = i + 4 == s.size();
-        int pad = 0;
-        if (last && s[i + 3] == '=') pad = s[i + 2] == '=' ? 2 : 1;
-        int v[4];
-        for (int j = 0; j < 4 - pad; ++j)
-            if ((v[j] = b64_val(s[i + j])) < 0) return false;
-        for (int j = 4 - pad; j < 4; ++j) v[j] = 0;
-        const uint32_t w = (uint32_t)v[0] << 18 | (uint32_t)v[1] << 12 | (uint32_t)v[2] << 6 | (uint32_t)v[3];
-        out.push_back((char)(w >> 16));
-        if (pad < 2) out.push_back((char)(w >> 8));
-        if (pad < 1) out.push_back((char)w);
+bool b64_decode_range(const char *in, size_t len, std::string &out) {
+    std::string filtered;
+    if (memchr(in, '\r', len) || memchr(in, '\n', len)) {
+        filtered.reserve(len);
+        for (size_t i = 0; i < len; ++i)
+            if (in[i] != '\r' && in[i] != '\n') filtered.push_back(in[i]);
+        in = filtered.data();
+        len = filtered.size();
     }
+    if (len % 4) return false;
+    out.resize(len / 4 * 3);
+    char *o = len ? &out[0] : nullptr;
+    size_t w = 0;
+    for (size_t i = 0; i < len; i += 4) {
+        const uint8_t *q = reinterpret_cast<const uint8_t *>(in + i);
+        int pad = 0;
+        if (i + 4 == len && q[3] == '=') pad = q[2] == '=' ? 2 : 1;
+        int v[4] = {0, 0, 0, 0};
+        for (int j = 0; j < 4 - pad; ++j)
+            if ((v[j] = kB64.v[q[j]]) < 0) return false;
+        const uint32_t x = (uint32_t)v[0] << 18 | (uint32_t)v[1] << 12 | (uint32_t)v[2] << 6 | (uint32_t)v[3];
+        o[w++] = (char)(x >> 16);
+        if (pad < 2) o[w++] = (char)(x >> 8);
+        if (pad < 1) o[w++] = (char)x;
+    }
+    out.resize(w);
     return true;
 }
+
+bool b64_decode(const std::string &in, std::string &out) { return b64_decode_range(in.data(), in.size(), out); }
 
 void json_bytes(std::string &s, const uint8_t *p, size_t n, bool null_if_empty) {
     if (!n && null_if_empty) {
@@ -220,7 +244,9 @@ void json_bytes(std::string &s, const uint8_t *p, size_t n, bool null_if_empty) 
 // ValRequest / EchoRequest{ValRequest} (rbc/request.go:9-17)
 std::string json_val(const uint8_t *root, size_t rl, const uint8_t *branch, size_t bl, const uint8_t *block,
                      size_t kl) {
-    std::string s = "{\"RootHash\":";
+    std::string s;
+    s.reserve(64 + 4 * ((rl + 2) / 3) + 4 * ((bl + 2) / 3) + 4 * ((kl + 2) / 3));
+    s = "{\"RootHash\":";
     json_bytes(s, root, rl, true);
     s += ",\"Branch\":";
     json_bytes(s, branch, bl, true);
@@ -271,6 +297,11 @@ struct JsonIn {
     bool str(std::string &out) {
         if (!eat('"')) return false;
         out.clear();
+        // plain run up to the closing quote (no escapes / control bytes): one copy
+        const char *q = p;
+        while (q < e && *q != '"' && *q != '\\' && (unsigned char)*q >= 0x20) ++q;
+        out.assign(p, q);
+        p = q;
         while (p < e && *p != '"') {
             char c = *p++;
             if ((unsigned char)c < 0x20) return false;
@@ -344,6 +375,16 @@ struct JsonIn {
         if (lit("null")) {
             out.clear();
             return true;
+        }
+        // common case, a string without escapes: decode in place
+        if (peek('"')) {
+            const char *q = p + 1;
+            while (q < e && *q != '"' && *q != '\\' && (unsigned char)*q >= 0x20) ++q;
+            if (q < e && *q == '"') {
+                const char *b = p + 1;
+                p = q + 1;
+                return b64_decode_range(b, (size_t)(q - b), out);
+            }
         }
         std::string s;
         return str(s) && b64_decode(s, out);
