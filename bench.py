@@ -815,6 +815,18 @@ def main(argv):
                 iso["valu_frac_of_attainable"] = round(cps / SHA_PROBE_CPS, 4)
             r["isolated"] = iso
 
+    # BASELINE configs[1] measures RS encode + Merkle build alone: the same
+    # kernels timed alone on the chip (the serial steps before the warmup, or
+    # the serial schedule's own spans)
+    commit_src = iso_ms if iso_ms is not None else (stage_ms if not pipe else None)
+    commit_only = None
+    if commit_src is not None:
+        cms = commit_src["enc"] + commit_src["leaf"] + commit_src["tree"]
+        commit_only = {"GBps": round(I * n * S / (cms / 1e3) / 1e9, 2), "ms_per_batch": round(cms, 4),
+                       "unit": "GB/s of committed shard bytes (N*S per instance), per rank",
+                       "note": "RS encode + Merkle build alone (BASELINE configs[1]'s stages): encode + leaf "
+                               "hashing + tree spans of serial steps"}
+
     # GPU phase rates (per rank, from the stage events): encode+commit =
     # N*S shard bytes per instance; verify+decode = k*S value bytes
     enc_ms = stage_ms["enc"] + stage_ms["leaf"] + stage_ms["tree"]
@@ -876,6 +888,7 @@ def main(argv):
                                 if pipe else "serial")},
         "stage_ms": {kk: round(v, 4) for kk, v in stage_ms.items()},
         "phases": phases,
+        "commit_only": commit_only,
         **checks,
         "roofline": roof,
         "roofline_encode": codec_roof,
