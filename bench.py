@@ -826,6 +826,13 @@ def main(argv):
                        "unit": "GB/s of committed shard bytes (N*S per instance), per rank",
                        "note": "RS encode + Merkle build alone (BASELINE configs[1]'s stages): encode + leaf "
                                "hashing + tree spans of serial steps"}
+    receive_only = None
+    if commit_src is not None:
+        rms = commit_src["verify"] + commit_src["interp"]
+        receive_only = {"GBps": round(I * n * S / (rms / 1e3) / 1e9, 2), "ms_per_batch": round(rms, 4),
+                        "unit": "GB/s of committed shard bytes (N*S per instance), per rank",
+                        "note": "ECHO-side Merkle branch verify + RS reconstruct / re-encode / root recheck alone "
+                                "(BASELINE configs[2]'s stages): verify + interpolate spans of serial steps"}
 
     # GPU phase rates (per rank, from the stage events): encode+commit =
     # N*S shard bytes per instance; verify+decode = k*S value bytes
@@ -889,6 +896,7 @@ def main(argv):
         "stage_ms": {kk: round(v, 4) for kk, v in stage_ms.items()},
         "phases": phases,
         "commit_only": commit_only,
+        "receive_only": receive_only,
         **checks,
         "roofline": roof,
         "roofline_encode": codec_roof,
