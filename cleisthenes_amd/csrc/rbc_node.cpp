@@ -467,7 +467,6 @@ struct Op {
     uint8_t root[32] = {};
     // OP_INTERP
     std::string iroot;
-    std::vector<std::string> in;
     std::vector<const uint8_t *> ptrs;
     std::vector<size_t> lens;
     std::vector<uint8_t> out;
@@ -544,13 +543,15 @@ struct rbc_node {
         auto op = std::make_unique<Op>();
         op->kind = OP_INTERP;
         op->iroot = root;
-        op->in = s.echo;  // snapshot: later ECHOs do not touch the launch's inputs
+        // snapshot by reference: an ECHO slot is written once and never again,
+        // and a root's state is never erased, so the shards the launch reads
+        // stay in place while later ECHOs fill other slots
         op->ptrs.resize(n);
         op->lens.resize(n);
         size_t S = 1;
         for (int j = 0; j < n; ++j) {
-            op->ptrs[j] = (const uint8_t *)op->in[j].data();
-            op->lens[j] = op->in[j].size();
+            op->ptrs[j] = (const uint8_t *)s.echo[j].data();
+            op->lens[j] = s.echo[j].size();
             if (op->lens[j]) S = op->lens[j];
         }
         op->out.resize((size_t)k * S);
@@ -566,13 +567,13 @@ struct rbc_node {
         send(-1, RBC_MSG_ECHO,
              json_val((const uint8_t *)r.root.data(), r.root.size(), (const uint8_t *)r.branch.data(),
                       r.branch.size(), (const uint8_t *)r.block[0].data(), r.block[0].size()));
-        on_echo(self, r.root, r.block[0]);
+        on_echo(self, r.root, std::string(r.block[0]));
     }
 
-    void on_echo(int from, const std::string &root, const std::string &shard) {
+    void on_echo(int from, const std::string &root, std::string &&shard) {
         RootState &s = state(root);
         if (s.echo[from].empty()) {
-            s.echo[from] = shard;
+            s.echo[from] = std::move(shard);
             s.echoes++;
         }
         advance(root);
@@ -656,7 +657,7 @@ struct rbc_node {
                     rejected++;
                     break;
                 }
-                on_echo(op.sender, op.req.root, op.req.block[0]);
+                on_echo(op.sender, op.req.root, std::move(op.req.block[0]));
                 break;
             case OP_INTERP: {
                 RootState &s = state(op.iroot);
