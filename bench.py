@@ -1002,18 +1002,24 @@ def cpu_baseline(args, host):
     main_cfg = args.config
     res = run(main_cfg, 6e9, threads)
     single = run(main_cfg, 6e9 / 16, 1)
-    per_config = {}
+    per_config, per_config_1 = {}, {}
     for cfg in [c.strip() for c in args.cpu_configs.split(",") if c.strip() in CONFIGS]:
         per_config[cfg] = res if cfg == main_cfg else run(cfg, 1.5e9, threads)
+        # one core too (BASELINE.md's CPU table: 1 core and all cores per config)
+        per_config_1[cfg] = single if cfg == main_cfg else run(cfg, 1.5e9 / 16, 1)
     return {"value": res["value"], "unit": "GB/s", "cores": threads, "kind": "port",
             "sample": res["sample"] + "; same per-instance pipeline as the GPU step (verified leaves reused)",
             "phases": res["phases"],
-            "single_core": {"value": single["value"], "unit": "GB/s", "cores": 1, "sample": single["sample"]},
-            "per_config": {c: {"value": r["value"], "phases": r["phases"], "sample": r["sample"]}
+            "single_core": {"value": single["value"], "unit": "GB/s", "cores": 1, "phases": single["phases"],
+                            "sample": single["sample"]},
+            "per_config": {c: {"value": r["value"], "phases": r["phases"], "sample": r["sample"],
+                               "single_core": {"value": per_config_1[c]["value"],
+                                               "phases": per_config_1[c]["phases"]}}
                            for c, r in per_config.items()},
             "host": host, "simd": ("avx2 " if feats & 1 else "") + ("sha-ni" if feats & 2 else ""),
             "status_sum": res["status_sum"] + single["status_sum"] +
-            sum(r["status_sum"] for r in per_config.values())}
+            sum(r["status_sum"] for r in per_config.values()) +
+            sum(r["status_sum"] for c, r in per_config_1.items() if c != main_cfg)}
 
 
 if __name__ == "__main__":
