@@ -821,6 +821,50 @@ def test_host_batch_pinned_direct_copies(gpu, ref, lens):
         assert res["values"][i, : len(v)].tobytes() == v.tobytes()
 
 
+def test_host_api_errors_do_not_disturb_tickets_in_flight(gpu, ref):
+    """Argument errors are returned at submit without touching the tickets in
+    flight; per-instance failures (too few shards, wrong root, ragged lengths)
+    come back as per-instance status of an otherwise good batch; every other
+    ticket still lands bit-exact."""
+    n, f = 16, 5
+    k = n - 2 * f
+    ctx = gpu.Context(n, f)
+    rng = np.random.default_rng(55)
+    B, count = 3000, 4
+    S = (B + k - 1) // k
+    vals = [rng.integers(0, 256, B, dtype=np.uint8) for _ in range(count)]
+    want = [ref.encode_commit(n, f, v) for v in vals]
+    t_ok = ctx.shard_commit_submit(vals)
+    # an argument error at submit: a zero-length value (Split's ErrShortData)
+    with pytest.raises(Exception) as ei:
+        ctx.shard_commit_submit([vals[0], np.zeros(0, np.uint8)])
+    assert getattr(ei.value, "code", None) == -6  # RBC_ERR_SHORT_DATA
+    rx = np.zeros((count, n, S), np.uint8)
+    present = np.zeros((count, n), np.uint8)
+    roots = np.zeros((count, 32), np.uint8)
+    for i in range(count):
+        sh, root, _, _ = want[i]
+        pres = rng.permutation(n)[: n - f]
+        present[i, pres] = 1
+        rx[i] = sh * present[i, :, None]
+        roots[i] = np.frombuffer(root, np.uint8)
+    present[1] = 0
+    present[1, :k - 1] = 1           # instance 1: k-1 shards -> too few
+    roots[2, 0] ^= 1                 # instance 2: wrong root -> root mismatch
+    t_rx = ctx.interpolate_submit(rx, [S] * count, present, roots)
+    t_ok2 = ctx.shard_commit_submit(vals[::-1])
+    r_rx = t_rx.wait()
+    st = r_rx["status"]
+    assert st[0] == 0 and st[3] == 0
+    assert st[1] == -3 and st[2] == -8, st  # RBC_ERR_TOO_FEW_SHARDS, RBC_ERR_ROOT_MISMATCH
+    for i in (0, 3):
+        assert r_rx["values"][i, :B].tobytes() == vals[i].tobytes()
+    for t, vv in ((t_ok, vals), (t_ok2, vals[::-1])):
+        r = t.wait()
+        for i, v in enumerate(vv):
+            assert bytes(r["roots"][i]) == ref.encode_commit(n, f, v)[1]
+
+
 @pytest.mark.parametrize("n,f,B,pad", [(16, 5, 6000, 0), (16, 5, 5999, 13), (128, 42, 1 << 20, 0),
                                         (256, 85, 64 << 10, 5), (4, 1, 1, 3)])
 def test_host_interpolate_zero_copy_reads_present_rows_only(gpu, ref, n, f, B, pad):
