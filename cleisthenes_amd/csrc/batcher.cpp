@@ -20,6 +20,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -119,10 +120,20 @@ struct rbc_batcher {
     int max_batch = 256;
     int max_wait_us = 200;
     std::mutex mu;
-    std::condition_variable cv_work, cv_done;
+    std::condition_variable cv_work;
     std::deque<Req> q[3];
-    std::unordered_map<uint64_t, int> done;  // ticket -> status
-    uint64_t next = 1;
+    // Completed tickets -> status, sharded by ticket so that the callers'
+    // waits and polls (one per request, from many threads) and the worker's
+    // completions contend per shard, not on the queue lock, and a finished
+    // launch wakes only the waiters of the shards it touched.
+    static constexpr int kShards = 64;
+    struct DoneShard {
+        std::mutex mu;
+        std::condition_variable cv;
+        std::unordered_map<uint64_t, int> done;
+    };
+    DoneShard shard[kShards];
+    std::atomic<uint64_t> next{1};
     bool stop = false;
     uint64_t batches = 0, requests = 0;
     std::thread worker;
@@ -297,11 +308,18 @@ void rbc_batcher::finish(Pending &P) {
         });
     }
     if (P.pin) pool.push_back(std::move(P.pin));  // the launch is complete: its buffers are free
+    uint64_t touched = 0;  // bit per shard
+    for (int i = 0; i < count; ++i) {
+        const int sh = (int)(b[i].ticket % kShards);
+        std::lock_guard<std::mutex> lk(shard[sh].mu);
+        shard[sh].done[b[i].ticket] = P.st[i];
+        touched |= 1ull << sh;
+    }
+    for (int sh = 0; sh < kShards; ++sh)
+        if (touched >> sh & 1) shard[sh].cv.notify_all();
     std::lock_guard<std::mutex> lk(mu);
-    for (int i = 0; i < count; ++i) done[b[i].ticket] = P.st[i];
     batches++;
     requests += count;
-    cv_done.notify_all();
 }
 
 // Worker: coalesce, submit asynchronously, and complete launches in order.
@@ -341,12 +359,22 @@ void rbc_batcher::run() {
             cv_work.wait_until(lk, earliest);
             continue;
         }
-        std::vector<Req> batch;
-        while (!q[pick].empty() && (int)batch.size() < max_batch) {
-            batch.push_back(std::move(q[pick].front()));
-            q[pick].pop_front();
+        // take the requests in O(1) under the lock (the whole queue when it
+        // fits one launch), and move them into the batch outside it, so that
+        // the submitting threads are not held up
+        std::deque<Req> taken;
+        if ((int)q[pick].size() <= max_batch) {
+            taken.swap(q[pick]);
+        } else {
+            for (int i = 0; i < max_batch; ++i) {
+                taken.push_back(std::move(q[pick].front()));
+                q[pick].pop_front();
+            }
         }
         lk.unlock();
+        std::vector<Req> batch;
+        batch.reserve(taken.size());
+        for (auto &r : taken) batch.push_back(std::move(r));
         inflight.push_back(submit((Kind)pick, std::move(batch)));
         if (inflight.size() >= depth_max) {
             finish(*inflight.front());
@@ -452,20 +480,25 @@ int rbc_batcher_interpolate(rbc_batcher *b, const uint8_t *root, const uint8_t *
 
 int rbc_batcher_wait(rbc_batcher *b, uint64_t ticket) {
     if (!b) return RBC_ERR_INVALID_ARG;
-    std::unique_lock<std::mutex> lk(b->mu);
-    if (ticket == 0 || ticket >= b->next) return RBC_ERR_INVALID_ARG;
-    b->cv_work.notify_one();
-    b->cv_done.wait(lk, [&] { return b->done.count(ticket) != 0; });
-    const int s = b->done[ticket];
-    b->done.erase(ticket);
+    if (ticket == 0 || ticket >= b->next.load()) return RBC_ERR_INVALID_ARG;
+    auto &sh = b->shard[ticket % rbc_batcher::kShards];
+    std::unique_lock<std::mutex> lk(sh.mu);
+    if (!sh.done.count(ticket)) {
+        b->cv_work.notify_one();  // a waiter: the worker re-checks what is due
+        sh.cv.wait(lk, [&] { return sh.done.count(ticket) != 0; });
+    }
+    const auto it = sh.done.find(ticket);
+    const int s = it->second;
+    sh.done.erase(it);
     return s;
 }
 
 int rbc_batcher_poll(rbc_batcher *b, uint64_t ticket, int *done_out) {
     if (!b || !done_out) return RBC_ERR_INVALID_ARG;
-    std::lock_guard<std::mutex> lk(b->mu);
-    if (ticket == 0 || ticket >= b->next) return RBC_ERR_INVALID_ARG;
-    *done_out = b->done.count(ticket) != 0;
+    if (ticket == 0 || ticket >= b->next.load()) return RBC_ERR_INVALID_ARG;
+    auto &sh = b->shard[ticket % rbc_batcher::kShards];
+    std::lock_guard<std::mutex> lk(sh.mu);
+    *done_out = sh.done.count(ticket) != 0;
     return RBC_OK;
 }
 
