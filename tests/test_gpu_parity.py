@@ -393,6 +393,9 @@ def test_device_too_few_and_root_mismatch(gpu):
 @pytest.mark.parametrize("n,f,B", [
     (4, 1, 1024), (4, 1, 1), (5, 0, 77), (1, 0, 10), (7, 2, 333), (13, 4, 5 * 64), (13, 4, 5 * 55),
     (13, 4, 5 * 56), (13, 4, 5 * 63), (64, 21, 22 * 16), (64, 21, 22 * 15), (256, 85, 86 * 4096 + 3),
+    # the FFT codec's geometries at tiny and odd shard lengths (S = 1, 3, 17, 2, 7, 4097)
+    (128, 42, 1), (128, 42, 44 * 3), (128, 42, 44 * 17 - 5), (64, 21, 22 * 2 - 1), (256, 85, 86 * 7),
+    (128, 42, 44 * 4097),
 ])
 def test_device_pipeline_edge_geometries(gpu, ref, n, f, B):
     I = 5
