@@ -363,6 +363,35 @@ def test_device_pipeline_many_instances_properties(gpu, ref):
     assert np.array_equal(roots, roots2)
 
 
+@pytest.mark.parametrize("n,f,B", [(128, 42, 5000), (256, 85, 3000), (16, 5, 700)])
+def test_device_verify_present_masks_extremes(gpu, ref, n, f, B):
+    """ECHO verify with the present-row compaction: an instance with no
+    received shard, one with every shard, one with a single shard, and random
+    ones (C2 takes the compacted per-leaf walk, C4 the compacted leaves + shared
+    paths): valid = present and proved, exactly."""
+    I = 6
+    pl = Pipeline(gpu, n, f, B, I, seed=n + B, corrupt_frac=0.0)
+    pl.commit()
+    rng = np.random.default_rng(n)
+    present = np.zeros((I, n), np.uint8)
+    present[1] = 1
+    present[2, rng.integers(n)] = 1
+    for i in range(3, I):
+        present[i, rng.permutation(n)[: rng.integers(1, n)]] = 1
+    pl.b["present"].upload(present)
+    sh = pl.shards().copy()
+    sh[4, np.flatnonzero(present[4])[0], 0] ^= 1  # one received shard that does not verify
+    pl.b["shards"].upload(sh)
+    c, b = pl.ctx, pl.b
+    b["valid"].upload(np.full(I * n, 7, np.uint8))
+    c.dev_verify(None, I, b["shards"], pl.spitch, None, pl.S, b["branches"], b["roots"], b["present"], b["valid"],
+                 b["leaves_r"])
+    got = pl.arr("valid", shape=(I, n))
+    want = present.copy()
+    want[4, np.flatnonzero(present[4])[0]] = 0
+    assert np.array_equal(got, want)
+
+
 def test_device_too_few_and_root_mismatch(gpu):
     """present = k-1 -> TOO_FEW_SHARDS; wrong expected root -> ROOT_MISMATCH;
     a corrupted used shard that passes verify (present mask forged) ->
