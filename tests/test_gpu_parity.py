@@ -392,6 +392,36 @@ def test_device_verify_present_masks_extremes(gpu, ref, n, f, B):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("n,f,B", [(128, 42, 44 * 600 + 7), (256, 85, 86 * 500), (64, 21, 22 * 901)])
+def test_device_interpolate_present_set_extremes(gpu, ref, n, f, B):
+    """Interpolate on the FFT codec's geometries with the decode's extreme
+    shapes: exactly k shards all parity (every data row regenerated, m = k),
+    exactly k all data (nothing to solve, every parity row re-encoded), every
+    shard present, and a random k: value, digest and status equal the C
+    oracle's."""
+    k = n - 2 * f
+    I = 4
+    pl = Pipeline(gpu, n, f, B, I, seed=B, corrupt_frac=0.0)
+    pl.commit()
+    present = np.zeros((I, n), np.uint8)
+    present[0, k:2 * k] = 1                       # k parity rows only
+    present[1, :k] = 1                            # the k data rows
+    present[2, :] = 1                             # everything
+    present[3, np.random.default_rng(B).permutation(n)[:k]] = 1
+    pl.b["present"].upload(present)
+    pl.receive()
+    status = pl.arr("status", np.int32)
+    out = pl.arr("out", shape=(I, pl.opitch))
+    digests = pl.arr("digests", shape=(I, 32))
+    sh = pl.shards()
+    roots = pl.arr("roots", shape=(I, 32))
+    for i in range(I):
+        rc, value, dig = ref.interpolate(n, f, sh[i, :, :pl.S] * present[i, :, None], present[i], bytes(roots[i]))
+        assert status[i] == rc == 0, i
+        assert np.array_equal(out[i, :k * pl.S], value) and bytes(digests[i]) == dig, i
+        assert out[i, :B].tobytes() == pl.values[i, :B].tobytes()
+
+
 def test_device_too_few_and_root_mismatch(gpu):
     """present = k-1 -> TOO_FEW_SHARDS; wrong expected root -> ROOT_MISMATCH;
     a corrupted used shard that passes verify (present mask forged) ->
