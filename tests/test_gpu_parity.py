@@ -422,6 +422,32 @@ def test_device_interpolate_present_set_extremes(gpu, ref, n, f, B):
         assert out[i, :B].tobytes() == pl.values[i, :B].tobytes()
 
 
+@pytest.mark.parametrize("n,f,B", [(16, 5, 6 * (32 << 20) + 5), (256, 85, 86 * (1 << 20)), (128, 42, 44 * (4 << 20))],
+                         ids=["S=32MiB", "N=256,S=1MiB", "N=128,S=4MiB"])
+def test_device_pipeline_large_instances(gpu, ref, n, f, B):
+    """Maximum-size shapes: one instance of 0.5-1.2 GiB of shards (row
+    offsets past 2^24 / 2^31 bits of a single row stay exact), through commit,
+    verify and interpolate against the C oracle."""
+    I = 1
+    pl = Pipeline(gpu, n, f, B, I, seed=n, corrupt_frac=1.0)
+    pl.commit()
+    sh = pl.shards()
+    root = bytes(pl.arr("roots", shape=(I, 32))[0])
+    want_sh, want_root, _, _ = ref.encode_commit(n, f, pl.values[0, :B])
+    assert root == want_root
+    assert np.array_equal(sh[0, :, :pl.S], want_sh)
+    pl.receive()
+    assert pl.arr("status", np.int32)[0] == 0
+    out = pl.arr("out", shape=(I, pl.opitch))
+    assert out[0, :B].tobytes() == pl.values[0, :B].tobytes()
+    exp_valid = pl.present[0].copy()
+    exp_valid[pl.corrupt[0]] = 0
+    rx = want_sh.copy()
+    rx[pl.corrupt[0], 0] ^= 0x5A
+    rc, value, dig = ref.interpolate(n, f, rx, exp_valid, want_root)
+    assert rc == 0 and bytes(pl.arr("digests", shape=(I, 32))[0]) == dig
+
+
 def test_device_too_few_and_root_mismatch(gpu):
     """present = k-1 -> TOO_FEW_SHARDS; wrong expected root -> ROOT_MISMATCH;
     a corrupted used shard that passes verify (present mask forged) ->
