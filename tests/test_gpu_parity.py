@@ -953,6 +953,91 @@ def test_host_api_errors_do_not_disturb_tickets_in_flight(gpu, ref):
             assert bytes(r["roots"][i]) == ref.encode_commit(n, f, v)[1]
 
 
+def test_host_api_randomized_interleaving(gpu, ref):
+    """A seeded random mix of the host batch entry points (shard_commit,
+    interpolate, shard_commit_val, validate_batch), pinned or pageable, with
+    more tickets outstanding than slots and waits / polls in random order:
+    every result equals the C oracle.  Exercises slot reuse and the deferred
+    device-to-host copies under arbitrary orderings."""
+    import random
+    from cleisthenes_amd import protocol
+    n, f = 16, 5
+    k = n - 2 * f
+    ctx = gpu.Context(n, f)
+    rnd = random.Random(4242)
+    rng = np.random.default_rng(4242)
+    live = []  # (ticket, check)
+
+    def alloc(shape, pinned):
+        return gpu.pinned_empty(shape) if pinned else np.zeros(shape, np.uint8)
+
+    for step in range(40):
+        kind = rnd.choice(["commit", "interp", "val", "validate"])
+        pinned = rnd.random() < 0.5
+        count = rnd.randint(1, 5)
+        B = rnd.choice([1, 7, 600, 4096, 6 * 1000 + 3])
+        vals = []
+        for _ in range(count):
+            a = alloc(B, pinned)
+            a[:] = rng.integers(0, 256, B, dtype=np.uint8)
+            vals.append(a)
+        want = [ref.encode_commit(n, f, v) for v in vals]
+        if kind == "commit":
+            t = ctx.shard_commit_submit(vals)
+
+            def check(r, want=want):
+                for i, (sh, root, br, _) in enumerate(want):
+                    S = sh.shape[1]
+                    assert np.array_equal(r["shards"][i, :, :S], sh) and bytes(r["roots"][i]) == root
+        elif kind == "val":
+            t = ctx.shard_commit_val_submit(vals)
+
+            def check(r, want=want):
+                for i, (sh, root, br, _) in enumerate(want):
+                    j = rnd.randrange(n)
+                    flat = b"".join(bytes(br[j, lvl]) for lvl in range(ctx.depth) if not (lvl == 0 and (j ^ 1) >= n))
+                    assert r["message"](i, j) == protocol.pb_encode(protocol.VAL, protocol.json_encode_val(
+                        root, flat, bytes(sh[j])))
+        elif kind == "interp":
+            S = want[0][0].shape[1]
+            rx = alloc((count, n, S), pinned)
+            present = np.zeros((count, n), np.uint8)
+            roots = np.zeros((count, 32), np.uint8)
+            for i, (sh, root, _, _) in enumerate(want):
+                present[i, rng.permutation(n)[: rnd.randint(k, n)]] = 1
+                rx[i] = sh * present[i, :, None]
+                roots[i] = np.frombuffer(root, np.uint8)
+            t = ctx.interpolate_submit(rx, [S] * count, present, roots,
+                                       values_out=alloc((count, k * S), pinned) if pinned else None)
+
+            def check(r, vals=vals, B=B):
+                assert (r["status"] == 0).all()
+                for i, v in enumerate(vals):
+                    assert r["values"][i, :B].tobytes() == v.tobytes()
+        else:
+            sh, root, br, _ = want[0]
+            js = [rnd.randrange(n) for _ in range(6)]
+            shards = [bytes(sh[j]) for j in js]
+            bad = rnd.randrange(6)
+            shards[bad] = bytes([shards[bad][0] ^ 1]) + shards[bad][1:]
+            flats = [b"".join(bytes(br[j, lvl]) for lvl in range(ctx.depth) if not (lvl == 0 and (j ^ 1) >= n))
+                     for j in js]
+            ok = ctx.validate_batch(shards, js, flats, [root] * 6)  # synchronous
+            assert list(ok) == [i != bad for i in range(6)]
+            continue
+        live.append((t, check))
+        # randomly complete some outstanding tickets, in random order
+        while live and rnd.random() < 0.4:
+            i = rnd.randrange(len(live))
+            t, chk = live.pop(i)
+            if rnd.random() < 0.5:
+                t.done()
+            chk(t.wait())
+    rnd.shuffle(live)
+    for t, chk in live:
+        chk(t.wait())
+
+
 @pytest.mark.parametrize("n,f,B,pad", [(16, 5, 6000, 0), (16, 5, 5999, 13), (128, 42, 1 << 20, 0),
                                         (256, 85, 64 << 10, 5), (4, 1, 1, 3)])
 def test_host_interpolate_zero_copy_reads_present_rows_only(gpu, ref, n, f, B, pad):
