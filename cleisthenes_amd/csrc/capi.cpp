@@ -64,6 +64,12 @@ int gf_md_rcmax(uint32_t shard_pitch) {
     return v ? v : (shard_pitch <= 2048 ? 4 : 8);
 }
 
+int env_prio(const char *name) {
+    const char *e = getenv(name);
+    const int x = e ? atoi(e) : 0;
+    return (x >= 0 && x <= 3) ? x : 0;
+}
+
 int tree_width(int n) {
     int w = 1;
     while (w < n) w <<= 1;
@@ -181,6 +187,11 @@ int host_slots() {
 struct rbc_ctx {
     int n = 0, f = 0, k = 0, p = 0, depth = 0, width = 0, device = 0;
     bool fft = false;              // additive-FFT codec active (rs_fft.hip)
+    // wave issue priorities (s_setprio 0..3) of the commit-side kernels
+    // (encode, leaves, tree build) and the receive-side ones (verify,
+    // interpolate); rbc_ctx_set_wave_priority, RBC_TX_PRIO / RBC_RX_PRIO
+    int tx_prio = 0, rx_prio = 0;
+    int rxv_prio = 0;              // ECHO verify (RBC_RXV_PRIO A/B; else rx_prio)
     std::vector<uint8_t> h_M;      // n x k encode matrix
     uint8_t *d_M = nullptr;        // device copy; parity rows at d_M + k*k
     std::mutex mu;
@@ -221,6 +232,9 @@ int ctx_create_kn(int n, int k, int device, rbc_ctx **out) {
     c->depth = tree_depth(n);
     c->device = device;
     c->fft = codec_default() != RBC_CODEC_MATRIX && rbc_fft_supported(n, k);
+    c->tx_prio = env_prio("RBC_TX_PRIO");
+    c->rx_prio = env_prio("RBC_RX_PRIO");
+    c->rxv_prio = getenv("RBC_RXV_PRIO") ? env_prio("RBC_RXV_PRIO") : c->rx_prio;
     if (!rbchost::build_matrix(k, n, c->h_M)) { delete c; return RBC_ERR_SINGULAR; }
     // d_M = [n x k encode matrix | exp[512] | log[256]] (tables for decode_prepare_fft)
     std::vector<uint8_t> up(c->h_M);
@@ -280,6 +294,7 @@ int stage_encode(rbc_ctx *c, hipStream_t st, int count, const uint8_t *values, u
         a.row_pitch = shard_pitch;
         a.lens = value_lens;
         a.uniform_len = uniform_value_len;
+        a.prio = c->tx_prio;
         RBC_HIP(rbc_launch_rs_fft(a, st));
         return RBC_OK;
     }
@@ -301,6 +316,7 @@ int stage_encode(rbc_ctx *c, hipStream_t st, int count, const uint8_t *values, u
     g.uniform_len = uniform_value_len;
     g.coef = c->d_M + (size_t)c->k * c->k;
     g.coef_inst_stride = 0;
+    g.prio = c->tx_prio;
     RBC_HIP(rbc_launch_gf_rows(g, st));
     return RBC_OK;
 }
@@ -323,6 +339,7 @@ int stage_leaves(rbc_ctx *c, hipStream_t st, int count, const uint8_t *shards, u
     a.leaves_inst_pitch = (uint64_t)c->n * 32;
     a.n = c->n;
     a.depth = c->depth;
+    a.prio = c->tx_prio;
     RBC_HIP(rbc_launch_sha_rows(a, false, st));
     return RBC_OK;
 }
@@ -342,6 +359,7 @@ int stage_merkle_build(rbc_ctx *c, hipStream_t st, int count, const uint8_t *lea
     m.roots = roots;
     m.branches = c->depth > 0 ? branches : nullptr;
     m.br_inst_pitch = (uint64_t)c->n * c->depth * 32;
+    m.prio = c->tx_prio;
     RBC_HIP(rbc_launch_merkle(m, false, st));
     return RBC_OK;
 }
@@ -371,6 +389,7 @@ int stage_verify(rbc_ctx *c, hipStream_t st, int count, const uint8_t *shards, u
     a.roots = roots;
     a.present = present;
     a.valid = valid;
+    a.prio = c->rxv_prio;
     // Shared-path verification: leaves, then one hash per
     // distinct branch-walk input.  RBC_VERIFY_PATH=0 runs the per-leaf walk.
     static const int path_env = [] {  // 0 never, 1 (default) where it pays, 2 always
@@ -426,6 +445,7 @@ int stage_verify(rbc_ctx *c, hipStream_t st, int count, const uint8_t *shards, u
         p.roots = roots;
         p.present = present;
         p.valid = valid;
+        p.prio = c->rxv_prio;
         RBC_HIP(rbc_launch_merkle_path(p, st));
         return RBC_OK;
     }
@@ -527,6 +547,7 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
         g.idx_stride2 = pa.regen_stride;
         g.status = status;
         g.rcount = pa.rcount;
+        g.prio = c->rx_prio;
         RBC_HIP(rbc_launch_gf_rows(g, st));
         // 2) parity positions: additive-FFT re-encode of the completed data half
         FftArgs a{};
@@ -549,6 +570,7 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
         }
         a.values_out = values_out;  // join fused into the re-encode (it loads every data row anyway)
         a.value_pitch_out = value_pitch;
+        a.prio = c->rx_prio;
         RBC_HIP(rbc_launch_rs_fft(a, st));
     } else if (nr > 0) {
         GfArgs g{};
@@ -582,6 +604,7 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
             g.counter = pa.counter;
             g.n = c->n;
         }
+        g.prio = c->rx_prio;
         RBC_HIP(rbc_launch_gf_rows(g, st));
     }
     return RBC_OK;
@@ -645,6 +668,7 @@ int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *sha
         j.values = values_out;
         j.value_pitch = value_pitch;
         j.status = status;
+        j.prio = c->rx_prio;
         RBC_HIP(rbc_launch_join(j, js));
     }
     if (fork) RBC_HIP(hipEventRecord(w.ev_join, w.aux));
@@ -663,6 +687,7 @@ int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *sha
     a.leaves_inst_pitch = (uint64_t)c->n * 32;
     a.n = c->n;
     a.depth = c->depth;
+    a.prio = c->rx_prio;
     if (leaves_verified) {
         // hash only the rows in the device-built list: every missing position
         // plus any valid-but-unused shard the re-encoding disagreed with
@@ -684,6 +709,7 @@ int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *sha
     m.leaves_inst_pitch = (uint64_t)c->n * 32;
     m.expect_roots = roots;
     m.status = status;
+    m.prio = c->rx_prio;
     RBC_HIP(rbc_launch_merkle(m, true, st));
     if (digests)
         RBC_HIP(rbc_launch_digest(leaves, (uint64_t)c->n * 32, c->k, status, digests, count, st));
@@ -822,6 +848,14 @@ int rbc_ctx_params(const rbc_ctx *c, int *k, int *p, int *depth) {
     if (k) *k = c->k;
     if (p) *p = c->p;
     if (depth) *depth = c->depth;
+    return RBC_OK;
+}
+
+int rbc_ctx_set_wave_priority(rbc_ctx *c, int commit_prio, int receive_prio) {
+    if (!c || commit_prio < 0 || commit_prio > 3 || receive_prio < 0 || receive_prio > 3) return RBC_ERR_INVALID_ARG;
+    c->tx_prio = commit_prio;
+    c->rx_prio = receive_prio;
+    c->rxv_prio = receive_prio;
     return RBC_OK;
 }
 

@@ -18,6 +18,18 @@
 
 #define RBC_DEV __device__ __forceinline__
 
+// Wave issue priority (s_setprio, 0..3) from a kernel argument: the SIMD's
+// instruction arbiter prefers higher-priority waves.  Two streams of
+// VALU-bound kernels share every SIMD under the bench's pipeline; raising
+// the waves of the stream on the critical path lets its dependent SHA
+// chains issue as if alone while the other stream fills the gaps.
+// `p` is a kernel argument, so the branch is uniform (scalar).
+RBC_DEV void set_wave_prio(int p) {
+    if (p == 1) __builtin_amdgcn_s_setprio(1);
+    else if (p == 2) __builtin_amdgcn_s_setprio(2);
+    else if (p >= 3) __builtin_amdgcn_s_setprio(3);
+}
+
 namespace rbcdev {
 
 RBC_DEV uint32_t rotr(uint32_t x, uint32_t n) { return __builtin_amdgcn_alignbit(x, x, n); }

@@ -42,6 +42,7 @@ struct GfArgs {
     uint32_t *counter;
     int n;
     const int32_t *rcount;     // per-instance output row count (nullable -> R)
+    int prio;                  // wave issue priority 0..3 (set_wave_prio)
 };
 
 struct ShaArgs {
@@ -67,6 +68,7 @@ struct ShaArgs {
     const uint8_t *roots;      // [I][32]
     const uint8_t *present;    // [I][N] (nullable -> all present)
     uint8_t *valid;            // [I][N]
+    int prio;                  // wave issue priority 0..3 (set_wave_prio)
 };
 
 struct MerkleArgs {
@@ -80,6 +82,7 @@ struct MerkleArgs {
     int32_t *status;           // check: in/out
     uint8_t *digests;          // check: [I][32] (nullable)
     int trees_per_block;       // set by rbc_launch_merkle
+    int prio;                  // wave issue priority 0..3 (set_wave_prio)
 };
 
 // merkle_path_kernel: shared-path branch verification over precomputed leaves
@@ -94,6 +97,7 @@ struct PathArgs {
     const int32_t *status;     // nullable
     uint8_t *valid;            // [I][N]
     int inst_per_block;        // set by rbc_launch_merkle_path
+    int prio;                  // wave issue priority 0..3 (set_wave_prio)
 };
 
 struct PrepArgs {
@@ -137,6 +141,7 @@ struct JoinArgs {
     uint8_t *values;           // [I][value_pitch]
     uint32_t value_pitch;
     const int32_t *status;
+    int prio;                  // wave issue priority 0..3 (set_wave_prio)
 };
 
 // rs_fft_kernel (rs_fft.hip): additive-FFT systematic encode, one lane per
@@ -164,6 +169,7 @@ struct FftArgs {
     // written straight from the loaded data rows (nullable)
     uint8_t *values_out;
     uint32_t value_pitch_out;
+    int prio;                  // wave issue priority 0..3 (set_wave_prio)
 };
 
 bool rbc_fft_supported(int n, int k);

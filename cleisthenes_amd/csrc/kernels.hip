@@ -66,6 +66,7 @@ RBC_DEV uint4 mask16(uint4 v, int nvalid) {
 // ============================================================================
 template <int RC, int TPB>
 __global__ __launch_bounds__(TPB, (RC <= 21 ? 3 : 2)) void gf_rows_kernel(GfArgs a) {
+    set_wave_prio(a.prio);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int KP = (a.K + 1) & ~1;
     uint4 *s_t01 = reinterpret_cast<uint4 *>(smem);
@@ -225,6 +226,7 @@ __global__ __launch_bounds__(TPB, (RC <= 21 ? 3 : 2)) void gf_rows_kernel(GfArgs
 // ============================================================================
 template <int RC>
 __global__ __launch_bounds__(64) void gf_short_kernel(GfArgs a) {
+    set_wave_prio(a.prio);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int TPB = 64;
     const int KP = (a.K + 1) & ~1;
@@ -313,6 +315,7 @@ __global__ __launch_bounds__(64) void gf_short_kernel(GfArgs a) {
 // ============================================================================
 template <bool VERIFY>
 __global__ __launch_bounds__(256) void sha_rows_kernel(ShaArgs a) {
+    set_wave_prio(a.prio);
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     int inst, pos;
     if (a.list) {  // compacted (inst, pos) work list built on the device
@@ -377,6 +380,7 @@ __global__ __launch_bounds__(256) void sha_rows_kernel(ShaArgs a) {
 // per-message verify keep sha_rows_kernel.
 template <bool VERIFY>
 __global__ __launch_bounds__(256) void sha_rows2_kernel(ShaArgs a) {
+    set_wave_prio(a.prio);
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int half = a.rows_per_inst >> 1;
     if (t >= a.count * half) return;
@@ -452,6 +456,7 @@ __global__ __launch_bounds__(256) void sha_rows2_kernel(ShaArgs a) {
 // ============================================================================
 template <bool CHECK>
 __global__ __launch_bounds__(64) void merkle_kernel(MerkleArgs a) {
+    set_wave_prio(a.prio);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t *nodes = reinterpret_cast<uint32_t *>(smem);
     const int G = a.trees_per_block, W = a.width, n = a.n;
@@ -589,6 +594,7 @@ __global__ __launch_bounds__(64) void merkle_kernel(MerkleArgs a) {
 // ============================================================================
 template <int L>
 __global__ __launch_bounds__(64) void merkle_path_kernel(PathArgs a) {
+    set_wave_prio(a.prio);
     // one wave per block; lane owns leaf positions p = s*64 + lane (s < L)
     __shared__ uint32_t s_pair[64 * L][17];  // +1 word: conflict-free rows; an owner's task
                                               // digest overwrites words 0..7 of its own row
@@ -1000,6 +1006,7 @@ __global__ __launch_bounds__(256) void decode_prepare_fft_kernel(PrepArgs a, con
 // ============================================================================
 constexpr int JOIN_U = 4;
 __global__ __launch_bounds__(256) void join_kernel(JoinArgs a) {
+    set_wave_prio(a.prio);
     const int inst = (int)(blockIdx.x / a.blocks_per_inst);
     const uint32_t tile = blockIdx.x - (uint32_t)inst * a.blocks_per_inst;
     if (a.status && a.status[inst] != 0) return;

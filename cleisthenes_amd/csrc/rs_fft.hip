@@ -271,6 +271,7 @@ template <int LOGW, int K, int N, int MODE>
 // waves_per_eu(2): at N=256 the decode variant otherwise takes 256 VGPRs + 25
 // AGPRs (one wave per SIMD); with the hint it fits 256 with no scratch
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void rs_fft_kernel(FftArgs a) {
+    set_wave_prio(a.prio);
     constexpr int W = 1 << LOGW;
     constexpr int G = 3;   // encode: outputs are stored in groups of 2^G rows
 #ifndef RBC_FFT_GD

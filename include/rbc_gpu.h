@@ -83,6 +83,12 @@ int rbc_ctx_encode_matrix(const rbc_ctx *ctx, uint8_t *out);
 #define RBC_CODEC_FFT 2
 int rbc_ctx_set_codec(rbc_ctx *ctx, int codec);
 int rbc_ctx_codec(const rbc_ctx *ctx, int *codec); /* effective: MATRIX or FFT */
+/* Wave issue priority (0..3, the SIMD arbiter's s_setprio level) of this
+ * context's commit-side kernels (encode, leaf hashing, tree build) and
+ * receive-side kernels (ECHO verify, interpolate).  Only matters when both
+ * sides run concurrently on two streams; results are identical either way.
+ * Defaults: RBC_TX_PRIO / RBC_RX_PRIO from the environment, else 0. */
+int rbc_ctx_set_wave_priority(rbc_ctx *ctx, int commit_prio, int receive_prio);
 
 /* ---- device memory / streams / events (so a host runtime needs no other
  *      GPU library to drive the rbc_dev_* path) ---------------------------- */
