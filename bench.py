@@ -288,6 +288,14 @@ def main(argv):
     if phased:
         set_bytes += I * (opitch + 32 + 4)  # per-set value / digest / status (decode and check run apart)
     nsets = max(3 if pipe3 else 2, args.sets) if pipe else 1
+    # Wave issue priority (s_setprio) under the two-stream schedule: the
+    # receiver stream (verify + interpolate, whose regen-hash tail is a
+    # latency-bound dependent chain) at 2, the proposer at 0.  A/B on one box
+    # (tools/gpu_r02prio*.sh): 442-446 GB/s at 0/0, 447-451 at 0/2, 411 at 3/0.
+    # RBC_TX_PRIO / RBC_RX_PRIO override.
+    prio_tx = int(os.environ.get("RBC_TX_PRIO", "0"))
+    prio_rx = int(os.environ.get("RBC_RX_PRIO", "2" if pipe else "0"))
+    ctx.set_wave_priority(prio_tx, prio_rx)
     budget = float(os.environ.get("RBC_BENCH_HBM_BUDGET", 250e9))
     while pipe and nsets * set_bytes + other_bytes > budget:
         nsets -= 1
@@ -882,6 +890,7 @@ def main(argv):
                    "parallelism": f"instances partitioned over {world} GPU(s) in contiguous blocks"
                                   + (", RCCL all-gather of {root,digest} records" if gather else ""),
                    "gf_codec": ctx.codec,
+                   "wave_priority": {"commit": prio_tx, "receive": prio_rx},
                    **({"rehearsal": "all ranks on device 0, no RCCL (not a multi-GPU measurement)"}
                       if args.rehearse_on_one_gpu else {}),
                    "pipeline": ((f"balanced: commit(t) then rehash+check(t-2) || verify+decode(t-1), two streams, "

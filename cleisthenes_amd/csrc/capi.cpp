@@ -122,10 +122,11 @@ struct Ws {
     // the box has GPU_MAX_HW_QUEUES = 4 hardware queues per process)
     bool fork = true;
     hipStream_t aux = nullptr;  // created on first use
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_hashed = nullptr;
     bool init() {
         return hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) == hipSuccess &&
-               hipEventCreateWithFlags(&ev_join, hipEventDisableTiming) == hipSuccess;
+               hipEventCreateWithFlags(&ev_join, hipEventDisableTiming) == hipSuccess &&
+               hipEventCreateWithFlags(&ev_hashed, hipEventDisableTiming) == hipSuccess;
     }
     void release() {
         for (DevBuf *b : {&used, &regen, &dmat, &nmiss, &flags, &list, &counter, &rcount, &cls, &vleaves, &vlist})
@@ -133,8 +134,9 @@ struct Ws {
         if (aux) (void)hipStreamDestroy(aux);
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         if (ev_join) (void)hipEventDestroy(ev_join);
+        if (ev_hashed) (void)hipEventDestroy(ev_hashed);
         aux = nullptr;
-        ev_fork = ev_join = nullptr;
+        ev_fork = ev_join = ev_hashed = nullptr;
     }
 };
 
@@ -671,7 +673,6 @@ int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *sha
         j.prio = c->rx_prio;
         RBC_HIP(rbc_launch_join(j, js));
     }
-    if (fork) RBC_HIP(hipEventRecord(w.ev_join, w.aux));
     }
     }  // decode phase
     const int nr = c->n - c->k;
@@ -710,11 +711,27 @@ int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *sha
     m.expect_roots = roots;
     m.status = status;
     m.prio = c->rx_prio;
+    // the batch digest (one serial 23-compression chain per instance at C2)
+    // needs only the data leaves: with the fork it runs on the aux stream
+    // beside the root recheck instead of after it
+    static const bool digest_fork = [] {  // RBC_DIGEST_FORK=0: digest after the recheck (A/B)
+        const char *e = getenv("RBC_DIGEST_FORK");
+        return !e || atoi(e) != 0;
+    }();
+    hipStream_t ds = st;
+    if (fork && digests && digest_fork) {
+        RBC_HIP(hipEventRecord(w.ev_hashed, st));
+        RBC_HIP(hipStreamWaitEvent(w.aux, w.ev_hashed, 0));
+        ds = w.aux;
+    }
     RBC_HIP(rbc_launch_merkle(m, true, st));
     if (digests)
-        RBC_HIP(rbc_launch_digest(leaves, (uint64_t)c->n * 32, c->k, status, digests, count, st));
+        RBC_HIP(rbc_launch_digest(leaves, (uint64_t)c->n * 32, c->k, status, digests, count, ds));
     }  // check phase
-    if (fork) RBC_HIP(hipStreamWaitEvent(st, w.ev_join, 0));  // join back before returning
+    if (fork) {  // join back before returning
+        RBC_HIP(hipEventRecord(w.ev_join, w.aux));
+        RBC_HIP(hipStreamWaitEvent(st, w.ev_join, 0));
+    }
     return RBC_OK;
 }
 

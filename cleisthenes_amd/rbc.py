@@ -242,6 +242,10 @@ class Context:
         check(lib.rbc_ctx_codec(self._p, byref(c)))
         return "fft" if c.value == self.CODEC_FFT else "matrix"
 
+    def set_wave_priority(self, commit: int, receive: int) -> None:
+        """s_setprio level (0..3) of the commit-side / receive-side kernels."""
+        check(lib.rbc_ctx_set_wave_priority(self._p, commit, receive), "rbc_ctx_set_wave_priority")
+
     def set_codec(self, codec: str) -> None:
         check(lib.rbc_ctx_set_codec(self._p, {"auto": 0, "matrix": 1, "fft": 2}[codec]), "rbc_ctx_set_codec")
 

@@ -158,7 +158,8 @@ int rbc_dev_verify(rbc_ctx *ctx, void *stream, int count, const uint8_t *shards,
  * write value = data shards 0..k-1 concatenated (k*S_i bytes, pad kept) to
  * values_out [count][value_pitch] (bytes past k*S_i are unspecified, and a
  * row is defined only where status[i] == RBC_OK) and the batch digest
- * SHA-256(leaf_0 || .. || leaf_{k-1}) to digests [count][32].
+ * SHA-256(leaf_0 || .. || leaf_{k-1}) to digests [count][32] (likewise
+ * defined only where status[i] == RBC_OK).
  * status[i]: RBC_OK, RBC_ERR_TOO_FEW_SHARDS or RBC_ERR_ROOT_MISMATCH.
  * leaves_verified != 0: `leaves` already holds SHA-256 of the valid shards
  * (rbc_dev_verify output) and only regenerated rows are hashed; 0: all rows. */
