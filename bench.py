@@ -92,6 +92,7 @@ def parse_args(argv):
                          "together (leaves(t) || verify(t-1) || regen hashing(t-2)), then their GF/FFT/tree "
                          "phases together; 4: as 1 with verify(t-1) split by instances over both streams; "
                          "5: balanced two streams -- commit(t) then rehash+check(t-2) || verify+decode(t-1); "
+                         "6: as 1, commit(t) starts when the receiver has DECODED t-2 (overlaps its rehash tail); "
                          "0: one stream, stages in order")
     ap.add_argument("--sets", type=int, default=0,
                     help="shard buffer sets of the pipelined schedule (0: the minimum, 2 for --pipeline 1, "
@@ -287,7 +288,8 @@ def main(argv):
         set_bytes += I * (n + n * 32)  # per-set valid + verified leaves (verify and interpolate run apart)
     if phased:
         set_bytes += I * (opitch + 32 + 4)  # per-set value / digest / status (decode and check run apart)
-    nsets = max(3 if pipe3 else 2, args.sets) if pipe else 1
+    pdec = args.pipeline == 6  # commit(t) starts when the receiver finished DECODING t-2
+    nsets = max(3 if (pipe3 or pdec) else 2, args.sets) if pipe else 1
     # Wave issue priority (s_setprio) under the two-stream schedule: the
     # receiver stream (verify + interpolate, whose regen-hash tail is a
     # latency-bound dependent chain) at 2, the proposer at 0.  A/B on one box
@@ -436,7 +438,13 @@ def main(argv):
     # decoding t-2: the commit then overlaps the decode's tail, not its head
     pwait_verify = os.environ.get("RBC_BENCH_PWAIT", "") == "verify" and nsets >= 3
     evRV = [ca.Event() for _ in range(nsets)]
-    for e in evRV:
+    # --pipeline 6: interpolate(t-1) runs as DECODE (value join forked onto
+    # the aux stream) then REHASH + CHECK; commit(t) waits for the DECODE of
+    # t-2 (which implies batch t-3, the last reader of set t % 3, is done),
+    # so the commit overlaps the latency-bound regen-hash tail instead of
+    # starting when it ends
+    evRD = [ca.Event() for _ in range(nsets)]
+    for e in evRV + evRD:
         e.record(stream)
 
     def pstep(t, ev=None):
@@ -447,6 +455,9 @@ def main(argv):
         if pwait_verify:
             if t >= 2:
                 P.wait(evRV[(t - 2) % nsets])
+        elif pdec:
+            if t >= 2:
+                P.wait(evRD[(t - 2) % nsets])
         else:
             P.wait(evR[t % nsets])
         recP("t0")
@@ -468,8 +479,15 @@ def main(argv):
                        d_leaves_r)
         recR("verify")
         evRV[(t - 1) % nsets].record(R)
-        ctx.dev_interpolate(R.ptr, I, sr["shards"], spitch, None, S, d_valid, d_leaves_r, 1, sr["roots"], d_out,
-                            opitch, d_digests, d_status)
+        if pdec:
+            iargs = (I, sr["shards"], spitch, None, S, d_valid, d_leaves_r, 1, sr["roots"], d_out, opitch,
+                     d_digests, d_status)
+            ctx.dev_interpolate_phases(R.ptr, ctx.INTERP_DECODE | ctx.INTERP_FORK, *iargs)
+            evRD[(t - 1) % nsets].record(R)
+            ctx.dev_interpolate_phases(R.ptr, ctx.INTERP_REHASH | ctx.INTERP_CHECK, *iargs)
+        else:
+            ctx.dev_interpolate(R.ptr, I, sr["shards"], spitch, None, S, d_valid, d_leaves_r, 1, sr["roots"],
+                                d_out, opitch, d_digests, d_status)
         recR("interp")
         if gather:
             ctx.dev_allgather_records(R.ptr, I, slots, sr["roots"], d_digests, d_status, d_gather)
@@ -901,6 +919,8 @@ def main(argv):
                                  "sets") if pipe3 else
                                 (f"verify(t-1) first half || second half, then commit(t) || interpolate(t-1), "
                                  f"two streams, {nsets} shard sets") if vsplit else
+                                (f"commit(t) from decode(t-2) on || verify+interpolate(t-1) (decode, then "
+                                 f"rehash+check), two streams, {nsets} shard sets") if pdec else
                                 (f"commit(t) || verify+interpolate(t-1) on two streams, {nsets} shard sets")
                                 if pipe else "serial")},
         "stage_ms": {kk: round(v, 4) for kk, v in stage_ms.items()},

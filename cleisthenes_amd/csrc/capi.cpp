@@ -121,6 +121,7 @@ struct Ws {
     // stream each (their concurrency comes from the slots themselves, and
     // the box has GPU_MAX_HW_QUEUES = 4 hardware queues per process)
     bool fork = true;
+    bool join_pending = false;  // a forked join awaits its CHECK phase
     hipStream_t aux = nullptr;  // created on first use
     hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_hashed = nullptr;
     bool init() {
@@ -421,7 +422,7 @@ int stage_verify(rbc_ctx *c, hipStream_t st, int count, const uint8_t *shards, u
             vc = vl + (size_t)count * c->n;
         }
         RBC_HIP(hipMemsetAsync(vc, 0, 4, st));
-        RBC_HIP(rbc_launch_compact_present(present, c->n, count, valid, vl, vc, st));
+        RBC_HIP(rbc_launch_compact_present(present, c->n, count, valid, vl, vc, st, c->rxv_prio));
         a.list = vl;
         a.list_count = vc;
     }
@@ -493,6 +494,7 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
     pa.dmat = w.dmat.as<uint8_t>();
     pa.dmat_stride = (uint64_t)std::max(nr, 1) * c->k;
     pa.status = status;
+    pa.prio = c->rx_prio;
     if (compare) {
         pa.nmiss = w.nmiss.as<int32_t>();
         pa.flags = w.flags.as<uint32_t>();
@@ -615,14 +617,19 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
 // interpolate phases: 1 = decode (prepare, missing-data GF, FFT re-encode +
 // compare, value join), 2 = rehash (SHA of the regenerated rows), 4 = check
 // (Merkle root recheck + batch digest).  All three (7) is rbc_dev_interpolate;
-// the join then forks onto the aux stream beside the rehash.
-constexpr int kPhaseDecode = 1, kPhaseRehash = 2, kPhaseCheck = 4, kPhaseAll = 7;
+// the join then forks onto the aux stream beside the rehash.  8 = fork: a
+// DECODE call runs its join on the aux stream and the same batch's later
+// CHECK call joins it back (rbc_dev_interpolate_phases, RBC_INTERP_FORK).
+constexpr int kPhaseDecode = 1, kPhaseRehash = 2, kPhaseCheck = 4, kPhaseAll = 7, kPhaseFork = 8;
 
 int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shards, uint32_t shard_pitch,
                       const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *valid, uint8_t *leaves,
                       int leaves_verified, const uint8_t *roots, uint8_t *values_out, uint32_t value_pitch,
                       uint8_t *digests, int32_t *status, int phases = kPhaseAll) {
-    if (phases < 1 || phases > kPhaseAll) return RBC_ERR_INVALID_ARG;
+    if (phases & ~(kPhaseAll | kPhaseFork)) return RBC_ERR_INVALID_ARG;
+    const bool fork_req = (phases & kPhaseFork) != 0;
+    phases &= kPhaseAll;
+    if (phases < 1) return RBC_ERR_INVALID_ARG;
     if (count < 0 || (count > 0 && (!shards || !valid || !leaves || !roots || !values_out || !status)))
         return RBC_ERR_INVALID_ARG;
     if (shard_pitch % kAlign || value_pitch % 16) return RBC_ERR_INVALID_ARG;
@@ -643,7 +650,10 @@ int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *sha
     // value assembly (HBM-bound) forks onto the aux stream beside the regen
     // hashing (latency-bound, under-fills the SIMDs); it needs only the
     // regenerated rows.  values_out is defined where status == 0.
-    const bool fork = !fused_join && w.fork && phases == kPhaseAll;
+    // (phased calls: only on request, since the join is then outstanding on
+    // the aux stream until the batch's CHECK call)
+    const bool fork = !fused_join && w.fork && (phases == kPhaseAll || (fork_req && (phases & kPhaseDecode)));
+    if (phases & kPhaseDecode) w.join_pending = fork;
     if (phases & kPhaseDecode) {
     int rc = stage_regenerate(c, w, st, count, shards, shard_pitch, shard_lens, uniform_shard_len, valid, status,
                               leaves_verified, fused_join ? values_out : nullptr, value_pitch);
@@ -719,16 +729,17 @@ int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *sha
         return !e || atoi(e) != 0;
     }();
     hipStream_t ds = st;
-    if (fork && digests && digest_fork) {
+    if (w.join_pending && digests && digest_fork) {
         RBC_HIP(hipEventRecord(w.ev_hashed, st));
         RBC_HIP(hipStreamWaitEvent(w.aux, w.ev_hashed, 0));
         ds = w.aux;
     }
     RBC_HIP(rbc_launch_merkle(m, true, st));
     if (digests)
-        RBC_HIP(rbc_launch_digest(leaves, (uint64_t)c->n * 32, c->k, status, digests, count, ds));
+        RBC_HIP(rbc_launch_digest(leaves, (uint64_t)c->n * 32, c->k, status, digests, count, ds, c->rx_prio));
     }  // check phase
-    if (fork) {  // join back before returning
+    if (w.join_pending && (phases & kPhaseCheck)) {  // join back before returning
+        w.join_pending = false;
         RBC_HIP(hipEventRecord(w.ev_join, w.aux));
         RBC_HIP(hipStreamWaitEvent(st, w.ev_join, 0));
     }

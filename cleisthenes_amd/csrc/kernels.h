@@ -126,6 +126,7 @@ struct PrepArgs {
     uint32_t cls_stride;
     const uint8_t *gf_exp;     // device exp[512] / log[256] tables (FFT prepare)
     const uint8_t *gf_log;
+    int prio;                  // wave issue priority 0..3 (set_wave_prio)
 };
 
 struct JoinArgs {
@@ -200,12 +201,12 @@ hipError_t rbc_launch_merkle(const MerkleArgs &a, bool check, hipStream_t st);
 hipError_t rbc_launch_merkle_path(const PathArgs &a, hipStream_t st);
 hipError_t rbc_launch_decode_prepare(const PrepArgs &a, hipStream_t st);
 hipError_t rbc_launch_digest(const uint8_t *leaves, uint64_t leaves_inst_pitch, int k, const int32_t *status,
-                             uint8_t *digests, int count, hipStream_t st);
+                             uint8_t *digests, int count, hipStream_t st, int prio = 0);
 hipError_t rbc_launch_join(const JoinArgs &a, hipStream_t st);
 hipError_t rbc_launch_inject_faults(uint8_t *shards, uint64_t inst_pitch, uint32_t row_pitch,
                                     const int32_t *corrupt, int count, hipStream_t st);
 hipError_t rbc_launch_compact_present(const uint8_t *present, int n, int count, uint8_t *valid, uint32_t *list,
-                                     uint32_t *counter, hipStream_t st);
+                                     uint32_t *counter, hipStream_t st, int prio = 0);
 hipError_t rbc_launch_pack_records(const uint8_t *roots, const uint8_t *digests, const int32_t *status, int count,
                                    int slots, uint8_t *out, hipStream_t st);
 hipError_t rbc_launch_fill_random(uint8_t *dst, uint64_t first_row, uint64_t rows, uint64_t pitch, uint64_t seed,

@@ -748,7 +748,8 @@ __global__ __launch_bounds__(64) void merkle_path_kernel(PathArgs a) {
 // assembled from 16-byte reads inside that range only (no over-read).
 // ============================================================================
 __global__ __launch_bounds__(64) void digest_kernel(const uint8_t *leaves, uint64_t leaves_inst_pitch, int k,
-                                                    const int32_t *status, uint8_t *digests, int count) {
+                                                    const int32_t *status, uint8_t *digests, int count, int prio) {
+    set_wave_prio(prio);
     const int inst = blockIdx.x * blockDim.x + threadIdx.x;
     if (inst >= count) return;
     if (status && status[inst] != 0) return;
@@ -795,6 +796,7 @@ __global__ __launch_bounds__(64) void digest_kernel(const uint8_t *leaves, uint6
 // regenerates every non-used position (data and parity) of the re-encoding.
 // ============================================================================
 __global__ __launch_bounds__(256) void decode_prepare_kernel(PrepArgs a) {
+    set_wave_prio(a.prio);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int n = a.n, k = a.k;
     uint8_t *s_exp = smem;             // 512
@@ -888,6 +890,7 @@ __global__ __launch_bounds__(256) void decode_prepare_kernel(PrepArgs a) {
 // ============================================================================
 __global__ __launch_bounds__(256) void decode_prepare_fft_kernel(PrepArgs a, const uint8_t *exp_tab,
                                                                   const uint8_t *log_tab) {
+    set_wave_prio(a.prio);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int n = a.n, k = a.k;
     uint8_t *s_exp = smem;           // 512
@@ -1086,7 +1089,9 @@ __global__ void inject_faults_kernel(uint8_t *shards, uint64_t inst_pitch, uint3
 // ============================================================================
 constexpr int COMPACT_IPB = 16;
 __global__ __launch_bounds__(256) void compact_present_kernel(const uint8_t *present, int n, int count,
-                                                              uint8_t *valid, uint32_t *list, uint32_t *counter) {
+                                                              uint8_t *valid, uint32_t *list, uint32_t *counter,
+                                                              int prio) {
+    set_wave_prio(prio);
     __shared__ uint32_t s_cnt[COMPACT_IPB];
     __shared__ uint32_t s_base;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1240,11 +1245,11 @@ __global__ __launch_bounds__(256) void gather_present_kernel(const uint8_t *host
 // launchers
 // ============================================================================
 hipError_t rbc_launch_compact_present(const uint8_t *present, int n, int count, uint8_t *valid, uint32_t *list,
-                                     uint32_t *counter, hipStream_t st) {
+                                     uint32_t *counter, hipStream_t st, int prio) {
     if (count <= 0) return hipSuccess;
     if (n > 256) return hipErrorInvalidValue;
     hipLaunchKernelGGL(compact_present_kernel, dim3((count + COMPACT_IPB - 1) / COMPACT_IPB), dim3(256), 0, st,
-                       present, n, count, valid, list, counter);
+                       present, n, count, valid, list, counter, prio);
     return hipGetLastError();
 }
 
@@ -1417,10 +1422,10 @@ hipError_t rbc_launch_merkle(const MerkleArgs &a, bool check, hipStream_t st) {
 }
 
 hipError_t rbc_launch_digest(const uint8_t *leaves, uint64_t leaves_inst_pitch, int k, const int32_t *status,
-                             uint8_t *digests, int count, hipStream_t st) {
+                             uint8_t *digests, int count, hipStream_t st, int prio) {
     if (count <= 0) return hipSuccess;
     hipLaunchKernelGGL(digest_kernel, dim3((count + 63) / 64), dim3(64), 0, st, leaves, leaves_inst_pitch, k, status,
-                       digests, count);
+                       digests, count, prio);
     return hipGetLastError();
 }
 

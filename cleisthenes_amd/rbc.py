@@ -444,7 +444,7 @@ class Context:
                                       _dv(values_out), value_pitch, _dv(digests), _dv(status)),
               "rbc_dev_interpolate")
 
-    INTERP_DECODE, INTERP_REHASH, INTERP_CHECK = 1, 2, 4
+    INTERP_DECODE, INTERP_REHASH, INTERP_CHECK, INTERP_FORK = 1, 2, 4, 8
 
     def dev_interpolate_phases(self, stream, phases, count, shards, shard_pitch, shard_lens, uniform_len, valid,
                                leaves, leaves_verified, roots, values_out, value_pitch, digests, status):

@@ -179,6 +179,12 @@ int rbc_dev_interpolate(rbc_ctx *ctx, void *stream, int count, uint8_t *shards, 
 #define RBC_INTERP_DECODE 1
 #define RBC_INTERP_REHASH 2
 #define RBC_INTERP_CHECK 4
+/* RBC_INTERP_FORK (with DECODE): the value join runs on the context's aux
+ * stream beside the batch's REHASH, and the batch's CHECK call joins it back
+ * (values_out is complete when the CHECK work on `stream` is); no other
+ * DECODE may run on this context in between.  rbc_dev_interpolate forks the
+ * same way inside one call. */
+#define RBC_INTERP_FORK 8
 int rbc_dev_interpolate_phases(rbc_ctx *ctx, void *stream, int phases, int count, uint8_t *shards,
                                uint32_t shard_pitch, const uint32_t *shard_lens, uint32_t uniform_shard_len,
                                const uint8_t *valid, uint8_t *leaves, int leaves_verified, const uint8_t *roots,
