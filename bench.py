@@ -93,6 +93,8 @@ def parse_args(argv):
                          "phases together; 4: as 1 with verify(t-1) split by instances over both streams; "
                          "5: balanced two streams -- commit(t) then rehash+check(t-2) || verify+decode(t-1); "
                          "6: as 1, commit(t) starts when the receiver has DECODED t-2 (overlaps its rehash tail); "
+                         "7: as 1 with the receiver as rbc_dev_receive_step (verify(t-1) and the regen hashing of "
+                         "t-2 in one SHA launch); "
                          "0: one stream, stages in order")
     ap.add_argument("--sets", type=int, default=0,
                     help="shard buffer sets of the pipelined schedule (0: the minimum, 2 for --pipeline 1, "
@@ -289,7 +291,10 @@ def main(argv):
     if phased:
         set_bytes += I * (opitch + 32 + 4)  # per-set value / digest / status (decode and check run apart)
     pdec = args.pipeline == 6  # commit(t) starts when the receiver finished DECODING t-2
-    nsets = max(3 if (pipe3 or pdec) else 2, args.sets) if pipe else 1
+    rxs = args.pipeline == 7   # receiver = rbc_dev_receive_step (verify(t) + rehash(t-1) in one SHA launch)
+    nsets = max(3 if (pipe3 or pdec or rxs) else 2, args.sets) if pipe else 1
+    if rxs:
+        set_bytes += I * (n + n * 32 + opitch + 32 + 4) * 2 // 3  # per-parity receiver buffers
     # Wave issue priority (s_setprio) under the two-stream schedule: the
     # receiver stream (verify + interpolate, whose regen-hash tail is a
     # latency-bound dependent chain) at 2, the proposer at 0.  A/B on one box
@@ -318,6 +323,10 @@ def main(argv):
     d_digests = mb(I * 32)
     d_status = mb(I * 4)
     d_count = mb(16)
+    # --pipeline 7: a batch's receiver buffers live across two receive steps
+    rxb = [dict(valid=mb(I * n), leaves_r=mb(I * n * 32), out=mb(I * opitch), digests=mb(I * 32), status=mb(I * 4))
+           for _ in range(2)] if rxs else None
+    rx_pending = {}
     gather = (world > 1 or args.force_gather) and not args.rehearse_on_one_gpu
     slots = acs.max_share(total, world)
     d_gather = mb(world * slots * 64) if gather else None
@@ -500,6 +509,60 @@ def main(argv):
     # receiver stream's SHA work: P verifies the first half of t-1 (its own
     # context's workspace) then commits t; R verifies the second half, waits
     # for P's half and interpolates t-1.
+    def pstep_rx(t, ev=None):
+        """--pipeline 7: P commits t into set t % 3 once batch t-3 is complete;
+        R runs rbc_dev_receive_step(cur = t-1, prev = t-2): verify(t-1) and
+        the regen hashing of t-2 in one SHA launch, t-2's recheck + digest,
+        then t-1's decode; batch t-2 is complete when it returns."""
+        P, R = stream, rstream
+        recP = (lambda name: ev[name].record(P)) if ev is not None else (lambda name: None)
+        recR = (lambda name: ev[name].record(R)) if ev is not None else (lambda name: None)
+        sp = sets[t % nsets]
+        P.wait(evR[t % nsets])
+        recP("t0")
+        ctx.dev_encode(P.ptr, I, d_values, vpitch, None, B, sp["shards"], spitch)
+        recP("enc")
+        ctx.dev_leaves(P.ptr, I, sp["shards"], spitch, None, S, sp["leaves"])
+        recP("leaf")
+        ctx.dev_merkle_build(P.ptr, I, sp["leaves"], sp["roots"], sp["branches"])
+        recP("tree")
+        ctx.dev_inject_faults(P.ptr, I, sp["shards"], spitch, d_corrupt)
+        recP("fault")
+        evP[t % nsets].record(P)
+        if t == 0:
+            return
+        x = t - 1
+        sr, rb = sets[x % nsets], rxb[x % 2]
+        R.wait(evP[x % nsets])
+        recR("r0")
+        cur = ctx.rx_batch(I, sr["shards"], spitch, None, S, sr["branches"], sr["roots"], d_present, rb["valid"],
+                           rb["leaves_r"], rb["out"], opitch, rb["digests"], rb["status"])
+        prev = rx_pending.pop(x - 1, None)
+        ctx.dev_receive_step(R.ptr, cur, prev)
+        rx_pending[x] = cur
+        recR("verify")
+        recR("interp")
+        if gather and prev is not None:
+            pb = rxb[(x - 1) % 2]
+            ctx.dev_allgather_records(R.ptr, I, slots, sets[(x - 1) % nsets]["roots"], pb["digests"], pb["status"],
+                                      d_gather)
+        recR("gather")
+        if prev is not None:
+            evR[(x - 1) % nsets].record(R)
+
+    def rx_flush():
+        """complete the batch the last receive step decoded (outside the timed region)"""
+        if rxs and rx_pending:
+            x, cur = rx_pending.popitem()
+            ctx.dev_receive_step(rstream.ptr, None, cur)
+            if gather:  # the guard checks the gathered records of this batch
+                pb = rxb[x % 2]
+                ctx.dev_allgather_records(rstream.ptr, I, slots, sets[x % nsets]["roots"], pb["digests"],
+                                          pb["status"], d_gather)
+            rstream.sync()
+            return x
+        return None
+
     vsplit = args.pipeline == 4
     if vsplit:
         h1 = I // 2
@@ -707,9 +770,9 @@ def main(argv):
                   for a_, b_ in zip(stage_names[:-1], stage_names[1:])}
 
     if pipe:
-        args.warmup = max(args.warmup, 3 if pipe3 else 2)  # fill the pipeline: a decode before the guard
+        args.warmup = max(args.warmup, 3 if (pipe3 or rxs) else 2)  # fill the pipeline: a decode before the guard
         for t in range(args.warmup):
-            (pstep_bal if bal else pstep_phased if phased else pstep3 if pipe3 else pstep_split if vsplit
+            (pstep_rx if rxs else pstep_bal if bal else pstep_phased if phased else pstep3 if pipe3 else pstep_split if vsplit
              else pstep)(t)
     else:
         for _ in range(args.warmup):
@@ -721,7 +784,7 @@ def main(argv):
     t0 = time.perf_counter()
     if pipe:
         for t in range(args.warmup, args.warmup + args.steps):
-            (pstep_bal if bal else pstep_phased if phased else pstep3 if pipe3 else pstep_split if vsplit
+            (pstep_rx if rxs else pstep_bal if bal else pstep_phased if phased else pstep3 if pipe3 else pstep_split if vsplit
              else pstep)(t, ev_sets[t - args.warmup])
     else:
         for t in range(args.steps):
@@ -731,6 +794,9 @@ def main(argv):
     elapsed_max = rdz.max(elapsed)
     # the set the last decode read
     last = sets[(args.warmup + args.steps - (3 if pipe3 else 2)) % nsets] if pipe else sets[0]
+    x_last = rx_flush()
+    if rxs:
+        last = sets[x_last % nsets]
     if bal:
         pipe_spans = (("t0", "enc"), ("enc", "leaf"), ("leaf", "tree"), ("tree", "fault"), ("v0", "verify"),
                       ("verify", "decode"), ("g0", "regen"), ("regen", "check"), ("check", "gather"))
@@ -748,6 +814,8 @@ def main(argv):
 
     # ---- correctness of the timed run's last round (outside the timed region)
     res_out, res_status, res_dig = ((last["out"], last["status"], last["digests"]) if phased
+                                    else (rxb[x_last % 2]["out"], rxb[x_last % 2]["status"],
+                                          rxb[x_last % 2]["digests"]) if rxs
                                     else (d_out, d_status, d_digests))
     checks = check_results(args, ca, acs, synth, rdz, ctx, dev, stream, world, rank, first, I, total, slots, n, f,
                            k, B, S, vpitch, opitch, d_values, res_out, res_status, res_dig, last["roots"],
@@ -772,7 +840,7 @@ def main(argv):
     # PMC-measured HBM traffic per launch (tools/profile.sh + tools/pmc_summary.py
     # on this bench's default command), newest round first
     pm, pmc_path = {}, None
-    for cand in ("pmc_traffic_r02.json", "pmc_traffic_r01.json"):
+    for cand in ("pmc_traffic_r02s2.json", "pmc_traffic_r02.json", "pmc_traffic_r01.json"):
         pth = os.path.join(ROOT, "profiles", cand)
         if os.path.exists(pth):
             try:
@@ -919,6 +987,9 @@ def main(argv):
                                  "sets") if pipe3 else
                                 (f"verify(t-1) first half || second half, then commit(t) || interpolate(t-1), "
                                  f"two streams, {nsets} shard sets") if vsplit else
+                                (f"commit(t) || receive step: verify(t-1) + rehash(t-2) in one SHA launch, "
+                                 f"recheck(t-2), decode(t-1) (rbc_dev_receive_step), two streams, {nsets} shard "
+                                 "sets") if rxs else
                                 (f"commit(t) from decode(t-2) on || verify+interpolate(t-1) (decode, then "
                                  f"rehash+check), two streams, {nsets} shard sets") if pdec else
                                 (f"commit(t) || verify+interpolate(t-1) on two streams, {nsets} shard sets")

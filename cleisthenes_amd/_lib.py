@@ -28,6 +28,15 @@ i32p = POINTER(c_int32)
 szp = POINTER(c_size_t)
 u8pp = POINTER(u8p)
 
+
+class RxBatch(ctypes.Structure):
+    """rbc_rx_batch (include/rbc_gpu.h): one batch of rbc_dev_receive_step."""
+    _fields_ = [("count", c_int), ("shards", c_void_p), ("shard_pitch", c_uint32), ("shard_lens", c_void_p),
+                ("uniform_shard_len", c_uint32), ("branches", c_void_p), ("roots", c_void_p),
+                ("present", c_void_p), ("valid", c_void_p), ("leaves", c_void_p), ("values_out", c_void_p),
+                ("value_pitch", c_uint32), ("digests", c_void_p), ("status", c_void_p)]
+
+
 _SIGS = {
     "rbc_strerror": (c_char_p, [c_int]),
     "rbc_abi_version": (c_int, []),
@@ -68,6 +77,7 @@ _SIGS = {
                                c_void_p, c_void_p, c_void_p, c_void_p]),
     "rbc_dev_interpolate": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_uint32, c_void_p, c_uint32, c_void_p,
                                     c_void_p, c_int, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p]),
+    "rbc_dev_receive_step": (c_int, [c_void_p, c_void_p, POINTER(RxBatch), POINTER(RxBatch)]),
     "rbc_dev_interpolate_phases": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_uint32, c_void_p, c_uint32,
                                            c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_uint32, c_void_p,
                                            c_void_p]),

@@ -122,6 +122,7 @@ struct Ws {
     // the box has GPU_MAX_HW_QUEUES = 4 hardware queues per process)
     bool fork = true;
     bool join_pending = false;  // a forked join awaits its CHECK phase
+    int rx_count = 0;           // receive_step: batch decoded by the last call, awaiting its rehash + check
     hipStream_t aux = nullptr;  // created on first use
     hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_hashed = nullptr;
     bool init() {
@@ -746,6 +747,150 @@ int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *sha
     return RBC_OK;
 }
 
+// Pipelined receiver (rbc_dev_receive_step): cur's ECHO verify and prev's
+// regen hashing share one SHA launch; prev's recheck + digest follow, then
+// cur's decode.  The value join of cur runs on the aux stream and is waited
+// for by the next call (with prev's digest), so a batch is final when the
+// call that names it `prev` has run.
+int check_rx_batch(rbc_ctx *c, const rbc_rx_batch *b) {
+    if (b->count < 0) return RBC_ERR_INVALID_ARG;
+    if (b->count == 0) return RBC_OK;
+    if (!b->shards || !b->roots || !b->valid || !b->leaves || !b->values_out || !b->status ||
+        (c->depth > 0 && !b->branches))
+        return RBC_ERR_INVALID_ARG;
+    if (b->shard_pitch % kAlign || b->value_pitch % 16) return RBC_ERR_INVALID_ARG;
+    if (!b->shard_lens && (b->uniform_shard_len == 0 || b->uniform_shard_len > b->shard_pitch ||
+                           b->value_pitch < (uint64_t)b->uniform_shard_len * c->k))
+        return RBC_ERR_INVALID_ARG;
+    if ((uint64_t)c->n * b->shard_pitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
+    return RBC_OK;
+}
+
+int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, const rbc_rx_batch *prev) {
+    Ws &w = c->ws;
+    int rc;
+    if (cur && (rc = check_rx_batch(c, cur))) return rc;
+    if (prev && (rc = check_rx_batch(c, prev))) return rc;
+    const bool hc = cur && cur->count > 0, hp = prev && prev->count > 0;
+    // prev must be the batch whose decode the previous call left in the workspace
+    if (hp != (w.rx_count > 0) || (hp && prev->count != w.rx_count)) return RBC_ERR_INVALID_ARG;
+    if (!hc && !hp) return RBC_OK;
+    if (!aux_stream(w)) return RBC_ERR_DEVICE;
+    const int nr = c->n - c->k;
+    ShaArgs v{}, r{};
+    bool v_walk = false, v_path = false;
+    if (hc) {
+        v.count = cur->count;
+        v.rows_per_inst = c->n;
+        v.rows = cur->shards;
+        v.inst_pitch = (uint64_t)c->n * cur->shard_pitch;
+        v.row_pitch = cur->shard_pitch;
+        v.lens = cur->shard_lens;
+        v.uniform_len = cur->uniform_shard_len;
+        v.leaves = cur->leaves;
+        v.leaves_inst_pitch = (uint64_t)c->n * 32;
+        v.n = c->n;
+        v.depth = c->depth;
+        v.branches = cur->branches;
+        v.br_inst_pitch = (uint64_t)c->n * c->depth * 32;
+        v.roots = cur->roots;
+        v.present = cur->present;
+        v.valid = cur->valid;
+        v.prio = c->rxv_prio;
+        if (cur->present && c->n <= 256) {  // hash only the received shards (stage_verify)
+            RBC_HIP(w.vlist.ensure((size_t)cur->count * c->n * 4 + 64));
+            uint32_t *vl = w.vlist.as<uint32_t>(), *vc = vl + (size_t)cur->count * c->n;
+            RBC_HIP(hipMemsetAsync(vc, 0, 4, st));
+            RBC_HIP(rbc_launch_compact_present(cur->present, c->n, cur->count, cur->valid, vl, vc, st, c->rxv_prio));
+            v.list = vl;
+            v.list_count = vc;
+        }
+        // the shared-path verify where the branch walk is a real share (C4), as stage_verify
+        const uint32_t blocks_per_row = cur->shard_lens ? 0u : (cur->uniform_shard_len + 9 + 63) / 64;
+        v_path = (cur->shard_lens || 16u * (uint32_t)c->depth >= blocks_per_row) && c->depth >= 1 && c->width <= 256;
+        v_walk = !v_path;
+    }
+    if (hp && nr > 0) {
+        r.count = prev->count;
+        r.rows_per_inst = nr;
+        r.rows = prev->shards;
+        r.inst_pitch = (uint64_t)c->n * prev->shard_pitch;
+        r.row_pitch = prev->shard_pitch;
+        r.lens = prev->shard_lens;
+        r.uniform_len = prev->uniform_shard_len;
+        r.status = prev->status;
+        r.leaves = prev->leaves;
+        r.leaves_inst_pitch = (uint64_t)c->n * 32;
+        r.list = w.list.as<uint32_t>();
+        r.list_count = w.counter.as<uint32_t>();
+    }
+    RBC_HIP(rbc_launch_sha_rx(v, r, v_walk, st));
+    if (hc && v_path) {
+        PathArgs p{};
+        p.count = cur->count;
+        p.n = c->n;
+        p.width = c->width;
+        p.lg_width = c->depth;
+        p.depth = c->depth;
+        p.leaves = cur->leaves;
+        p.leaves_inst_pitch = (uint64_t)c->n * 32;
+        p.branches = cur->branches;
+        p.br_inst_pitch = (uint64_t)c->n * c->depth * 32;
+        p.roots = cur->roots;
+        p.present = cur->present;
+        p.valid = cur->valid;
+        p.prio = c->rxv_prio;
+        RBC_HIP(rbc_launch_merkle_path(p, st));
+    }
+    if (hp) {
+        if (prev->digests) {  // beside the recheck, on the aux stream (after prev's join)
+            RBC_HIP(hipEventRecord(w.ev_hashed, st));
+            RBC_HIP(hipStreamWaitEvent(w.aux, w.ev_hashed, 0));
+            RBC_HIP(rbc_launch_digest(prev->leaves, (uint64_t)c->n * 32, c->k, prev->status, prev->digests,
+                                      prev->count, w.aux, c->rx_prio));
+        }
+        RBC_HIP(hipEventRecord(w.ev_join, w.aux));  // prev's join (+ digest) done
+        MerkleArgs m{};
+        m.count = prev->count;
+        m.n = c->n;
+        m.width = c->width;
+        m.depth = c->depth;
+        m.k = c->k;
+        m.leaves = prev->leaves;
+        m.leaves_inst_pitch = (uint64_t)c->n * 32;
+        m.expect_roots = prev->roots;
+        m.status = prev->status;
+        m.prio = c->rx_prio;
+        RBC_HIP(rbc_launch_merkle(m, true, st));
+    }
+    w.rx_count = 0;
+    if (hc) {
+        rc = stage_regenerate(c, w, st, cur->count, cur->shards, cur->shard_pitch, cur->shard_lens,
+                              cur->uniform_shard_len, cur->valid, cur->status, 1);
+        if (rc) return rc;
+        RBC_HIP(hipEventRecord(w.ev_fork, st));
+        RBC_HIP(hipStreamWaitEvent(w.aux, w.ev_fork, 0));
+        JoinArgs j{};
+        j.count = cur->count;
+        j.k = c->k;
+        j.chunks = cur->value_pitch / 16;
+        j.shards = cur->shards;
+        j.inst_pitch = (uint64_t)c->n * cur->shard_pitch;
+        j.row_pitch = cur->shard_pitch;
+        j.inst_bytes = (uint32_t)((uint64_t)c->n * cur->shard_pitch);
+        j.lens = cur->shard_lens;
+        j.uniform_len = cur->uniform_shard_len;
+        j.values = cur->values_out;
+        j.value_pitch = cur->value_pitch;
+        j.status = cur->status;
+        j.prio = c->rx_prio;
+        RBC_HIP(rbc_launch_join(j, w.aux));
+        w.rx_count = cur->count;
+    }
+    if (hp) RBC_HIP(hipStreamWaitEvent(st, w.ev_join, 0));
+    return RBC_OK;
+}
+
 // klauspost checkShards / shardSize (reedsolomon.go)
 int check_shards(const size_t *lens, int n, bool nilok, size_t *size_out) {
     size_t size = 0;
@@ -1055,6 +1200,13 @@ int rbc_dev_interpolate(rbc_ctx *c, void *stream, int count, uint8_t *shards, ui
     return rbc_dev_interpolate_phases(c, stream, kPhaseAll, count, shards, shard_pitch, shard_lens,
                                       uniform_shard_len, valid, leaves, leaves_verified, roots, values_out,
                                       value_pitch, digests, status);
+}
+
+int rbc_dev_receive_step(rbc_ctx *c, void *stream, const rbc_rx_batch *cur, const rbc_rx_batch *prev) {
+    if (!c) return RBC_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);  // shared decode workspace
+    RBC_HIP(hipSetDevice(c->device));
+    return stage_receive_step(c, as_stream(stream), cur, prev);
 }
 
 int rbc_dev_interpolate_phases(rbc_ctx *c, void *stream, int phases, int count, uint8_t *shards,

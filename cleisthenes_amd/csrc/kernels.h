@@ -197,6 +197,9 @@ hipError_t rbc_launch_rs_fft(const FftArgs &a, hipStream_t st);
 int rbc_gf_pick_rc(int R, int rcmax);
 hipError_t rbc_launch_gf_rows(const GfArgs &a, hipStream_t st);
 hipError_t rbc_launch_sha_rows(const ShaArgs &a, bool verify, hipStream_t st);
+// receive step: v's rows (list or all; branch walk + verdict when v_walk) and
+// r's listed regen rows in one launch (count <= 0 disables a side)
+hipError_t rbc_launch_sha_rx(const ShaArgs &v, const ShaArgs &r, bool v_walk, hipStream_t st);
 hipError_t rbc_launch_merkle(const MerkleArgs &a, bool check, hipStream_t st);
 hipError_t rbc_launch_merkle_path(const PathArgs &a, hipStream_t st);
 hipError_t rbc_launch_decode_prepare(const PrepArgs &a, hipStream_t st);

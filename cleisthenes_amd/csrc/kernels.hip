@@ -372,6 +372,74 @@ __global__ __launch_bounds__(256) void sha_rows_kernel(ShaArgs a) {
     }
 }
 
+// Receive step (rbc_dev_receive_step): ONE launch hashes the received ECHO
+// shards of batch t (list v, or every row when v.list is null; with
+// v_walk the branch walk + verdict of sha_rows_kernel<true> follows) and the
+// rows interpolate regenerated for batch t-1 (list r).  Separately, batch
+// t-1's regen hashing is a latency-bound tail (42 rows x 1024 instances at
+// C2 = 672 waves of 373 serial compressions for 1,024 SIMDs) and the
+// verify 1,376 waves; together they are 2,048 waves, as full as the leaves.
+__global__ __launch_bounds__(256) void sha_rx_kernel(ShaArgs v, ShaArgs r, int v_walk) {
+    set_wave_prio(v.prio);
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int nv = v.count <= 0 ? 0 : (v.list ? (int)*v.list_count : v.count * v.rows_per_inst);
+    const bool isv = t < nv;
+    int inst, pos;
+    if (isv) {
+        if (v.list) {
+            const uint32_t e = v.list[t];
+            inst = (int)(e >> 8);
+            pos = (int)(e & 0xffu);
+        } else {
+            inst = t / v.rows_per_inst;
+            pos = t - inst * v.rows_per_inst;
+        }
+    } else {
+        t -= nv;
+        if (r.count <= 0 || t >= (int)*r.list_count) return;
+        const uint32_t e = r.list[t];
+        inst = (int)(e >> 8);
+        pos = (int)(e & 0xffu);
+        if (r.status && r.status[inst] != 0) return;
+    }
+    const uint8_t *rows = isv ? v.rows : r.rows;
+    const uint64_t inst_pitch = isv ? v.inst_pitch : r.inst_pitch;
+    const uint32_t row_pitch = isv ? v.row_pitch : r.row_pitch;
+    const uint32_t S = isv ? inst_len(v.lens, v.uniform_len, inst) : inst_len(r.lens, r.uniform_len, inst);
+    uint8_t *leaves = isv ? v.leaves : r.leaves;
+    const uint64_t lpitch = isv ? v.leaves_inst_pitch : r.leaves_inst_pitch;
+    Sha256State s;
+    sha256_row(rows + (size_t)inst * inst_pitch + (size_t)pos * row_pitch, S, s);
+    uint32_t h[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) h[q] = s.h[q];
+    if (leaves) store_digest(leaves + (size_t)inst * lpitch + 32u * pos, h);
+    if (isv && v_walk) {
+        const uint8_t *br = v.branches + (size_t)inst * v.br_inst_pitch + (size_t)pos * v.depth * 32u;
+        uint32_t tix = (uint32_t)pos;
+        for (int l = 0; l < v.depth; ++l, tix >>= 1) {
+            const bool empty = (l == 0) && ((pos ^ 1) >= v.n);
+            uint32_t sib[8], o[8];
+            if (empty) {
+                sha256_node32(h, o);
+            } else {
+                load_digest(br + 32u * l, sib);
+                if (tix & 1u) sha256_node64(sib, h, o);
+                else sha256_node64(h, sib, o);
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) h[q] = o[q];
+        }
+        uint32_t root[8];
+        load_digest(v.roots + (size_t)inst * 32u, root);
+        bool ok = true;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) ok = ok && (h[q] == root[q]);
+        const bool present = v.present ? v.present[(size_t)inst * v.n + pos] != 0 : true;
+        v.valid[(size_t)inst * v.n + pos] = (ok && present) ? 1 : 0;
+    }
+}
+
 // Two rows per lane (rows 2t, 2t+1 of one instance, so one length), the
 // compressions interleaved: the per-wave dependent chain halves its stalls
 // (profiles/r01_sha_probe.txt: 6,071 SIMD clk per row-compression at one
@@ -1381,6 +1449,16 @@ hipError_t rbc_launch_sha_rows(const ShaArgs &a, bool verify, hipStream_t st) {
     dim3 grid((unsigned)((total + 255) / 256));
     if (verify) hipLaunchKernelGGL(sha_rows_kernel<true>, grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(sha_rows_kernel<false>, grid, dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t rbc_launch_sha_rx(const ShaArgs &v, const ShaArgs &r, bool v_walk, hipStream_t st) {
+    const long total = (v.count > 0 ? (long)v.count * v.rows_per_inst : 0) +
+                       (r.count > 0 ? (long)r.count * r.rows_per_inst : 0);
+    if (total <= 0) return hipSuccess;
+    if ((v.count > 0 && (!v.rows || (v_walk && (!v.valid || !v.roots)))) || (r.count > 0 && (!r.list || !r.list_count)))
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(sha_rx_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, v, r, v_walk ? 1 : 0);
     return hipGetLastError();
 }
 

@@ -453,6 +453,22 @@ class Context:
                                              int(leaves_verified), _dv(roots), _dv(values_out), value_pitch,
                                              _dv(digests), _dv(status)), "rbc_dev_interpolate_phases")
 
+    @staticmethod
+    def rx_batch(count, shards, shard_pitch, shard_lens, uniform_len, branches, roots, present, valid, leaves,
+                 values_out, value_pitch, digests, status) -> "_lib.RxBatch":
+        """An rbc_rx_batch of device buffers (DeviceBuffer / int / None)."""
+        def v(x):
+            p = _dv(x)
+            return p.value if isinstance(p, c_void_p) else p
+        return _lib.RxBatch(count, v(shards), shard_pitch, v(shard_lens), uniform_len, v(branches), v(roots),
+                            v(present), v(valid), v(leaves), v(values_out), value_pitch, v(digests), v(status))
+
+    def dev_receive_step(self, stream, cur=None, prev=None) -> None:
+        """Pipelined receiver: verify(cur) + rehash(prev) in one SHA launch,
+        prev's recheck + digest, cur's decode (rbc_dev_receive_step)."""
+        check(lib.rbc_dev_receive_step(self._p, _dv(stream), ctypes.byref(cur) if cur is not None else None,
+                                       ctypes.byref(prev) if prev is not None else None), "rbc_dev_receive_step")
+
     def dev_marshal_val(self, stream, count, msg_type, shards, shard_pitch, shard_lens, uniform_len, branches,
                         roots, out, out_pitch, out_lens):
         """Per-recipient VAL / ECHO pb.Message bytes in HBM (include/rbc_protocol.h)."""

@@ -189,6 +189,39 @@ int rbc_dev_interpolate_phases(rbc_ctx *ctx, void *stream, int phases, int count
                                uint32_t shard_pitch, const uint32_t *shard_lens, uint32_t uniform_shard_len,
                                const uint8_t *valid, uint8_t *leaves, int leaves_verified, const uint8_t *roots,
                                uint8_t *values_out, uint32_t value_pitch, uint8_t *digests, int32_t *status);
+/* Pipelined receiver, one call per batch:
+ * rbc_dev_receive_step(ctx, stream, cur, prev) hashes the received ECHO
+ * shards of `cur` (validateMessage, rbc/rbc.go:92-95) AND the rows
+ * interpolate regenerated for `prev` in ONE SHA launch, then runs prev's
+ * Merkle root recheck + batch digest, then cur's decode (first-k-valid
+ * prepare, missing-data GF, FFT re-encode + compare; the value join on the
+ * context's aux stream).  Alone, prev's regen hashing is a latency-bound tail
+ * (few long serial chains); beside cur's verify it fills the SIMDs.
+ * `prev` must be the `cur` of the previous call on this context (NULL on the
+ * first call); a last call with cur = NULL completes the final batch.  When a
+ * call's work on `stream` is done, prev's valid / leaves / status /
+ * values_out / digests are final and equal rbc_dev_verify followed by
+ * rbc_dev_interpolate(leaves_verified = 1) on the same inputs (interpolate,
+ * rbc/rbc.go:86-90); cur's buffers must stay untouched until the next call's
+ * work is done.  All pointers are device memory; present may be NULL (all
+ * received). */
+typedef struct rbc_rx_batch {
+    int count;
+    uint8_t *shards;             /* [count][n][shard_pitch], regenerated in place */
+    uint32_t shard_pitch;
+    const uint32_t *shard_lens;  /* S_i, or NULL: uniform_shard_len */
+    uint32_t uniform_shard_len;
+    const uint8_t *branches;     /* [count][n][d][32] */
+    const uint8_t *roots;        /* [count][32] */
+    const uint8_t *present;      /* [count][n] received ECHOs (nullable) */
+    uint8_t *valid;              /* [count][n] out */
+    uint8_t *leaves;             /* [count][n][32] out (own buffer per batch in flight) */
+    uint8_t *values_out;         /* [count][value_pitch] out */
+    uint32_t value_pitch;
+    uint8_t *digests;            /* [count][32] out (nullable) */
+    int32_t *status;             /* [count] out */
+} rbc_rx_batch;
+int rbc_dev_receive_step(rbc_ctx *ctx, void *stream, const rbc_rx_batch *cur, const rbc_rx_batch *prev);
 /* Synthetic Byzantine input for tests/bench: shards[i][corrupt[i]][0] ^= 0x5a
  * for every i with corrupt[i] >= 0 (corrupt: device int32[count]). */
 int rbc_dev_inject_faults(rbc_ctx *ctx, void *stream, int count, uint8_t *shards, uint32_t shard_pitch,

@@ -1157,6 +1157,78 @@ def test_merkle_build_branches_every_depth(gpu, ref, n, f):
         assert np.array_equal(brs[i], want_br), (n, i)
 
 
+@pytest.mark.parametrize("n,f,B,I,all_present", [(128, 42, 1 << 16, 96, False), (16, 5, 3001, 64, False),
+                                                  (256, 85, 86 * 40, 48, False), (64, 21, 22 * 700, 40, True),
+                                                  (7, 2, 1000, 33, False)])
+def test_receive_step_pipeline_equals_verify_then_interpolate(gpu, ref, n, f, B, I, all_present):
+    """rbc_dev_receive_step over three batches (verify(t) + rehash(t-1) in
+    one SHA launch, recheck(t-1), decode(t), join on the aux stream, a final
+    flush) yields exactly rbc_dev_verify + rbc_dev_interpolate(leaves_verified
+    = 1) per batch: valid masks, statuses, values, digests and leaves, with
+    corrupted ECHO shards, wrong committed roots and (all_present) no present
+    mask; the C4 shape takes the shared-path verify inside the step.  Sampled
+    instances are also checked against the C oracle."""
+    nb = 3
+    want, got = [], []
+    for mode in ("oneshot", "step"):
+        pls = []
+        for bi in range(nb):
+            pl = Pipeline(gpu, n, f, B, I, seed=1000 * n + 17 * bi + B, corrupt_frac=0.3)
+            b, c = pl.b, pl.ctx
+            c.dev_encode(None, I, b["values"], pl.vpitch, None, B, b["shards"], pl.spitch)
+            # a Byzantine proposer commits to a non-codeword every 7th instance
+            # (last row altered before the Merkle build: every branch verifies,
+            # interpolate's full re-encode must reject it)
+            byz = np.full(I, -1, np.int32)
+            byz[bi::7] = n - 1
+            d_byz = gpu.DeviceBuffer(I * 4)
+            d_byz.upload(byz)
+            c.dev_inject_faults(None, I, b["shards"], pl.spitch, d_byz)
+            c.dev_leaves(None, I, b["shards"], pl.spitch, None, pl.S, b["leaves"])
+            c.dev_merkle_build(None, I, b["leaves"], b["roots"], b["branches"])
+            c.dev_inject_faults(None, I, b["shards"], pl.spitch, b["corrupt"])
+            pls.append(pl)
+        present = (lambda pl: None) if all_present else (lambda pl: pl.b["present"])
+        if mode == "oneshot":
+            for pl in pls:
+                b, c = pl.b, pl.ctx
+                c.dev_verify(None, I, b["shards"], pl.spitch, None, pl.S, b["branches"], b["roots"], present(pl),
+                             b["valid"], b["leaves_r"])
+                c.dev_interpolate(None, I, b["shards"], pl.spitch, None, pl.S, b["valid"], b["leaves_r"], 1,
+                                  b["roots"], b["out"], pl.opitch, b["digests"], b["status"])
+        else:
+            rx = gpu.Context(n, f)
+            st = gpu.Stream(0)
+            bs = [rx.rx_batch(I, pl.b["shards"], pl.spitch, None, pl.S, pl.b["branches"], pl.b["roots"],
+                              present(pl), pl.b["valid"], pl.b["leaves_r"], pl.b["out"], pl.opitch,
+                              pl.b["digests"], pl.b["status"]) for pl in pls]
+            prev = None
+            for cur in bs + [None]:
+                rx.dev_receive_step(st.ptr, cur, prev)
+                prev = cur
+            with pytest.raises(gpu.RBCError):  # prev must be the last call's cur
+                rx.dev_receive_step(st.ptr, None, bs[0])
+            st.sync()
+        gpu.rbc.lib.rbc_device_sync(0)
+        res = []
+        for pl in pls:
+            stt = pl.arr("status", np.int32)
+            ok = stt == 0
+            res.append((stt, pl.arr("valid", shape=(I, n)), pl.arr("out", shape=(I, pl.opitch))[:, : pl.k * pl.S][ok],
+                        pl.arr("digests", shape=(I, 32))[ok], pl.arr("leaves_r", shape=(I, n, 32))[ok], pl))
+        (want if mode == "oneshot" else got).append(res)
+    for bi in range(nb):
+        (s0, v0, o0, d0, l0, _), (s1, v1, o1, d1, l1, pl) = want[0][bi], got[0][bi]
+        assert np.array_equal(s0, s1), bi
+        assert set(s1[bi::7]) == {-8} and (s1[np.arange(I) % 7 != bi] == 0).all(), bi
+        pr = np.ones((I, n), bool) if all_present else pl.present.astype(bool)
+        assert np.array_equal(v0[pr], v1[pr]) and not v1[~pr].any(), bi
+        assert np.array_equal(o0, o1) and np.array_equal(d0, d1) and np.array_equal(l0, l1), bi
+        ok = np.flatnonzero(s1 == 0)
+        for i in (ok[0], ok[-1]):
+            assert bytes(pl.values[i, :B]) == bytes(o1[np.searchsorted(ok, i)][:B])
+
+
 @pytest.mark.parametrize("n,f,B,I", [(128, 42, 1 << 16, 96), (16, 5, 3001, 64), (256, 85, 86 * 40, 48)])
 def test_interpolate_phases_equal_one_shot(gpu, ref, n, f, B, I):
     """rbc_dev_interpolate_phases (decode, rehash, check as three calls,
