@@ -1458,7 +1458,14 @@ hipError_t rbc_launch_sha_rx(const ShaArgs &v, const ShaArgs &r, bool v_walk, hi
     if (total <= 0) return hipSuccess;
     if ((v.count > 0 && (!v.rows || (v_walk && (!v.valid || !v.roots)))) || (r.count > 0 && (!r.list || !r.list_count)))
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(sha_rx_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, v, r, v_walk ? 1 : 0);
+    // one-wave blocks: 4.78-4.82 ms per C2 receive step against 5.03 with
+    // 256-thread blocks (tools/gpu_r02tpb.sh); RBC_RX_TPB overrides
+    static const int tpb = [] {
+        const char *e = getenv("RBC_RX_TPB");
+        const int x = e ? atoi(e) : 64;
+        return (x == 128 || x == 256) ? x : 64;
+    }();
+    hipLaunchKernelGGL(sha_rx_kernel, dim3((unsigned)((total + tpb - 1) / tpb)), dim3(tpb), 0, st, v, r, v_walk ? 1 : 0);
     return hipGetLastError();
 }
 
