@@ -85,16 +85,16 @@ def parse_args(argv):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-configs", default="c1,c2,c3,c4",
                     help="configs the CPU port is also timed on (the bench config always is)")
-    ap.add_argument("--pipeline", type=int, default=1,
-                    help="1 (default): overlap batch t's commit (proposer stream) with batch t-1's verify + "
+    ap.add_argument("--pipeline", type=int, default=7,
+                    help="7 (default): as 1 with the receiver as rbc_dev_receive_step -- verify(t-1) and the "
+                         "regen hashing of t-2 in one SHA launch; 1: overlap batch t's commit (proposer stream) with batch t-1's verify + "
                          "interpolate (receiver stream); 2: three streams -- commit(t) || verify(t-1) || "
                          "interpolate(t-2); 3: phase-aligned -- every step runs the SHA phases of three batches "
                          "together (leaves(t) || verify(t-1) || regen hashing(t-2)), then their GF/FFT/tree "
                          "phases together; 4: as 1 with verify(t-1) split by instances over both streams; "
                          "5: balanced two streams -- commit(t) then rehash+check(t-2) || verify+decode(t-1); "
                          "6: as 1, commit(t) starts when the receiver has DECODED t-2 (overlaps its rehash tail); "
-                         "7: as 1 with the receiver as rbc_dev_receive_step (verify(t-1) and the regen hashing of "
-                         "t-2 in one SHA launch); "
+
                          "0: one stream, stages in order")
     ap.add_argument("--sets", type=int, default=0,
                     help="shard buffer sets of the pipelined schedule (0: the minimum, 2 for --pipeline 1, "
@@ -306,7 +306,7 @@ def main(argv):
     budget = float(os.environ.get("RBC_BENCH_HBM_BUDGET", 250e9))
     while pipe and nsets * set_bytes + other_bytes > budget:
         nsets -= 1
-        if nsets < (3 if pipe3 else 2):
+        if nsets < (3 if (pipe3 or rxs or pdec) else 2):
             pipe, pipe3, nsets = False, False, 1
     sets = [dict(shards=mb(I * n * spitch), leaves=mb(I * n * 32), roots=mb(I * 32),
                  branches=mb(I * n * max(d, 1) * 32),
@@ -538,9 +538,10 @@ def main(argv):
         cur = ctx.rx_batch(I, sr["shards"], spitch, None, S, sr["branches"], sr["roots"], d_present, rb["valid"],
                            rb["leaves_r"], rb["out"], opitch, rb["digests"], rb["status"])
         prev = rx_pending.pop(x - 1, None)
-        ctx.dev_receive_step(R.ptr, cur, prev)
+        # "verify" = the step's hashing launch (verify(t-1) + regen hashing of t-2),
+        # "interp" = the rest (recheck(t-2), decode(t-1))
+        ctx.dev_receive_step(R.ptr, cur, prev, ev["verify"] if ev is not None else None)
         rx_pending[x] = cur
-        recR("verify")
         recR("interp")
         if gather and prev is not None:
             pb = rxb[(x - 1) % 2]
@@ -773,7 +774,7 @@ def main(argv):
     # over two committed sets (ECHO verify of batch t and the regen hashing of
     # t-1 in one SHA launch; BASELINE configs[2]'s stages), re-corrupting the
     # same ECHO shards before every pass (interpolate repaired them in place)
-    rx_step_ms = None
+    rx_step_ms = rx_sha_iso_ms = None
     if pipe and not phased and not args.no_isolated and nsets >= 2:
         rbuf = rxb or [dict(valid=mb(I * n), leaves_r=mb(I * n * 32), out=mb(I * opitch), digests=mb(I * 32),
                             status=mb(I * 4)) for _ in range(2)]
@@ -784,6 +785,7 @@ def main(argv):
         stream.sync()
         R, K_rx, pend = rstream, 8, None
         e_rx = [ca.Event(), ca.Event()]
+        e_sha = [(ca.Event(), ca.Event()) for _ in range(K_rx)]
         for t in range(K_rx + 2):
             sr, rb = sets[t % 2], rbuf[t % 2]
             ctx.dev_inject_faults(R.ptr, I, sr["shards"], spitch, d_corrupt)
@@ -791,7 +793,9 @@ def main(argv):
                 e_rx[0].record(R)
             cur = ctx.rx_batch(I, sr["shards"], spitch, None, S, sr["branches"], sr["roots"], d_present, rb["valid"],
                                rb["leaves_r"], rb["out"], opitch, rb["digests"], rb["status"])
-            ctx.dev_receive_step(R.ptr, cur, pend)
+            if t >= 2:
+                e_sha[t - 2][0].record(R)
+            ctx.dev_receive_step(R.ptr, cur, pend, e_sha[t - 2][1] if t >= 2 else None)
             pend = cur
         e_rx[1].record(R)
         ctx.dev_receive_step(R.ptr, None, pend)
@@ -800,6 +804,7 @@ def main(argv):
         if ok_rx != I:
             raise SystemExit(f"bench: receive_step pass decoded {ok_rx} of {I} instances")
         rx_step_ms = e_rx[0].elapsed_ms(e_rx[1]) / K_rx
+        rx_sha_iso_ms = sum(a_.elapsed_ms(b_) for a_, b_ in e_sha) / K_rx
 
     if pipe:
         args.warmup = max(args.warmup, 3 if (pipe3 or rxs) else 2)  # fill the pipeline: a decode before the guard
@@ -869,10 +874,16 @@ def main(argv):
         "sha_rows_kernel<verify>": (stage_ms["verify"], R_rows * (S + d * 32 + 32) + I * (32 + 2 * n),
                                     R_rows * (blocks_per_shard + 2 * d)),
     }
+    regen_rows = int(I * n - present_h.sum() + (corrupt_h >= 0).sum())
+    if rxs:  # --pipeline 7: ECHO verify of t and the regen hashing of t-1 are one launch
+        del kern["sha_rows_kernel<verify>"]
+        kern["sha_rx_kernel<verify+regen>"] = (
+            stage_ms["verify"], R_rows * (S + d * 32 + 32) + I * (32 + 2 * n) + regen_rows * (S + 32),
+            R_rows * (blocks_per_shard + 2 * d) + regen_rows * blocks_per_shard)
     # PMC-measured HBM traffic per launch (tools/profile.sh + tools/pmc_summary.py
     # on this bench's default command), newest round first
     pm, pmc_path = {}, None
-    for cand in ("pmc_traffic_r02s3.json", "pmc_traffic_r02.json", "pmc_traffic_r01.json"):
+    for cand in ("pmc_traffic_r02s4.json", "pmc_traffic_r02s3.json", "pmc_traffic_r02.json", "pmc_traffic_r01.json"):
         pth = os.path.join(ROOT, "profiles", cand)
         if os.path.exists(pth):
             try:
@@ -915,7 +926,6 @@ def main(argv):
     # chip-level SHA-256 rate of the whole step (all three hashing kernels,
     # both streams): under the pipelined schedule a kernel's own span also
     # holds the other stream's work, so this is the utilisation figure
-    regen_rows = int(I * n - present_h.sum() + (corrupt_h >= 0).sum())
     step_comp = I * n * blocks_per_shard + R_rows * (blocks_per_shard + 2 * d) + regen_rows * blocks_per_shard
     step_cps = step_comp / (elapsed_max / args.steps)  # per GPU
     sha_chip = {"compressions_per_step": int(step_comp), "achieved": round(step_cps / 1e9, 2),
@@ -928,9 +938,13 @@ def main(argv):
     roof = roofline(dom)
     codec_roof = roofline(enc_kernel)  # north_star: encode against the HBM peak
     if iso_ms is not None:
-        stage_of = {enc_kernel: "enc", "sha_rows_kernel<leaves>": "leaf", "sha_rows_kernel<verify>": "verify"}
+        stage_of = {enc_kernel: "enc", "sha_rows_kernel<leaves>": "leaf", "sha_rows_kernel<verify>": "verify",
+                    "sha_rx_kernel<verify+regen>": "rx_sha"}
+        iso_all = dict(iso_ms, rx_sha=rx_sha_iso_ms)
         for r in (roof, codec_roof):
-            ms_i = iso_ms[stage_of[r["kernel"]]]
+            ms_i = iso_all[stage_of[r["kernel"]]]
+            if not ms_i:
+                continue
             _, nbytes, ncomp = kern[r["kernel"]]
             iso = {"avg_ms": round(ms_i, 4), "achieved": round(nbytes / (ms_i / 1e3) / 1e9, 1),
                    "frac": round(nbytes / (ms_i / 1e3) / 1e9 / HBM_PEAK_GBS, 4),

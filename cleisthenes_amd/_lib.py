@@ -11,7 +11,8 @@ import re
 from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librbc_gpu.so")
+# RBC_GPU_LIB_AB: an alternative build of the same library for A/B runs (tools/build_ab.sh)
+LIB_PATH = os.environ.get("RBC_GPU_LIB_AB") or os.path.join(_HERE, "librbc_gpu.so")
 INCLUDE_DIR = os.path.join(os.path.dirname(_HERE), "include")
 HEADER_PATH = os.path.join(INCLUDE_DIR, "rbc_gpu.h")
 
@@ -77,7 +78,7 @@ _SIGS = {
                                c_void_p, c_void_p, c_void_p, c_void_p]),
     "rbc_dev_interpolate": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_uint32, c_void_p, c_uint32, c_void_p,
                                     c_void_p, c_int, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p]),
-    "rbc_dev_receive_step": (c_int, [c_void_p, c_void_p, POINTER(RxBatch), POINTER(RxBatch)]),
+    "rbc_dev_receive_step": (c_int, [c_void_p, c_void_p, POINTER(RxBatch), POINTER(RxBatch), c_void_p]),
     "rbc_dev_interpolate_phases": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_uint32, c_void_p, c_uint32,
                                            c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_uint32, c_void_p,
                                            c_void_p]),

@@ -766,7 +766,8 @@ int check_rx_batch(rbc_ctx *c, const rbc_rx_batch *b) {
     return RBC_OK;
 }
 
-int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, const rbc_rx_batch *prev) {
+int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, const rbc_rx_batch *prev,
+                       hipEvent_t ev_sha) {
     Ws &w = c->ws;
     int rc;
     if (cur && (rc = check_rx_batch(c, cur))) return rc;
@@ -842,6 +843,7 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
         p.prio = c->rxv_prio;
         RBC_HIP(rbc_launch_merkle_path(p, st));
     }
+    if (ev_sha) RBC_HIP(hipEventRecord(ev_sha, st));
     if (hp) {
         if (prev->digests) {  // beside the recheck, on the aux stream (after prev's join)
             RBC_HIP(hipEventRecord(w.ev_hashed, st));
@@ -1202,11 +1204,12 @@ int rbc_dev_interpolate(rbc_ctx *c, void *stream, int count, uint8_t *shards, ui
                                       value_pitch, digests, status);
 }
 
-int rbc_dev_receive_step(rbc_ctx *c, void *stream, const rbc_rx_batch *cur, const rbc_rx_batch *prev) {
+int rbc_dev_receive_step(rbc_ctx *c, void *stream, const rbc_rx_batch *cur, const rbc_rx_batch *prev,
+                         void *hashed_event) {
     if (!c) return RBC_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(c->mu);  // shared decode workspace
     RBC_HIP(hipSetDevice(c->device));
-    return stage_receive_step(c, as_stream(stream), cur, prev);
+    return stage_receive_step(c, as_stream(stream), cur, prev, reinterpret_cast<hipEvent_t>(hashed_event));
 }
 
 int rbc_dev_interpolate_phases(rbc_ctx *c, void *stream, int phases, int count, uint8_t *shards,

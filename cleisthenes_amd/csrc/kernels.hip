@@ -314,7 +314,17 @@ __global__ __launch_bounds__(64) void gf_short_kernel(GfArgs a) {
 // rbc/rbc.go:92-95) and writes valid = present && (root' == root).
 // ============================================================================
 template <bool VERIFY>
-__global__ __launch_bounds__(256) void sha_rows_kernel(ShaArgs a) {
+// Occupancy of the SHA kernels: under the two-stream schedule both streams'
+// SHA launches (2,048 waves each at C2) must be resident together, 4 waves
+// per SIMD, so every kernel that hashes rows is held to <= 128 VGPRs
+// (the verify walk then spills 36 B per lane, outside the block loop)
+#ifndef RBC_SHA_WPE
+#define RBC_SHA_WPE 4
+#endif
+#ifndef RBC_RX_WPE
+#define RBC_RX_WPE 4
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RBC_SHA_WPE))) void sha_rows_kernel(ShaArgs a) {
     set_wave_prio(a.prio);
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     int inst, pos;
@@ -379,7 +389,7 @@ __global__ __launch_bounds__(256) void sha_rows_kernel(ShaArgs a) {
 // t-1's regen hashing is a latency-bound tail (42 rows x 1024 instances at
 // C2 = 672 waves of 373 serial compressions for 1,024 SIMDs) and the
 // verify 1,376 waves; together they are 2,048 waves, as full as the leaves.
-__global__ __launch_bounds__(256) void sha_rx_kernel(ShaArgs v, ShaArgs r, int v_walk) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RBC_RX_WPE))) void sha_rx_kernel(ShaArgs v, ShaArgs r, int v_walk) {
     set_wave_prio(v.prio);
     int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int nv = v.count <= 0 ? 0 : (v.list ? (int)*v.list_count : v.count * v.rows_per_inst);
@@ -1446,6 +1456,10 @@ hipError_t rbc_launch_sha_rows(const ShaArgs &a, bool verify, hipStream_t st) {
         else hipLaunchKernelGGL(sha_rows2_kernel<false>, g2, dim3(tpb2), 0, st, a);
         return hipGetLastError();
     }
+    // 256-thread blocks: the per-SIMD SHA rate hardly grows past one wave, so
+    // the kernel's time is set by the SIMD that holds the most waves, and
+    // 4-wave blocks spread them evenly (C2 leaves alone: 2.07 ms; one-wave
+    // blocks 2.97, 128-thread 3.05; tools/gpu_r02shatpb.sh)
     dim3 grid((unsigned)((total + 255) / 256));
     if (verify) hipLaunchKernelGGL(sha_rows_kernel<true>, grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(sha_rows_kernel<false>, grid, dim3(256), 0, st, a);

@@ -463,11 +463,14 @@ class Context:
         return _lib.RxBatch(count, v(shards), shard_pitch, v(shard_lens), uniform_len, v(branches), v(roots),
                             v(present), v(valid), v(leaves), v(values_out), value_pitch, v(digests), v(status))
 
-    def dev_receive_step(self, stream, cur=None, prev=None) -> None:
+    def dev_receive_step(self, stream, cur=None, prev=None, hashed_event=None) -> None:
         """Pipelined receiver: verify(cur) + rehash(prev) in one SHA launch,
-        prev's recheck + digest, cur's decode (rbc_dev_receive_step)."""
+        prev's recheck + digest, cur's decode (rbc_dev_receive_step);
+        hashed_event (an Event) is recorded right after the hashing launch."""
         check(lib.rbc_dev_receive_step(self._p, _dv(stream), ctypes.byref(cur) if cur is not None else None,
-                                       ctypes.byref(prev) if prev is not None else None), "rbc_dev_receive_step")
+                                       ctypes.byref(prev) if prev is not None else None,
+                                       hashed_event.ptr if hashed_event is not None else None),
+              "rbc_dev_receive_step")
 
     def dev_marshal_val(self, stream, count, msg_type, shards, shard_pitch, shard_lens, uniform_len, branches,
                         roots, out, out_pitch, out_lens):

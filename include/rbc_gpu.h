@@ -221,7 +221,10 @@ typedef struct rbc_rx_batch {
     uint8_t *digests;            /* [count][32] out (nullable) */
     int32_t *status;             /* [count] out */
 } rbc_rx_batch;
-int rbc_dev_receive_step(rbc_ctx *ctx, void *stream, const rbc_rx_batch *cur, const rbc_rx_batch *prev);
+/* hashed_event (nullable, rbc_event_create): recorded on `stream` right after
+ * the hashing launch (and cur's shared-path walk), so a caller can time it. */
+int rbc_dev_receive_step(rbc_ctx *ctx, void *stream, const rbc_rx_batch *cur, const rbc_rx_batch *prev,
+                         void *hashed_event);
 /* Synthetic Byzantine input for tests/bench: shards[i][corrupt[i]][0] ^= 0x5a
  * for every i with corrupt[i] >= 0 (corrupt: device int32[count]). */
 int rbc_dev_inject_faults(rbc_ctx *ctx, void *stream, int count, uint8_t *shards, uint32_t shard_pitch,

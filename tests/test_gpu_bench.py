@@ -1,6 +1,7 @@
 """bench.py end to end on the GPU at a small batch: every schedule
-(--pipeline 0 serial, 1 two-stream default, 2 three-stream, 3 phase-aligned,
-4 split verify, 5 balanced) must pass the bench's own correctness guard (all instances decode, every
+(--pipeline 0 serial, 1 two-stream, 2 three-stream, 3 phase-aligned,
+4 split verify, 5 balanced, 6 commit from the receiver's decode, 7 two-stream with
+rbc_dev_receive_step, the default) must pass the bench's own correctness guard (all instances decode, every
 decoded value equals its input, sampled roots / digests equal the C oracle;
 the bench exits 3 otherwise) and print exactly one JSON line with the
 contract keys."""
@@ -15,7 +16,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("pipeline", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("pipeline", [0, 1, 2, 3, 4, 5, 6, 7])
 def test_bench_schedules_pass_their_guard(pipeline):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "3", "--instances", "96",
            "--pipeline", str(pipeline), "--no-cpu-baseline", "--no-pcie", "--oracle-samples", "4"]

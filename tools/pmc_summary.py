@@ -69,7 +69,11 @@ def main():
     # SHA-256 compressions per launch: leaves hash all N rows, ECHO verify the
     # N-f received rows (+2 per branch level)
     comp = {"sha_rows_kernel<leaves>": a.instances * n * blocks(S),
-            "sha_rows_kernel<verify>": a.instances * (n - f) * (blocks(S) + 2 * d)}
+            "sha_rows_kernel<verify>": a.instances * (n - f) * (blocks(S) + 2 * d),
+            # receive step: the received rows of t + the regenerated rows of t-1
+            # (the f absent rows, plus the bench's one corrupted ECHO in 10 % of instances)
+            "sha_rx_kernel<verify+regen>": a.instances * (n - f) * (blocks(S) + 2 * d)
+            + (a.instances * f + a.instances // 10) * blocks(S)}
     rows = {}
     for rl in sorted(set(pm) | set(tr)):
         c = pm.get(rl, {})

@@ -36,6 +36,8 @@ def role(name, grid, n, k, inst):
         if grid == inst * (n - k):
             return "sha_rows_kernel<regen>"
         return f"sha_rows_kernel<false>[grid {grid}]"
+    if b == "sha_rx_kernel":  # rbc_dev_receive_step: ECHO verify of t + regen hashing of t-1
+        return "sha_rx_kernel<verify+regen>"
     if b == "sha_rows_kernel<true>":
         return "sha_rows_kernel<verify>"
     return b
