@@ -770,41 +770,11 @@ def main(argv):
         iso_ms = {b_: sum(ev[a_].elapsed_ms(ev[b_]) for ev in iso_ev) / len(iso_ev)
                   for a_, b_ in zip(stage_names[:-1], stage_names[1:])}
 
-    # the receiver alone as a streaming node runs it: rbc_dev_receive_step
-    # over two committed sets (ECHO verify of batch t and the regen hashing of
-    # t-1 in one SHA launch; BASELINE configs[2]'s stages), re-corrupting the
-    # same ECHO shards before every pass (interpolate repaired them in place)
-    rx_step_ms = rx_sha_iso_ms = None
-    if pipe and not phased and not args.no_isolated and nsets >= 2:
-        rbuf = rxb or [dict(valid=mb(I * n), leaves_r=mb(I * n * 32), out=mb(I * opitch), digests=mb(I * 32),
-                            status=mb(I * 4)) for _ in range(2)]
-        for j in range(2):
-            ctx.dev_encode(stream.ptr, I, d_values, vpitch, None, B, sets[j]["shards"], spitch)
-            ctx.dev_leaves(stream.ptr, I, sets[j]["shards"], spitch, None, S, sets[j]["leaves"])
-            ctx.dev_merkle_build(stream.ptr, I, sets[j]["leaves"], sets[j]["roots"], sets[j]["branches"])
-        stream.sync()
-        R, K_rx, pend = rstream, 8, None
-        e_rx = [ca.Event(), ca.Event()]
-        e_sha = [(ca.Event(), ca.Event()) for _ in range(K_rx)]
-        for t in range(K_rx + 2):
-            sr, rb = sets[t % 2], rbuf[t % 2]
-            ctx.dev_inject_faults(R.ptr, I, sr["shards"], spitch, d_corrupt)
-            if t == 2:
-                e_rx[0].record(R)
-            cur = ctx.rx_batch(I, sr["shards"], spitch, None, S, sr["branches"], sr["roots"], d_present, rb["valid"],
-                               rb["leaves_r"], rb["out"], opitch, rb["digests"], rb["status"])
-            if t >= 2:
-                e_sha[t - 2][0].record(R)
-            ctx.dev_receive_step(R.ptr, cur, pend, e_sha[t - 2][1] if t >= 2 else None)
-            pend = cur
-        e_rx[1].record(R)
-        ctx.dev_receive_step(R.ptr, None, pend)
-        R.sync()
-        ok_rx = int((np.frombuffer(rbuf[(K_rx + 1) % 2]["status"].download().tobytes(), np.int32) == 0).sum())
-        if ok_rx != I:
-            raise SystemExit(f"bench: receive_step pass decoded {ok_rx} of {I} instances")
-        rx_step_ms = e_rx[0].elapsed_ms(e_rx[1]) / K_rx
-        rx_sha_iso_ms = sum(a_.elapsed_ms(b_) for a_, b_ in e_sha) / K_rx
+    # (the receiver alone as rbc_dev_receive_step, 8 back-to-back batches:
+    # 5.65 ms per C2 batch with its one-wave blocks, 4.87 with 256-thread
+    # blocks, against 4.77 for verify + interpolate as separate calls -- the
+    # receive step pays off only beside the proposer's stream)
+    rx_sha_iso_ms = None
 
     if pipe:
         args.warmup = max(args.warmup, 3 if (pipe3 or rxs) else 2)  # fill the pipeline: a decode before the guard
@@ -974,12 +944,6 @@ def main(argv):
                         "unit": "GB/s of committed shard bytes (N*S per instance), per rank",
                         "note": "ECHO-side Merkle branch verify + RS reconstruct / re-encode / root recheck alone "
                                 "(BASELINE configs[2]'s stages): verify + interpolate spans of serial steps"}
-        if rx_step_ms:
-            receive_only["receive_step"] = {
-                "GBps": round(I * n * S / (rx_step_ms / 1e3) / 1e9, 2), "ms_per_batch": round(rx_step_ms, 4),
-                "note": "the same stages as a streaming receiver runs them (rbc_dev_receive_step: ECHO verify "
-                        "of batch t and the regen hashing of t-1 in one SHA launch), 8 batches back to back on "
-                        "one stream, every instance decoded"}
 
     # GPU phase rates (per rank, from the stage events): encode+commit =
     # N*S shard bytes per instance; verify+decode = k*S value bytes

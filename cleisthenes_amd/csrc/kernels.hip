@@ -356,13 +356,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RBC_SHA_WPE
         uint32_t tix = (uint32_t)pos;
         for (int l = 0; l < a.depth; ++l, tix >>= 1) {
             const bool empty = (l == 0) && ((pos ^ 1) >= a.n);
-            uint32_t sib[8], o[8];
+            uint32_t o[8];
             if (empty) {
                 sha256_node32(h, o);
             } else {
+                // one node body with selected inputs (two inlined orderings
+                // cost code size and registers)
+                uint32_t sib[8], L[8], R[8];
                 load_digest(br + 32u * l, sib);
-                if (tix & 1u) sha256_node64(sib, h, o);
-                else sha256_node64(h, sib, o);
+                const bool right = (tix & 1u) != 0;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    L[q] = right ? sib[q] : h[q];
+                    R[q] = right ? h[q] : sib[q];
+                }
+                sha256_node64(L, R, o);
             }
 #pragma unroll
             for (int q = 0; q < 8; ++q) h[q] = o[q];
@@ -393,9 +401,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RBC_RX_WPE)
     set_wave_prio(v.prio);
     int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int nv = v.count <= 0 ? 0 : (v.list ? (int)*v.list_count : v.count * v.rows_per_inst);
-    const bool isv = t < nv;
+    // r's rows start at the next whole wave after v's, so every wave is all-v
+    // or all-r and the choice between the two argument blocks is scalar (the
+    // selected pointers and pitches stay in SGPRs: no spills at 128 VGPRs)
+    const int nv_pad = (nv + 63) & ~63;
+    const bool isv = __builtin_amdgcn_readfirstlane(t & ~63) < nv_pad;
     int inst, pos;
     if (isv) {
+        if (t >= nv) return;
         if (v.list) {
             const uint32_t e = v.list[t];
             inst = (int)(e >> 8);
@@ -405,7 +418,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RBC_RX_WPE)
             pos = t - inst * v.rows_per_inst;
         }
     } else {
-        t -= nv;
+        t -= nv_pad;
         if (r.count <= 0 || t >= (int)*r.list_count) return;
         const uint32_t e = r.list[t];
         inst = (int)(e >> 8);
@@ -429,13 +442,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RBC_RX_WPE)
         uint32_t tix = (uint32_t)pos;
         for (int l = 0; l < v.depth; ++l, tix >>= 1) {
             const bool empty = (l == 0) && ((pos ^ 1) >= v.n);
-            uint32_t sib[8], o[8];
+            uint32_t o[8];
             if (empty) {
                 sha256_node32(h, o);
             } else {
+                // one node body with selected inputs (two inlined orderings
+                // cost code size and registers)
+                uint32_t sib[8], L[8], R[8];
                 load_digest(br + 32u * l, sib);
-                if (tix & 1u) sha256_node64(sib, h, o);
-                else sha256_node64(h, sib, o);
+                const bool right = (tix & 1u) != 0;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    L[q] = right ? sib[q] : h[q];
+                    R[q] = right ? h[q] : sib[q];
+                }
+                sha256_node64(L, R, o);
             }
 #pragma unroll
             for (int q = 0; q < 8; ++q) h[q] = o[q];
@@ -1467,7 +1488,7 @@ hipError_t rbc_launch_sha_rows(const ShaArgs &a, bool verify, hipStream_t st) {
 }
 
 hipError_t rbc_launch_sha_rx(const ShaArgs &v, const ShaArgs &r, bool v_walk, hipStream_t st) {
-    const long total = (v.count > 0 ? (long)v.count * v.rows_per_inst : 0) +
+    const long total = (v.count > 0 ? ((long)v.count * v.rows_per_inst + 63) / 64 * 64 : 0) +
                        (r.count > 0 ? (long)r.count * r.rows_per_inst : 0);
     if (total <= 0) return hipSuccess;
     if ((v.count > 0 && (!v.rows || (v_walk && (!v.valid || !v.roots)))) || (r.count > 0 && (!r.list || !r.list_count)))
