@@ -196,6 +196,7 @@ struct rbc_ctx {
     // interpolate); rbc_ctx_set_wave_priority, RBC_TX_PRIO / RBC_RX_PRIO
     int tx_prio = 0, rx_prio = 0;
     int rxv_prio = 0;              // ECHO verify (RBC_RXV_PRIO A/B; else rx_prio)
+    int enc_prio = 0;              // RS encode (RBC_ENC_PRIO A/B; else tx_prio)
     std::vector<uint8_t> h_M;      // n x k encode matrix
     uint8_t *d_M = nullptr;        // device copy; parity rows at d_M + k*k
     std::mutex mu;
@@ -239,6 +240,7 @@ int ctx_create_kn(int n, int k, int device, rbc_ctx **out) {
     c->tx_prio = env_prio("RBC_TX_PRIO");
     c->rx_prio = env_prio("RBC_RX_PRIO");
     c->rxv_prio = getenv("RBC_RXV_PRIO") ? env_prio("RBC_RXV_PRIO") : c->rx_prio;
+    c->enc_prio = getenv("RBC_ENC_PRIO") ? env_prio("RBC_ENC_PRIO") : c->tx_prio;
     if (!rbchost::build_matrix(k, n, c->h_M)) { delete c; return RBC_ERR_SINGULAR; }
     // d_M = [n x k encode matrix | exp[512] | log[256]] (tables for decode_prepare_fft)
     std::vector<uint8_t> up(c->h_M);
@@ -298,7 +300,7 @@ int stage_encode(rbc_ctx *c, hipStream_t st, int count, const uint8_t *values, u
         a.row_pitch = shard_pitch;
         a.lens = value_lens;
         a.uniform_len = uniform_value_len;
-        a.prio = c->tx_prio;
+        a.prio = c->enc_prio;
         RBC_HIP(rbc_launch_rs_fft(a, st));
         return RBC_OK;
     }
@@ -320,7 +322,7 @@ int stage_encode(rbc_ctx *c, hipStream_t st, int count, const uint8_t *values, u
     g.uniform_len = uniform_value_len;
     g.coef = c->d_M + (size_t)c->k * c->k;
     g.coef_inst_stride = 0;
-    g.prio = c->tx_prio;
+    g.prio = c->enc_prio;
     RBC_HIP(rbc_launch_gf_rows(g, st));
     return RBC_OK;
 }
@@ -1031,6 +1033,7 @@ int rbc_ctx_set_wave_priority(rbc_ctx *c, int commit_prio, int receive_prio) {
     c->tx_prio = commit_prio;
     c->rx_prio = receive_prio;
     c->rxv_prio = receive_prio;
+    c->enc_prio = getenv("RBC_ENC_PRIO") ? env_prio("RBC_ENC_PRIO") : commit_prio;
     return RBC_OK;
 }
 
