@@ -308,6 +308,7 @@ def main(argv):
         nsets -= 1
         if nsets < (3 if (pipe3 or rxs or pdec) else 2):
             pipe, pipe3, nsets = False, False, 1
+            rxs = pdec = False
     sets = [dict(shards=mb(I * n * spitch), leaves=mb(I * n * 32), roots=mb(I * 32),
                  branches=mb(I * n * max(d, 1) * 32),
                  **({"valid": mb(I * n), "leaves_r": mb(I * n * 32)} if pipe3 else {}),
@@ -853,7 +854,7 @@ def main(argv):
     # PMC-measured HBM traffic per launch (tools/profile.sh + tools/pmc_summary.py
     # on this bench's default command), newest round first
     pm, pmc_path = {}, None
-    for cand in ("pmc_traffic_r02s4.json", "pmc_traffic_r02s3.json", "pmc_traffic_r02.json", "pmc_traffic_r01.json"):
+    for cand in ("pmc_traffic_r02s5.json", "pmc_traffic_r02.json", "pmc_traffic_r01.json"):
         pth = os.path.join(ROOT, "profiles", cand)
         if os.path.exists(pth):
             try:

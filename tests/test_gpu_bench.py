@@ -33,9 +33,9 @@ def test_bench_schedules_pass_their_guard(pipeline):
     assert 0 < d["roofline"]["frac"] < 1 and d["roofline"]["avg_ms"] > 0
 
 
-def _run(args, timeout=300):
+def _run(args, timeout=300, env=None):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
-                       timeout=timeout)
+                       timeout=timeout, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, r.stdout
@@ -63,3 +63,14 @@ def test_bench_one_rank_rccl_gather():
     assert d["rccl"] is not None and d["rccl"]["nranks"] == 1
     assert "torch" not in d["rccl"]["lib"]
     assert d["decoded_ok"] == 64 and d["values_ok"] and d["gather_ok"]
+
+
+def test_bench_falls_back_to_serial_when_the_shard_sets_do_not_fit():
+    """C3 with all 8,192 instances on one GPU cannot hold the pipeline's shard
+    sets: with an HBM budget below one set the default schedule must fall back
+    to the serial one and still pass its guard."""
+    env = dict(os.environ, RBC_BENCH_HBM_BUDGET="1e6")
+    d = _run(["--instances", "64", "--steps", "3", "--warmup", "2", "--no-cpu-baseline", "--no-pcie",
+              "--oracle-samples", "4"], env=env)
+    assert d["config"]["pipeline"] == "serial"
+    assert d["decoded_ok"] == 64 and d["values_ok"] and d["oracle_sample_ok"]
