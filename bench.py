@@ -298,7 +298,7 @@ def main(argv):
     # Wave issue priority (s_setprio) under the two-stream schedule: the
     # receiver stream (verify + interpolate, whose regen-hash tail is a
     # latency-bound dependent chain) at 2, the proposer at 0.  A/B on one box
-    # (tools/gpu_r02prio*.sh): 442-446 GB/s at 0/0, 447-451 at 0/2, 411 at 3/0.
+    # (tools/gpu_runs/gpu_r02prio*.sh): 442-446 GB/s at 0/0, 447-451 at 0/2, 411 at 3/0.
     # RBC_TX_PRIO / RBC_RX_PRIO override.
     prio_tx = int(os.environ.get("RBC_TX_PRIO", "0"))
     prio_rx = int(os.environ.get("RBC_RX_PRIO", "2" if pipe else "0"))
