@@ -75,8 +75,8 @@ def round_up(x, a):
 def parse_args(argv):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=60,
-                    help="timed steps (the default keeps ~0.4 s of GPU work in the timed region at C2)")
+    ap.add_argument("--steps", type=int, default=150,
+                    help="timed steps (the default keeps ~1 s of GPU work in the timed region at C2)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--instances", type=int, default=0, help="instances per GPU (weak scaling; default per config)")
