@@ -123,6 +123,7 @@ struct Ws {
     bool fork = true;
     bool join_pending = false;  // a forked join awaits its CHECK phase
     int rx_count = 0;           // receive_step: batch decoded by the last call, awaiting its rehash + check
+    const uint8_t *rx_shards = nullptr;  // ... and its shard buffer (identity check of `prev`)
     hipStream_t aux = nullptr;  // created on first use
     hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_hashed = nullptr;
     bool init() {
@@ -776,7 +777,8 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
     if (prev && (rc = check_rx_batch(c, prev))) return rc;
     const bool hc = cur && cur->count > 0, hp = prev && prev->count > 0;
     // prev must be the batch whose decode the previous call left in the workspace
-    if (hp != (w.rx_count > 0) || (hp && prev->count != w.rx_count)) return RBC_ERR_INVALID_ARG;
+    if (hp != (w.rx_count > 0) || (hp && (prev->count != w.rx_count || prev->shards != w.rx_shards)))
+        return RBC_ERR_INVALID_ARG;
     if (!hc && !hp) return RBC_OK;
     if (!aux_stream(w)) return RBC_ERR_DEVICE;
     const int nr = c->n - c->k;
@@ -890,6 +892,7 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
         j.prio = c->rx_prio;
         RBC_HIP(rbc_launch_join(j, w.aux));
         w.rx_count = cur->count;
+        w.rx_shards = cur->shards;
     }
     if (hp) RBC_HIP(hipStreamWaitEvent(st, w.ev_join, 0));
     return RBC_OK;

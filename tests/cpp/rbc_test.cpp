@@ -298,6 +298,119 @@ static void TestBatcherConcurrent() {
     rbc_ctx_destroy(ctx);
 }
 
+// rbc_dev_receive_step from a pure C-ABI client: three batches through the
+// pipelined receiver (verify(t) + regen hashing of t-1 in one launch) give
+// the same valid masks, statuses, values and digests as rbc_dev_verify +
+// rbc_dev_interpolate on identical inputs; a wrong `prev` is rejected.
+static void TestReceiveStep() {
+    const int n = 16, f = 5, I = 20, nb = 3;
+    const uint32_t B = 3001;
+    rbc_ctx *ctx = nullptr;
+    CHECK(rbc_ctx_create(n, f, 0, &ctx) == RBC_OK);
+    int k = 0, p = 0, d = 0;
+    CHECK(rbc_ctx_params(ctx, &k, &p, &d) == RBC_OK);
+    const uint32_t S = (B + k - 1) / k, spitch = (S + 63) / 64 * 64;
+    const uint64_t vpitch = ((uint64_t)k * S + 32 + 63) / 64 * 64;
+    const uint32_t opitch = (k * S + 15) / 16 * 16;
+    std::vector<uint8_t> present((size_t)I * n, 0);
+    std::vector<int32_t> corrupt(I, -1);
+    std::mt19937 g(77);
+    for (int i = 0; i < I; ++i) {
+        std::vector<int> idx(n);
+        for (int j = 0; j < n; ++j) idx[j] = j;
+        std::shuffle(idx.begin(), idx.end(), g);
+        for (int j = 0; j < n - f; ++j) present[(size_t)i * n + idx[j]] = 1;
+        if (i % 3 == 0) corrupt[i] = idx[0];
+    }
+    auto dmalloc = [](size_t bytes) {
+        void *q = nullptr;
+        return rbc_dev_malloc(0, bytes, &q) == RBC_OK ? (uint8_t *)q : nullptr;
+    };
+    uint8_t *d_present = dmalloc(present.size());
+    int32_t *d_corrupt = (int32_t *)dmalloc(I * 4);
+    CHECK(d_present && d_corrupt);
+    CHECK(rbc_memcpy_h2d(d_present, present.data(), present.size()) == RBC_OK);
+    CHECK(rbc_memcpy_h2d(d_corrupt, corrupt.data(), I * 4) == RBC_OK);
+    struct Bufs {
+        uint8_t *values, *shards, *leaves, *roots, *branches, *valid, *leaves_r, *out, *digests;
+        int32_t *status;
+    };
+    // [mode][batch]: mode 0 = verify + interpolate, mode 1 = receive step
+    Bufs b[2][nb];
+    for (int m = 0; m < 2; ++m)
+        for (int t = 0; t < nb; ++t) {
+            Bufs &x = b[m][t];
+            x.values = dmalloc(I * vpitch);
+            x.shards = dmalloc((size_t)I * n * spitch);
+            x.leaves = dmalloc((size_t)I * n * 32);
+            x.roots = dmalloc(I * 32);
+            x.branches = dmalloc((size_t)I * n * d * 32);
+            x.valid = dmalloc((size_t)I * n);
+            x.leaves_r = dmalloc((size_t)I * n * 32);
+            x.out = dmalloc((size_t)I * opitch);
+            x.digests = dmalloc(I * 32);
+            x.status = (int32_t *)dmalloc(I * 4);
+            CHECK(x.values && x.shards && x.leaves && x.roots && x.branches && x.valid && x.leaves_r && x.out &&
+                  x.digests && x.status);
+            const std::vector<uint8_t> v = random_bytes(I * vpitch, 900 + t);
+            CHECK(rbc_memcpy_h2d(x.values, v.data(), v.size()) == RBC_OK);
+            CHECK(rbc_dev_encode(ctx, nullptr, I, x.values, vpitch, nullptr, B, x.shards, spitch) == RBC_OK);
+            CHECK(rbc_dev_leaves(ctx, nullptr, I, x.shards, spitch, nullptr, S, x.leaves) == RBC_OK);
+            CHECK(rbc_dev_merkle_build(ctx, nullptr, I, x.leaves, x.roots, x.branches) == RBC_OK);
+            CHECK(rbc_dev_inject_faults(ctx, nullptr, I, x.shards, spitch, d_corrupt) == RBC_OK);
+        }
+    for (int t = 0; t < nb; ++t) {
+        Bufs &x = b[0][t];
+        CHECK(rbc_dev_verify(ctx, nullptr, I, x.shards, spitch, nullptr, S, x.branches, x.roots, d_present, x.valid,
+                             x.leaves_r) == RBC_OK);
+        CHECK(rbc_dev_interpolate(ctx, nullptr, I, x.shards, spitch, nullptr, S, x.valid, x.leaves_r, 1, x.roots,
+                                  x.out, opitch, x.digests, x.status) == RBC_OK);
+    }
+    rbc_rx_batch rb[nb];
+    for (int t = 0; t < nb; ++t) {
+        Bufs &x = b[1][t];
+        rb[t] = rbc_rx_batch{I, x.shards, spitch, nullptr, S, x.branches, x.roots, d_present, x.valid, x.leaves_r,
+                             x.out, opitch, x.digests, x.status};
+    }
+    CHECK(rbc_dev_receive_step(ctx, nullptr, &rb[0], nullptr, nullptr) == RBC_OK);
+    CHECK(rbc_dev_receive_step(ctx, nullptr, &rb[1], &rb[2], nullptr) == RBC_ERR_INVALID_ARG);  // not the last cur
+    for (int t = 1; t < nb; ++t) CHECK(rbc_dev_receive_step(ctx, nullptr, &rb[t], &rb[t - 1], nullptr) == RBC_OK);
+    CHECK(rbc_dev_receive_step(ctx, nullptr, nullptr, &rb[nb - 1], nullptr) == RBC_OK);
+    CHECK(rbc_device_sync(0) == RBC_OK);
+    for (int t = 0; t < nb; ++t) {
+        std::vector<int32_t> s0(I), s1(I);
+        std::vector<uint8_t> v0((size_t)I * n), v1((size_t)I * n), o0((size_t)I * opitch), o1((size_t)I * opitch),
+            g0(I * 32), g1(I * 32);
+        CHECK(rbc_memcpy_d2h(s0.data(), b[0][t].status, I * 4) == RBC_OK);
+        CHECK(rbc_memcpy_d2h(s1.data(), b[1][t].status, I * 4) == RBC_OK);
+        CHECK(rbc_memcpy_d2h(v0.data(), b[0][t].valid, v0.size()) == RBC_OK);
+        CHECK(rbc_memcpy_d2h(v1.data(), b[1][t].valid, v1.size()) == RBC_OK);
+        CHECK(rbc_memcpy_d2h(o0.data(), b[0][t].out, o0.size()) == RBC_OK);
+        CHECK(rbc_memcpy_d2h(o1.data(), b[1][t].out, o1.size()) == RBC_OK);
+        CHECK(rbc_memcpy_d2h(g0.data(), b[0][t].digests, g0.size()) == RBC_OK);
+        CHECK(rbc_memcpy_d2h(g1.data(), b[1][t].digests, g1.size()) == RBC_OK);
+        const std::vector<uint8_t> v = random_bytes(I * vpitch, 900 + t);
+        for (int i = 0; i < I; ++i) {
+            CHECK(s0[i] == RBC_OK && s1[i] == RBC_OK);
+            for (int j = 0; j < n; ++j)
+                CHECK(v0[(size_t)i * n + j] == v1[(size_t)i * n + j]);
+            CHECK(memcmp(o0.data() + (size_t)i * opitch, o1.data() + (size_t)i * opitch, k * S) == 0);
+            CHECK(memcmp(o1.data() + (size_t)i * opitch, v.data() + (size_t)i * vpitch, B) == 0);
+            CHECK(memcmp(g0.data() + i * 32, g1.data() + i * 32, 32) == 0);
+        }
+    }
+    for (int m = 0; m < 2; ++m)
+        for (int t = 0; t < nb; ++t) {
+            Bufs &x = b[m][t];
+            for (void *q : {(void *)x.values, (void *)x.shards, (void *)x.leaves, (void *)x.roots, (void *)x.branches,
+                            (void *)x.valid, (void *)x.leaves_r, (void *)x.out, (void *)x.digests, (void *)x.status})
+                rbc_dev_free(q);
+        }
+    rbc_dev_free(d_present);
+    rbc_dev_free(d_corrupt);
+    rbc_ctx_destroy(ctx);
+}
+
 int main() {
     int ndev = 0;
     rbc_device_count(&ndev);
@@ -309,7 +422,7 @@ int main() {
         {"TestOneEncode", TestOneEncode},   {"TestReconstruct", TestReconstruct},
         {"Test_shard", Test_shard},         {"Test_validateMessage", Test_validateMessage},
         {"Test_interpolate", Test_interpolate}, {"TestBatcherConcurrent", TestBatcherConcurrent},
-        {"TestUpdate", TestUpdate},
+        {"TestUpdate", TestUpdate},         {"TestReceiveStep", TestReceiveStep},
     };
     for (auto &t : tests) {
         const int before = failures;

@@ -18,7 +18,7 @@ def test_cpp_abi_suite():
     print(r.stdout)
     print(r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert r.stdout.count("PASS") == 7
+    assert r.stdout.count("PASS") == 8
 
 
 def test_cpp_abi_builds():
