@@ -1224,6 +1224,8 @@ int rbc_dev_interpolate_phases(rbc_ctx *c, void *stream, int phases, int count, 
                                uint8_t *values_out, uint32_t value_pitch, uint8_t *digests, int32_t *status) {
     if (!c) return RBC_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(c->mu);  // shared decode workspace
+    // the workspace holds a receive-step batch's regen list until its next call
+    if (c->ws.rx_count > 0) return RBC_ERR_INVALID_ARG;
     RBC_HIP(hipSetDevice(c->device));
     return stage_interpolate(c, c->ws, as_stream(stream), count, shards, shard_pitch, shard_lens, uniform_shard_len,
                              valid, leaves, leaves_verified, roots, values_out, value_pitch, digests, status, phases);

@@ -203,7 +203,9 @@ int rbc_dev_interpolate_phases(rbc_ctx *ctx, void *stream, int phases, int count
  * values_out / digests are final and equal rbc_dev_verify followed by
  * rbc_dev_interpolate(leaves_verified = 1) on the same inputs (interpolate,
  * rbc/rbc.go:86-90); cur's buffers must stay untouched until the next call's
- * work is done.  All pointers are device memory; present may be NULL (all
+ * work is done.  While a batch is pending, rbc_dev_interpolate(_phases) on
+ * the same context returns RBC_ERR_INVALID_ARG (they share its decode
+ * workspace).  All pointers are device memory; present may be NULL (all
  * received). */
 typedef struct rbc_rx_batch {
     int count;

@@ -1205,6 +1205,12 @@ def test_receive_step_pipeline_equals_verify_then_interpolate(gpu, ref, n, f, B,
             prev = None
             for cur in bs + [None]:
                 rx.dev_receive_step(st.ptr, cur, prev)
+                if cur is not None and prev is None:  # a batch is pending: interpolate must refuse
+                    pl = pls[0]
+                    with pytest.raises(gpu.RBCError):
+                        rx.dev_interpolate(st.ptr, I, pl.b["shards"], pl.spitch, None, pl.S, pl.b["valid"],
+                                           pl.b["leaves_r"], 1, pl.b["roots"], pl.b["out"], pl.opitch,
+                                           pl.b["digests"], pl.b["status"])
                 prev = cur
             with pytest.raises(gpu.RBCError):  # prev must be the last call's cur
                 rx.dev_receive_step(st.ptr, None, bs[0])
