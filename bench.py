@@ -877,6 +877,8 @@ def main(argv):
             r["traffic"] = pk["hbm_bytes_per_launch"]
             r["traffic_source"] = os.path.relpath(pmc_path, ROOT)
         if ncomp:
+            r["bound_note"] = ("SHA-256 is integer-VALU bound: HBM frac is not this kernel's roof (see valu and "
+                               "isolated); avg_ms is its span beside the other stream's kernels")
             # SHA-256 is integer-VALU bound (north_star: hashes/s against the VALU
             # peak): compressions/s against the issue-cost-weighted VALU peak, and
             # against the register-resident probe (what the instruction mix attains)
