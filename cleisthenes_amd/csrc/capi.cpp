@@ -779,10 +779,12 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
     // prev must be the batch whose decode the previous call left in the workspace
     if (hp != (w.rx_count > 0) || (hp && (prev->count != w.rx_count || prev->shards != w.rx_shards)))
         return RBC_ERR_INVALID_ARG;
+    if (hc && hp && cur->shards == prev->shards) return RBC_ERR_INVALID_ARG;  // one batch in both roles
     if (!hc && !hp) return RBC_OK;
     if (!aux_stream(w)) return RBC_ERR_DEVICE;
     const int nr = c->n - c->k;
     ShaArgs v{}, r{};
+    v.prio = c->rxv_prio;  // the launch's wave priority (also when only prev's rows are hashed)
     bool v_walk = false, v_path = false;
     if (hc) {
         v.count = cur->count;
@@ -801,7 +803,6 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
         v.roots = cur->roots;
         v.present = cur->present;
         v.valid = cur->valid;
-        v.prio = c->rxv_prio;
         if (cur->present && c->n <= 256) {  // hash only the received shards (stage_verify)
             RBC_HIP(w.vlist.ensure((size_t)cur->count * c->n * 4 + 64));
             uint32_t *vl = w.vlist.as<uint32_t>(), *vc = vl + (size_t)cur->count * c->n;
