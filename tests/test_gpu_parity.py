@@ -1272,3 +1272,26 @@ def test_interpolate_phases_equal_one_shot(gpu, ref, n, f, B, I):
         if i % 7 == 0:
             continue
         assert bytes(pl.values[i, :B]) == bytes(v1[np.cumsum(s1 == 0)[i] - 1][:B])
+
+
+def test_wave_priority_changes_no_result(gpu, ref):
+    """rbc_ctx_set_wave_priority only reorders issue on the SIMDs: commit and
+    receive at priority 0/0 and 3/3 (and the bench's 0/2) give identical
+    shards, roots, branches, valid masks, values, digests and statuses; a
+    level outside 0..3 is rejected."""
+    n, f, B, I = 128, 42, 1 << 16, 64
+    outs = []
+    for tx, rx in ((0, 0), (3, 3), (0, 2)):
+        pl = Pipeline(gpu, n, f, B, I, seed=4242, corrupt_frac=0.3)
+        pl.ctx.set_wave_priority(tx, rx)
+        pl.commit()
+        pl.receive()
+        gpu.rbc.lib.rbc_device_sync(0)
+        outs.append([pl.arr(k) for k in ("shards", "roots", "branches", "valid", "out", "digests", "status",
+                                          "leaves_r")])
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert np.array_equal(a, b)
+    for bad in ((4, 0), (0, -1)):
+        with pytest.raises(gpu.RBCError):
+            pl.ctx.set_wave_priority(*bad)
