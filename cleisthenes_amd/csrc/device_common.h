@@ -168,7 +168,11 @@ RBC_DEV void sha256_row(const uint8_t *row, uint32_t len, Sha256State &s) {
     const uint32_t nfull = len >> 6;
     uint32_t w[16];
     // software pipeline: block b+1's loads are in flight while block b is
-    // compressed (a compression is ~1.4k VALU ops, longer than an HBM miss)
+    // compressed (a compression is ~1.4k VALU ops, longer than an HBM miss).
+    // (Two blocks per iteration with ping-pong buffers drops 9 VALU per
+    // compression and is ~2 % faster alone, but takes the leaf kernel from 108
+    // to 124 VGPRs and the two-stream bench from 479-485 to 454-459 GB/s:
+    // tools/gpu_runs/gpu_r02unroll.sh.)
     uint4 q[4];
     if (nfull) load_block_raw(row, q);
     for (uint32_t b = 0; b < nfull; ++b) {
