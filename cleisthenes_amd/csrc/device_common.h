@@ -173,6 +173,8 @@ RBC_DEV void sha256_row(const uint8_t *row, uint32_t len, Sha256State &s) {
     // compression and is ~2 % faster alone, but takes the leaf kernel from 108
     // to 124 VGPRs and the two-stream bench from 479-485 to 454-459 GB/s:
     // tools/gpu_runs/gpu_r02unroll.sh.)
+    // (Without the prefetch the leaf kernel needs 95 VGPRs instead of 108,
+    // and the bench drops from 489-498 to 469-477 GB/s: tools/gpu_runs/gpu_r02pf.sh.)
     uint4 q[4];
     if (nfull) load_block_raw(row, q);
     for (uint32_t b = 0; b < nfull; ++b) {
@@ -180,6 +182,7 @@ RBC_DEV void sha256_row(const uint8_t *row, uint32_t len, Sha256State &s) {
         if (b + 1 < nfull) load_block_raw(row + 64u * (b + 1), q);
         sha256_compress(s, w);
     }
+
     const uint32_t rem = len & 63u;
     if (rem) {
         load_block_be(row + 64u * nfull, w);
