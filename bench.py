@@ -854,7 +854,7 @@ def main(argv):
     # PMC-measured HBM traffic per launch (tools/profile.sh + tools/pmc_summary.py
     # on this bench's default command), newest round first
     pm, pmc_path = {}, None
-    for cand in ("pmc_traffic_r02s7.json", "pmc_traffic_r02.json", "pmc_traffic_r01.json"):
+    for cand in ("pmc_traffic_r02s8.json", "pmc_traffic_r02.json", "pmc_traffic_r01.json"):
         pth = os.path.join(ROOT, "profiles", cand)
         if os.path.exists(pth):
             try:
