@@ -1295,3 +1295,77 @@ def test_wave_priority_changes_no_result(gpu, ref):
     for bad in ((4, 0), (0, -1)):
         with pytest.raises(gpu.RBCError):
             pl.ctx.set_wave_priority(*bad)
+
+
+@pytest.mark.parametrize("n,f", [(16, 5), (256, 85)])
+def test_receive_step_ragged_lengths_and_too_few_shards(gpu, ref, n, f):
+    """rbc_dev_receive_step with per-instance shard lengths (ragged batch from
+    the host shard+commit API), instances with only k-1 received shards
+    (TOO_FEW_SHARDS) and corrupted ECHOs: two batches through the receive step
+    equal rbc_dev_verify + rbc_dev_interpolate on copies of the same inputs;
+    every decoded value equals its input."""
+    ctx = gpu.Context(n, f)
+    k = ctx.k
+    rng = np.random.default_rng(n + 99)
+    lens = [1, k, 3 * k + 1, 50 * k, 7, 200 * k + 5, 64 * k, 5 * k + 3, 1000]
+    I = len(lens)
+    mb = gpu.DeviceBuffer
+    batches = []
+    for bi in range(2):
+        values = [rng.integers(0, 256, L, dtype=np.uint8) for L in lens]
+        out = ctx.shard_commit_batch(values)
+        Smax = out["shards"].shape[2]
+        pitch = rup(Smax, 64)
+        opitch = rup(k * Smax, 16)
+        sh = np.zeros((I, n, pitch), np.uint8)
+        sh[:, :, :Smax] = out["shards"]
+        present = np.zeros((I, n), np.uint8)
+        for i in range(I):
+            cnt = k - 1 if i % 4 == bi + 1 else n - f
+            pres = rng.permutation(n)[:cnt]
+            present[i, pres] = 1
+            if i % 3 == 0:
+                sh[i, pres[0], rng.integers(int(out["shard_lens"][i]))] ^= 0x21
+        batches.append(dict(values=values, out=out, sh=sh, present=present, pitch=pitch, opitch=opitch))
+    res = {}
+    for mode in ("oneshot", "step"):
+        c = gpu.Context(n, f)
+        bufs = []
+        for bt in batches:
+            d = dict(sh=mb(bt["sh"].nbytes), br=mb(bt["out"]["branches"].nbytes), rt=mb(I * 32), ln=mb(4 * I),
+                     pr=mb(I * n), va=mb(I * n), lv=mb(I * n * 32), vo=mb(I * bt["opitch"]), dg=mb(I * 32),
+                     st=mb(4 * I))
+            d["sh"].upload(bt["sh"])
+            d["br"].upload(np.ascontiguousarray(bt["out"]["branches"]))
+            d["rt"].upload(bt["out"]["roots"])
+            d["ln"].upload(bt["out"]["shard_lens"].astype(np.uint32))
+            d["pr"].upload(bt["present"])
+            bufs.append(d)
+        if mode == "oneshot":
+            for bt, d in zip(batches, bufs):
+                c.dev_verify(None, I, d["sh"], bt["pitch"], d["ln"], 0, d["br"], d["rt"], d["pr"], d["va"], d["lv"])
+                c.dev_interpolate(None, I, d["sh"], bt["pitch"], d["ln"], 0, d["va"], d["lv"], 1, d["rt"], d["vo"],
+                                  bt["opitch"], d["dg"], d["st"])
+        else:
+            rbs = [c.rx_batch(I, d["sh"], bt["pitch"], d["ln"], 0, d["br"], d["rt"], d["pr"], d["va"], d["lv"],
+                              d["vo"], bt["opitch"], d["dg"], d["st"]) for bt, d in zip(batches, bufs)]
+            c.dev_receive_step(None, rbs[0], None)
+            c.dev_receive_step(None, rbs[1], rbs[0])
+            c.dev_receive_step(None, None, rbs[1])
+        gpu.rbc.lib.rbc_device_sync(0)
+        res[mode] = [(np.frombuffer(d["st"].download().tobytes(), np.int32).copy(),
+                      np.frombuffer(d["va"].download().tobytes(), np.uint8).reshape(I, n).copy(),
+                      np.frombuffer(d["vo"].download().tobytes(), np.uint8).reshape(I, bt["opitch"]).copy(),
+                      np.frombuffer(d["dg"].download().tobytes(), np.uint8).reshape(I, 32).copy())
+                     for bt, d in zip(batches, bufs)]
+    for bi, bt in enumerate(batches):
+        (s0, v0, o0, g0), (s1, v1, o1, g1) = res["oneshot"][bi], res["step"][bi]
+        assert np.array_equal(s0, s1) and np.array_equal(v0, v1), bi
+        for i in range(I):
+            if i % 4 == bi + 1:
+                assert s1[i] == -3, (bi, i)  # TOO_FEW_SHARDS
+                continue
+            assert s1[i] == 0, (bi, i)
+            L = lens[i]
+            assert bytes(o1[i, :L]) == bytes(bt["values"][i]) and np.array_equal(o0[i, :L], o1[i, :L])
+            assert np.array_equal(g0[i], g1[i])
