@@ -1369,3 +1369,42 @@ def test_receive_step_ragged_lengths_and_too_few_shards(gpu, ref, n, f):
             L = lens[i]
             assert bytes(o1[i, :L]) == bytes(bt["values"][i]) and np.array_equal(o0[i, :L], o1[i, :L])
             assert np.array_equal(g0[i], g1[i])
+
+
+def test_receive_step_batches_of_different_sizes(gpu, ref):
+    """Consecutive receive steps on batches of 40, 17 and 33 instances (the
+    hashing launch covers cur's and prev's counts separately) give the same
+    statuses, values and digests as verify + interpolate."""
+    n, f, B = 16, 5, 2000
+    sizes = [40, 17, 33]
+    res = {}
+    for mode in ("oneshot", "step"):
+        pls = []
+        for bi, I in enumerate(sizes):
+            pl = Pipeline(gpu, n, f, B, I, seed=555 + bi, corrupt_frac=0.3)
+            pl.commit()
+            pl.ctx.dev_inject_faults(None, I, pl.b["shards"], pl.spitch, pl.b["corrupt"])
+            pls.append(pl)
+        if mode == "oneshot":
+            for pl in pls:
+                b, c, I = pl.b, pl.ctx, pl.I
+                c.dev_verify(None, I, b["shards"], pl.spitch, None, pl.S, b["branches"], b["roots"], b["present"],
+                             b["valid"], b["leaves_r"])
+                c.dev_interpolate(None, I, b["shards"], pl.spitch, None, pl.S, b["valid"], b["leaves_r"], 1,
+                                  b["roots"], b["out"], pl.opitch, b["digests"], b["status"])
+        else:
+            rx = gpu.Context(n, f)
+            bs = [rx.rx_batch(pl.I, pl.b["shards"], pl.spitch, None, pl.S, pl.b["branches"], pl.b["roots"],
+                              pl.b["present"], pl.b["valid"], pl.b["leaves_r"], pl.b["out"], pl.opitch,
+                              pl.b["digests"], pl.b["status"]) for pl in pls]
+            prev = None
+            for cur in bs + [None]:
+                rx.dev_receive_step(None, cur, prev)
+                prev = cur
+        gpu.rbc.lib.rbc_device_sync(0)
+        res[mode] = [(pl.arr("status", np.int32).copy(), pl.arr("out", shape=(pl.I, pl.opitch)).copy(),
+                      pl.arr("digests", shape=(pl.I, 32)).copy(), pl) for pl in pls]
+    for (s0, o0, d0, _), (s1, o1, d1, pl) in zip(res["oneshot"], res["step"]):
+        assert (s0 == 0).all() and np.array_equal(s0, s1)
+        assert np.array_equal(o0[:, : pl.k * pl.S], o1[:, : pl.k * pl.S]) and np.array_equal(d0, d1)
+        assert all(bytes(pl.values[i, :B]) == bytes(o1[i, :B]) for i in range(pl.I))
