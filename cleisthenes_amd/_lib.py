@@ -38,6 +38,11 @@ class RxBatch(ctypes.Structure):
                 ("value_pitch", c_uint32), ("digests", c_void_p), ("status", c_void_p)]
 
 
+class RxMarks(ctypes.Structure):
+    """rbc_rx_marks (include/rbc_gpu.h): timing events of rbc_dev_receive_step."""
+    _fields_ = [("hashed", c_void_p), ("decode_begin", c_void_p), ("decoded", c_void_p)]
+
+
 _SIGS = {
     "rbc_strerror": (c_char_p, [c_int]),
     "rbc_abi_version": (c_int, []),
@@ -58,8 +63,6 @@ _SIGS = {
     "rbc_host_free": (c_int, [c_void_p]),
     "rbc_stream_create": (c_int, [c_int, POINTER(c_void_p)]),
     "rbc_stream_create_priority": (c_int, [c_int, c_int, POINTER(c_void_p)]),
-    "rbc_stream_create_cu_mask": (c_int, [c_int, c_void_p, c_int, POINTER(c_void_p)]),
-    "rbc_device_cu_count": (c_int, [c_int, POINTER(c_int)]),
     "rbc_stream_destroy": (c_int, [c_void_p]),
     "rbc_stream_sync": (c_int, [c_void_p]),
     "rbc_event_create": (c_int, [POINTER(c_void_p)]),
@@ -68,6 +71,7 @@ _SIGS = {
     "rbc_event_elapsed_ms": (c_int, [c_void_p, c_void_p, POINTER(c_float)]),
     "rbc_stream_wait_event": (c_int, [c_void_p, c_void_p]),
     "rbc_device_sync": (c_int, [c_int]),
+    "rbc_device_mem_info": (c_int, [c_int, szp, szp]),
     "rbc_dev_encode": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_uint64, c_void_p, c_uint32, c_void_p,
                                c_uint32]),
     "rbc_dev_leaves": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_uint32, c_void_p, c_uint32, c_void_p]),
@@ -78,10 +82,7 @@ _SIGS = {
                                c_void_p, c_void_p, c_void_p, c_void_p]),
     "rbc_dev_interpolate": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_uint32, c_void_p, c_uint32, c_void_p,
                                     c_void_p, c_int, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p]),
-    "rbc_dev_receive_step": (c_int, [c_void_p, c_void_p, POINTER(RxBatch), POINTER(RxBatch), c_void_p]),
-    "rbc_dev_interpolate_phases": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_uint32, c_void_p, c_uint32,
-                                           c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_uint32, c_void_p,
-                                           c_void_p]),
+    "rbc_dev_receive_step": (c_int, [c_void_p, c_void_p, POINTER(RxBatch), POINTER(RxBatch), POINTER(RxMarks)]),
     "rbc_dev_inject_faults": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_uint32, c_void_p]),
     "rbc_shard_commit": (c_int, [c_void_p, c_int, c_void_p, szp, c_void_p, c_size_t, u32p, c_void_p, c_void_p,
                                  POINTER(c_uint64)]),
@@ -130,6 +131,8 @@ _SIGS = {
     "rbc_dev_fill_random": (c_int, [c_int, c_void_p, c_void_p, c_uint64, c_uint64, c_uint64, c_uint64]),
     "rbc_dev_count_mismatch": (c_int, [c_int, c_void_p, c_void_p, c_uint64, c_void_p, c_uint64, c_uint64, c_uint64,
                                        c_void_p]),
+    "rbc_dev_count_mismatch_rows": (c_int, [c_int, c_void_p, c_void_p, c_uint64, c_uint32, c_int, c_uint32, c_void_p,
+                                            c_uint64, c_uint32, c_uint64, c_void_p]),
     # include/rbc_protocol.h
     "rbc_pb_encode_rbc": (c_size_t, [c_int, c_void_p, c_size_t, c_void_p, c_size_t]),
     "rbc_pb_decode_rbc": (c_int, [c_void_p, c_size_t, POINTER(c_int), POINTER(c_void_p), szp]),

@@ -327,14 +327,9 @@ void rbc_batcher::finish(Pending &P) {
 // t+1 overlaps the GPU work (and copies) of batch t.
 void rbc_batcher::run() {
     std::deque<std::unique_ptr<Pending>> inflight;
-    // launches in flight (RBC_BATCHER_DEPTH, 1-8, default 4: 41 vs 27 GB/s of
-    // shard + commit through the coalescer at 2); the context needs as many
-    // host slots (RBC_HOST_SLOTS, default 4) or it retires one early
-    static const size_t depth_max = [] {
-        const char *e = getenv("RBC_BATCHER_DEPTH");
-        const int v = e ? atoi(e) : 4;
-        return (size_t)((v >= 1 && v <= 8) ? v : 4);
-    }();
+    // launches in flight: 4 (41 vs 27 GB/s of shard + commit through the
+    // coalescer at 2); the context has as many host slots
+    constexpr size_t depth_max = 4;
     std::unique_lock<std::mutex> lk(mu);
     while (true) {
         // pick the kind whose queue is full, or whose oldest request is due

@@ -32,43 +32,13 @@ namespace {
 constexpr size_t kAlign = 64;
 inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// rows per GF chunk (accumulators held in VGPRs); RBC_GF_RCMAX overrides
-int gf_rcmax() {
-    static const int v = [] {
-        const char *e = getenv("RBC_GF_RCMAX");
-        int x = e ? atoi(e) : 0;
-        return (x >= 1 && x <= 48) ? x : 21;
-    }();
-    return v;
-}
+// Rows per GF chunk (accumulators held in VGPRs) of the matrix codec.
+constexpr int kGfRcMax = 21;
 
-// RBC_CODEC=matrix forces the matrix kernel for new contexts (A/B runs)
-int codec_default() {
-    static const int v = [] {
-        const char *e = getenv("RBC_CODEC");
-        return (e && strcmp(e, "matrix") == 0) ? RBC_CODEC_MATRIX : RBC_CODEC_AUTO;
-    }();
-    return v;
-}
-
-// rows per chunk for the FFT codec's missing-data GF pass (RBC_GF_MDRC)
-int gf_md_rcmax(uint32_t shard_pitch) {
-    // rows per GF chunk for interpolate's missing data rows: 8 with 4 KiB
-    // column tiles; 4 with the one-wave tiles of short rows (C4: twice the
-    // blocks per CU for the 64-thread blocks, 2.32 -> 2.00 ms)
-    static const int v = [] {
-        const char *e = getenv("RBC_GF_MDRC");
-        int x = e ? atoi(e) : 0;
-        return (x >= 1 && x <= 48) ? x : 0;
-    }();
-    return v ? v : (shard_pitch <= 2048 ? 4 : 8);
-}
-
-int env_prio(const char *name) {
-    const char *e = getenv(name);
-    const int x = e ? atoi(e) : 0;
-    return (x >= 0 && x <= 3) ? x : 0;
-}
+// Rows per chunk of the FFT codec's missing-data GF pass: 8 with 4 KiB
+// column tiles; 4 with the one-wave tiles of short rows (C4: twice the blocks
+// per CU for the 64-thread blocks, 2.32 -> 2.00 ms).
+int gf_md_rcmax(uint32_t shard_pitch) { return shard_pitch <= 2048 ? 4 : 8; }
 
 int tree_width(int n) {
     int w = 1;
@@ -121,7 +91,6 @@ struct Ws {
     // stream each (their concurrency comes from the slots themselves, and
     // the box has GPU_MAX_HW_QUEUES = 4 hardware queues per process)
     bool fork = true;
-    bool join_pending = false;  // a forked join awaits its CHECK phase
     int rx_count = 0;           // receive_step: batch decoded by the last call, awaiting its rehash + check
     const uint8_t *rx_shards = nullptr;  // ... and its shard buffer (identity check of `prev`)
     hipStream_t aux = nullptr;  // created on first use
@@ -176,16 +145,9 @@ struct Slot {
     }
 };
 
-// host-API submissions in flight per context (RBC_HOST_SLOTS, default 4: the
-// batcher keeps 4 launches in flight, tools/batcher_bench.cpp)
-int host_slots() {
-    static const int v = [] {
-        const char *e = getenv("RBC_HOST_SLOTS");
-        int x = e ? atoi(e) : 0;
-        return (x >= 1 && x <= 8) ? x : 4;
-    }();
-    return v;
-}
+// host-API submissions in flight per context: the batcher keeps 4 launches
+// in flight (tools/batcher_bench.cpp), and the box has 4 hardware queues
+constexpr int kHostSlots = 4;
 
 }  // namespace
 
@@ -194,10 +156,8 @@ struct rbc_ctx {
     bool fft = false;              // additive-FFT codec active (rs_fft.hip)
     // wave issue priorities (s_setprio 0..3) of the commit-side kernels
     // (encode, leaves, tree build) and the receive-side ones (verify,
-    // interpolate); rbc_ctx_set_wave_priority, RBC_TX_PRIO / RBC_RX_PRIO
+    // interpolate); rbc_ctx_set_wave_priority, default 0
     int tx_prio = 0, rx_prio = 0;
-    int rxv_prio = 0;              // ECHO verify (RBC_RXV_PRIO A/B; else rx_prio)
-    int enc_prio = 0;              // RS encode (RBC_ENC_PRIO A/B; else tx_prio)
     std::vector<uint8_t> h_M;      // n x k encode matrix
     uint8_t *d_M = nullptr;        // device copy; parity rows at d_M + k*k
     std::mutex mu;
@@ -237,11 +197,7 @@ int ctx_create_kn(int n, int k, int device, rbc_ctx **out) {
     c->width = tree_width(n);
     c->depth = tree_depth(n);
     c->device = device;
-    c->fft = codec_default() != RBC_CODEC_MATRIX && rbc_fft_supported(n, k);
-    c->tx_prio = env_prio("RBC_TX_PRIO");
-    c->rx_prio = env_prio("RBC_RX_PRIO");
-    c->rxv_prio = getenv("RBC_RXV_PRIO") ? env_prio("RBC_RXV_PRIO") : c->rx_prio;
-    c->enc_prio = getenv("RBC_ENC_PRIO") ? env_prio("RBC_ENC_PRIO") : c->tx_prio;
+    c->fft = rbc_fft_supported(n, k);
     if (!rbchost::build_matrix(k, n, c->h_M)) { delete c; return RBC_ERR_SINGULAR; }
     // d_M = [n x k encode matrix | exp[512] | log[256]] (tables for decode_prepare_fft)
     std::vector<uint8_t> up(c->h_M);
@@ -301,7 +257,7 @@ int stage_encode(rbc_ctx *c, hipStream_t st, int count, const uint8_t *values, u
         a.row_pitch = shard_pitch;
         a.lens = value_lens;
         a.uniform_len = uniform_value_len;
-        a.prio = c->enc_prio;
+        a.prio = c->tx_prio;
         RBC_HIP(rbc_launch_rs_fft(a, st));
         return RBC_OK;
     }
@@ -310,7 +266,7 @@ int stage_encode(rbc_ctx *c, hipStream_t st, int count, const uint8_t *values, u
     g.tiles = (int)((shard_pitch + 4095) / 4096);
     g.R = c->p;
     g.K = c->k;
-    g.rc = rbc_gf_pick_rc(c->p > 0 ? c->p : 1, gf_rcmax());
+    g.rc = rbc_gf_pick_rc(c->p > 0 ? c->p : 1, kGfRcMax);
     g.mode = GF_MODE_ENCODE;
     g.in = values;
     g.in_inst_pitch = value_pitch;
@@ -323,7 +279,7 @@ int stage_encode(rbc_ctx *c, hipStream_t st, int count, const uint8_t *values, u
     g.uniform_len = uniform_value_len;
     g.coef = c->d_M + (size_t)c->k * c->k;
     g.coef_inst_stride = 0;
-    g.prio = c->enc_prio;
+    g.prio = c->tx_prio;
     RBC_HIP(rbc_launch_gf_rows(g, st));
     return RBC_OK;
 }
@@ -396,13 +352,9 @@ int stage_verify(rbc_ctx *c, hipStream_t st, int count, const uint8_t *shards, u
     a.roots = roots;
     a.present = present;
     a.valid = valid;
-    a.prio = c->rxv_prio;
+    a.prio = c->rx_prio;
     // Shared-path verification: leaves, then one hash per
-    // distinct branch-walk input.  RBC_VERIFY_PATH=0 runs the per-leaf walk.
-    static const int path_env = [] {  // 0 never, 1 (default) where it pays, 2 always
-        const char *e = getenv("RBC_VERIFY_PATH");
-        return e ? atoi(e) : 1;
-    }();
+    // distinct branch-walk input.
     // The per-leaf walk costs 2d compressions per row on top of the leaf's
     // ceil((S+9)/64); the shared-path form pays off where that walk is a real
     // share (C4: 16 vs 13) and only adds a launch where it is not (C2: 14 vs
@@ -412,12 +364,7 @@ int stage_verify(rbc_ctx *c, hipStream_t st, int count, const uint8_t *shards, u
     // Only the received ECHOs are validated (validateMessage runs per message):
     // with a present mask the shards to hash are compacted into a device list
     // first (N-f of N in the bench: a third fewer SHA rows than hashing all N).
-    // RBC_VERIFY_COMPACT=0 hashes every row and masks the verdict instead.
-    static const int compact_env = [] {
-        const char *e = getenv("RBC_VERIFY_COMPACT");
-        return e ? atoi(e) : 1;
-    }();
-    if (present && compact_env && c->n <= 256) {
+    if (present && c->n <= 256) {
         uint32_t *vl = nullptr, *vc = nullptr;
         {
             std::lock_guard<std::mutex> lk(c->mu);
@@ -426,11 +373,11 @@ int stage_verify(rbc_ctx *c, hipStream_t st, int count, const uint8_t *shards, u
             vc = vl + (size_t)count * c->n;
         }
         RBC_HIP(hipMemsetAsync(vc, 0, 4, st));
-        RBC_HIP(rbc_launch_compact_present(present, c->n, count, valid, vl, vc, st, c->rxv_prio));
+        RBC_HIP(rbc_launch_compact_present(present, c->n, count, valid, vl, vc, st, c->rx_prio));
         a.list = vl;
         a.list_count = vc;
     }
-    if (path_env && (path_pays || path_env == 2) && c->depth >= 1 && c->width <= 256) {
+    if (path_pays && c->depth >= 1 && c->width <= 256) {
         uint8_t *lv = leaves;
         if (!lv) {
             std::lock_guard<std::mutex> lk(c->mu);
@@ -452,7 +399,7 @@ int stage_verify(rbc_ctx *c, hipStream_t st, int count, const uint8_t *shards, u
         p.roots = roots;
         p.present = present;
         p.valid = valid;
-        p.prio = c->rxv_prio;
+        p.prio = c->rx_prio;
         RBC_HIP(rbc_launch_merkle_path(p, st));
         return RBC_OK;
     }
@@ -479,7 +426,7 @@ int ensure_ws(rbc_ctx *c, Ws &w, int count) {
 // and the rows that need hashing are collected in ws_list
 int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shards, uint32_t shard_pitch,
                      const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *valid,
-                     int32_t *status, int compare = 0, uint8_t *values_out = nullptr, uint32_t value_pitch = 0) {
+                     int32_t *status, int compare = 0) {
     int rc = ensure_ws(c, w, count);
     if (rc) return rc;
     if (compare) RBC_HIP(hipMemsetAsync(w.counter.p, 0, 16, st));
@@ -576,8 +523,6 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
             a.list = pa.list;
             a.counter = pa.counter;
         }
-        a.values_out = values_out;  // join fused into the re-encode (it loads every data row anyway)
-        a.value_pitch_out = value_pitch;
         a.prio = c->rx_prio;
         RBC_HIP(rbc_launch_rs_fft(a, st));
     } else if (nr > 0) {
@@ -586,7 +531,7 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
         g.tiles = (int)((shard_pitch + 4095) / 4096);
         g.R = nr;
         g.K = c->k;
-        g.rc = rbc_gf_pick_rc(nr, gf_rcmax());
+        g.rc = rbc_gf_pick_rc(nr, kGfRcMax);
         g.mode = GF_MODE_DECODE;
         g.in = shards;
         g.in_inst_pitch = (uint64_t)c->n * shard_pitch;
@@ -618,77 +563,76 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
     return RBC_OK;
 }
 
-// interpolate phases: 1 = decode (prepare, missing-data GF, FFT re-encode +
-// compare, value join), 2 = rehash (SHA of the regenerated rows), 4 = check
-// (Merkle root recheck + batch digest).  All three (7) is rbc_dev_interpolate;
-// the join then forks onto the aux stream beside the rehash.  8 = fork: a
-// DECODE call runs its join on the aux stream and the same batch's later
-// CHECK call joins it back (rbc_dev_interpolate_phases, RBC_INTERP_FORK).
-constexpr int kPhaseDecode = 1, kPhaseRehash = 2, kPhaseCheck = 4, kPhaseAll = 7, kPhaseFork = 8;
+// On every exit after work was forked onto the aux stream, `st` waits for it,
+// so a failing later launch never leaves the forked outputs unordered with
+// the caller's stream.
+struct JoinBack {
+    Ws &w;
+    hipStream_t st;
+    bool armed = false;
+    ~JoinBack() {
+        if (!armed) return;
+        (void)hipEventRecord(w.ev_join, w.aux);
+        (void)hipStreamWaitEvent(st, w.ev_join, 0);
+    }
+};
 
+int launch_join(rbc_ctx *c, hipStream_t js, int count, const uint8_t *shards, uint32_t shard_pitch,
+                const uint32_t *shard_lens, uint32_t uniform_shard_len, uint8_t *values_out, uint32_t value_pitch,
+                const int32_t *status) {
+    JoinArgs j{};
+    j.count = count;
+    j.k = c->k;
+    j.chunks = value_pitch / 16;
+    j.shards = shards;
+    j.inst_pitch = (uint64_t)c->n * shard_pitch;
+    j.row_pitch = shard_pitch;
+    j.inst_bytes = (uint32_t)((uint64_t)c->n * shard_pitch);
+    j.lens = shard_lens;
+    j.uniform_len = uniform_shard_len;
+    j.values = values_out;
+    j.value_pitch = value_pitch;
+    j.status = status;
+    j.prio = c->rx_prio;
+    RBC_HIP(rbc_launch_join(j, js));
+    return RBC_OK;
+}
+
+// interpolate: decode (prepare, missing-data GF, FFT re-encode + compare),
+// value join, rehash of the regenerated rows, Merkle root recheck + batch
+// digest.  values_out == NULL is the row-view form: no join, the value is the
+// k data rows of `shards` (regenerated in place).  With w.fork the join
+// (HBM-bound) runs on the aux stream beside the rehash (latency-bound, it
+// under-fills the SIMDs) and the digest beside the recheck.
 int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shards, uint32_t shard_pitch,
                       const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *valid, uint8_t *leaves,
                       int leaves_verified, const uint8_t *roots, uint8_t *values_out, uint32_t value_pitch,
-                      uint8_t *digests, int32_t *status, int phases = kPhaseAll) {
-    if (phases & ~(kPhaseAll | kPhaseFork)) return RBC_ERR_INVALID_ARG;
-    const bool fork_req = (phases & kPhaseFork) != 0;
-    phases &= kPhaseAll;
-    if (phases < 1) return RBC_ERR_INVALID_ARG;
-    if (count < 0 || (count > 0 && (!shards || !valid || !leaves || !roots || !values_out || !status)))
+                      uint8_t *digests, int32_t *status) {
+    if (count < 0 || (count > 0 && (!shards || !valid || !leaves || !roots || !status)))
         return RBC_ERR_INVALID_ARG;
-    if (shard_pitch % kAlign || value_pitch % 16) return RBC_ERR_INVALID_ARG;
+    if (shard_pitch % kAlign || (values_out && value_pitch % 16)) return RBC_ERR_INVALID_ARG;
     if (!shard_lens && (uniform_shard_len == 0 || uniform_shard_len > shard_pitch ||
-                        value_pitch < (uint64_t)uniform_shard_len * c->k))
+                        (values_out && value_pitch < (uint64_t)uniform_shard_len * c->k)))
         return RBC_ERR_INVALID_ARG;
     if ((uint64_t)c->n * shard_pitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
     if (count == 0) return RBC_OK;
-    // RBC_FUSE_JOIN=1: rs_fft_kernel<decode> writes the value from the data
-    // rows it loads anyway (saves the join's k*S re-read, but lengthens the
-    // critical path: measured slower at C2 than the join overlapping the
-    // latency-bound regen hashing on the aux stream)
-    static const bool fuse_env = [] {
-        const char *e = getenv("RBC_FUSE_JOIN");
-        return e && atoi(e) != 0;
-    }();
-    const bool fused_join = fuse_env && c->fft && c->n > c->k;
-    // value assembly (HBM-bound) forks onto the aux stream beside the regen
-    // hashing (latency-bound, under-fills the SIMDs); it needs only the
-    // regenerated rows.  values_out is defined where status == 0.
-    // (phased calls: only on request, since the join is then outstanding on
-    // the aux stream until the batch's CHECK call)
-    const bool fork = !fused_join && w.fork && (phases == kPhaseAll || (fork_req && (phases & kPhaseDecode)));
-    if (phases & kPhaseDecode) w.join_pending = fork;
-    if (phases & kPhaseDecode) {
     int rc = stage_regenerate(c, w, st, count, shards, shard_pitch, shard_lens, uniform_shard_len, valid, status,
-                              leaves_verified, fused_join ? values_out : nullptr, value_pitch);
+                              leaves_verified);
     if (rc) return rc;
-    if (!fused_join) {
-    hipStream_t js = st;
-    if (fork) {
-        if (!aux_stream(w)) return RBC_ERR_DEVICE;
-        RBC_HIP(hipEventRecord(w.ev_fork, st));
-        RBC_HIP(hipStreamWaitEvent(w.aux, w.ev_fork, 0));
-        js = w.aux;
+    JoinBack jb{w, st};
+    if (w.fork && (values_out || digests) && !aux_stream(w)) return RBC_ERR_DEVICE;
+    if (values_out) {
+        hipStream_t js = st;
+        if (w.fork) {
+            RBC_HIP(hipEventRecord(w.ev_fork, st));
+            RBC_HIP(hipStreamWaitEvent(w.aux, w.ev_fork, 0));
+            jb.armed = true;
+            js = w.aux;
+        }
+        rc = launch_join(c, js, count, shards, shard_pitch, shard_lens, uniform_shard_len, values_out, value_pitch,
+                         status);
+        if (rc) return rc;
     }
-    {
-        JoinArgs j{};
-        j.count = count;
-        j.k = c->k;
-        j.chunks = value_pitch / 16;
-        j.shards = shards;
-        j.inst_pitch = (uint64_t)c->n * shard_pitch;
-        j.row_pitch = shard_pitch;
-        j.inst_bytes = (uint32_t)((uint64_t)c->n * shard_pitch);
-        j.lens = shard_lens;
-        j.uniform_len = uniform_shard_len;
-        j.values = values_out;
-        j.value_pitch = value_pitch;
-        j.status = status;
-        j.prio = c->rx_prio;
-        RBC_HIP(rbc_launch_join(j, js));
-    }
-    }
-    }  // decode phase
     const int nr = c->n - c->k;
     ShaArgs a{};
     a.count = count;
@@ -712,8 +656,7 @@ int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *sha
     } else {
         a.rows_per_inst = c->n;
     }
-    if ((phases & kPhaseRehash) && a.rows_per_inst > 0) RBC_HIP(rbc_launch_sha_rows(a, false, st));
-    if (phases & kPhaseCheck) {
+    if (a.rows_per_inst > 0) RBC_HIP(rbc_launch_sha_rows(a, false, st));
     MerkleArgs m{};
     m.count = count;
     m.n = c->n;
@@ -726,28 +669,18 @@ int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *sha
     m.status = status;
     m.prio = c->rx_prio;
     // the batch digest (one serial 23-compression chain per instance at C2)
-    // needs only the data leaves: with the fork it runs on the aux stream
-    // beside the root recheck instead of after it
-    static const bool digest_fork = [] {  // RBC_DIGEST_FORK=0: digest after the recheck (A/B)
-        const char *e = getenv("RBC_DIGEST_FORK");
-        return !e || atoi(e) != 0;
-    }();
+    // needs only the data leaves: it runs on the aux stream beside the recheck
     hipStream_t ds = st;
-    if (w.join_pending && digests && digest_fork) {
+    if (w.fork && digests) {
         RBC_HIP(hipEventRecord(w.ev_hashed, st));
         RBC_HIP(hipStreamWaitEvent(w.aux, w.ev_hashed, 0));
+        jb.armed = true;
         ds = w.aux;
     }
     RBC_HIP(rbc_launch_merkle(m, true, st));
     if (digests)
         RBC_HIP(rbc_launch_digest(leaves, (uint64_t)c->n * 32, c->k, status, digests, count, ds, c->rx_prio));
-    }  // check phase
-    if (w.join_pending && (phases & kPhaseCheck)) {  // join back before returning
-        w.join_pending = false;
-        RBC_HIP(hipEventRecord(w.ev_join, w.aux));
-        RBC_HIP(hipStreamWaitEvent(st, w.ev_join, 0));
-    }
-    return RBC_OK;
+    return RBC_OK;  // jb joins the aux stream back
 }
 
 // Pipelined receiver (rbc_dev_receive_step): cur's ECHO verify and prev's
@@ -758,19 +691,25 @@ int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *sha
 int check_rx_batch(rbc_ctx *c, const rbc_rx_batch *b) {
     if (b->count < 0) return RBC_ERR_INVALID_ARG;
     if (b->count == 0) return RBC_OK;
-    if (!b->shards || !b->roots || !b->valid || !b->leaves || !b->values_out || !b->status ||
-        (c->depth > 0 && !b->branches))
+    if (!b->shards || !b->roots || !b->valid || !b->leaves || !b->status || (c->depth > 0 && !b->branches))
         return RBC_ERR_INVALID_ARG;
-    if (b->shard_pitch % kAlign || b->value_pitch % 16) return RBC_ERR_INVALID_ARG;
+    if (b->shard_pitch % kAlign || (b->values_out && b->value_pitch % 16)) return RBC_ERR_INVALID_ARG;
     if (!b->shard_lens && (b->uniform_shard_len == 0 || b->uniform_shard_len > b->shard_pitch ||
-                           b->value_pitch < (uint64_t)b->uniform_shard_len * c->k))
+                           (b->values_out && b->value_pitch < (uint64_t)b->uniform_shard_len * c->k)))
         return RBC_ERR_INVALID_ARG;
     if ((uint64_t)c->n * b->shard_pitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
     return RBC_OK;
 }
 
+// cur and prev are both in flight during a call: no output buffer may be shared
+bool rx_alias(const rbc_rx_batch *a, const rbc_rx_batch *b) {
+    auto same = [](const void *x, const void *y) { return x && x == y; };
+    return same(a->shards, b->shards) || same(a->leaves, b->leaves) || same(a->status, b->status) ||
+           same(a->valid, b->valid) || same(a->values_out, b->values_out) || same(a->digests, b->digests);
+}
+
 int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, const rbc_rx_batch *prev,
-                       hipEvent_t ev_sha) {
+                       const rbc_rx_marks *marks) {
     Ws &w = c->ws;
     int rc;
     if (cur && (rc = check_rx_batch(c, cur))) return rc;
@@ -779,12 +718,12 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
     // prev must be the batch whose decode the previous call left in the workspace
     if (hp != (w.rx_count > 0) || (hp && (prev->count != w.rx_count || prev->shards != w.rx_shards)))
         return RBC_ERR_INVALID_ARG;
-    if (hc && hp && cur->shards == prev->shards) return RBC_ERR_INVALID_ARG;  // one batch in both roles
+    if (hc && hp && rx_alias(cur, prev)) return RBC_ERR_INVALID_ARG;
     if (!hc && !hp) return RBC_OK;
     if (!aux_stream(w)) return RBC_ERR_DEVICE;
     const int nr = c->n - c->k;
     ShaArgs v{}, r{};
-    v.prio = c->rxv_prio;  // the launch's wave priority (also when only prev's rows are hashed)
+    v.prio = c->rx_prio;  // the launch's wave priority (also when only prev's rows are hashed)
     bool v_walk = false, v_path = false;
     if (hc) {
         v.count = cur->count;
@@ -807,7 +746,7 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
             RBC_HIP(w.vlist.ensure((size_t)cur->count * c->n * 4 + 64));
             uint32_t *vl = w.vlist.as<uint32_t>(), *vc = vl + (size_t)cur->count * c->n;
             RBC_HIP(hipMemsetAsync(vc, 0, 4, st));
-            RBC_HIP(rbc_launch_compact_present(cur->present, c->n, cur->count, cur->valid, vl, vc, st, c->rxv_prio));
+            RBC_HIP(rbc_launch_compact_present(cur->present, c->n, cur->count, cur->valid, vl, vc, st, c->rx_prio));
             v.list = vl;
             v.list_count = vc;
         }
@@ -845,10 +784,20 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
         p.roots = cur->roots;
         p.present = cur->present;
         p.valid = cur->valid;
-        p.prio = c->rxv_prio;
+        p.prio = c->rx_prio;
         RBC_HIP(rbc_launch_merkle_path(p, st));
     }
-    if (ev_sha) RBC_HIP(hipEventRecord(ev_sha, st));
+    if (marks && marks->hashed) RBC_HIP(hipEventRecord((hipEvent_t)marks->hashed, st));
+    // From here on prev's aux-stream work (its join from the previous call and
+    // its digest) is joined back into `st` on every exit, errors included.
+    struct PrevJoin {
+        Ws &w;
+        hipStream_t st;
+        bool armed = false;
+        ~PrevJoin() {
+            if (armed) (void)hipStreamWaitEvent(st, w.ev_join, 0);
+        }
+    } pj{w, st};
     if (hp) {
         if (prev->digests) {  // beside the recheck, on the aux stream (after prev's join)
             RBC_HIP(hipEventRecord(w.ev_hashed, st));
@@ -857,6 +806,7 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
                                       prev->count, w.aux, c->rx_prio));
         }
         RBC_HIP(hipEventRecord(w.ev_join, w.aux));  // prev's join (+ digest) done
+        pj.armed = true;
         MerkleArgs m{};
         m.count = prev->count;
         m.n = c->n;
@@ -870,33 +820,24 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
         m.prio = c->rx_prio;
         RBC_HIP(rbc_launch_merkle(m, true, st));
     }
-    w.rx_count = 0;
+    w.rx_count = 0;  // prev is complete once this call's work on `st` is; cur is pending only on success
     if (hc) {
+        if (marks && marks->decode_begin) RBC_HIP(hipEventRecord((hipEvent_t)marks->decode_begin, st));
         rc = stage_regenerate(c, w, st, cur->count, cur->shards, cur->shard_pitch, cur->shard_lens,
                               cur->uniform_shard_len, cur->valid, cur->status, 1);
         if (rc) return rc;
-        RBC_HIP(hipEventRecord(w.ev_fork, st));
-        RBC_HIP(hipStreamWaitEvent(w.aux, w.ev_fork, 0));
-        JoinArgs j{};
-        j.count = cur->count;
-        j.k = c->k;
-        j.chunks = cur->value_pitch / 16;
-        j.shards = cur->shards;
-        j.inst_pitch = (uint64_t)c->n * cur->shard_pitch;
-        j.row_pitch = cur->shard_pitch;
-        j.inst_bytes = (uint32_t)((uint64_t)c->n * cur->shard_pitch);
-        j.lens = cur->shard_lens;
-        j.uniform_len = cur->uniform_shard_len;
-        j.values = cur->values_out;
-        j.value_pitch = cur->value_pitch;
-        j.status = cur->status;
-        j.prio = c->rx_prio;
-        RBC_HIP(rbc_launch_join(j, w.aux));
+        if (marks && marks->decoded) RBC_HIP(hipEventRecord((hipEvent_t)marks->decoded, st));
+        if (cur->values_out) {  // the row-view form (values_out NULL) has no join
+            RBC_HIP(hipEventRecord(w.ev_fork, st));
+            RBC_HIP(hipStreamWaitEvent(w.aux, w.ev_fork, 0));
+            rc = launch_join(c, w.aux, cur->count, cur->shards, cur->shard_pitch, cur->shard_lens,
+                             cur->uniform_shard_len, cur->values_out, cur->value_pitch, cur->status);
+            if (rc) return rc;
+        }
         w.rx_count = cur->count;
         w.rx_shards = cur->shards;
     }
-    if (hp) RBC_HIP(hipStreamWaitEvent(st, w.ev_join, 0));
-    return RBC_OK;
+    return RBC_OK;  // pj: `st` waits for prev's join + digest
 }
 
 // klauspost checkShards / shardSize (reedsolomon.go)
@@ -1036,8 +977,6 @@ int rbc_ctx_set_wave_priority(rbc_ctx *c, int commit_prio, int receive_prio) {
     if (!c || commit_prio < 0 || commit_prio > 3 || receive_prio < 0 || receive_prio > 3) return RBC_ERR_INVALID_ARG;
     c->tx_prio = commit_prio;
     c->rx_prio = receive_prio;
-    c->rxv_prio = receive_prio;
-    c->enc_prio = getenv("RBC_ENC_PRIO") ? env_prio("RBC_ENC_PRIO") : commit_prio;
     return RBC_OK;
 }
 
@@ -1106,21 +1045,6 @@ int rbc_stream_create_priority(int device, int high, void **stream) {
     hipStream_t s;
     RBC_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, high ? greatest : least));
     *stream = s;
-    return RBC_OK;
-}
-int rbc_stream_create_cu_mask(int device, const uint32_t *mask, int words, void **stream) {
-    if (!stream || !mask || words < 1) return RBC_ERR_INVALID_ARG;
-    RBC_HIP(hipSetDevice(device));
-    hipStream_t s;
-    RBC_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask));
-    *stream = s;
-    return RBC_OK;
-}
-int rbc_device_cu_count(int device, int *cus) {
-    if (!cus) return RBC_ERR_INVALID_ARG;
-    int v = 0;
-    RBC_HIP(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device));
-    *cus = v;
     return RBC_OK;
 }
 int rbc_stream_destroy(void *stream) { RBC_HIP(hipStreamDestroy(as_stream(stream))); return RBC_OK; }
@@ -1206,30 +1130,21 @@ int rbc_dev_interpolate(rbc_ctx *c, void *stream, int count, uint8_t *shards, ui
                         const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *valid,
                         uint8_t *leaves, int leaves_verified, const uint8_t *roots, uint8_t *values_out,
                         uint32_t value_pitch, uint8_t *digests, int32_t *status) {
-    return rbc_dev_interpolate_phases(c, stream, kPhaseAll, count, shards, shard_pitch, shard_lens,
-                                      uniform_shard_len, valid, leaves, leaves_verified, roots, values_out,
-                                      value_pitch, digests, status);
-}
-
-int rbc_dev_receive_step(rbc_ctx *c, void *stream, const rbc_rx_batch *cur, const rbc_rx_batch *prev,
-                         void *hashed_event) {
-    if (!c) return RBC_ERR_INVALID_ARG;
-    std::lock_guard<std::mutex> lk(c->mu);  // shared decode workspace
-    RBC_HIP(hipSetDevice(c->device));
-    return stage_receive_step(c, as_stream(stream), cur, prev, reinterpret_cast<hipEvent_t>(hashed_event));
-}
-
-int rbc_dev_interpolate_phases(rbc_ctx *c, void *stream, int phases, int count, uint8_t *shards,
-                               uint32_t shard_pitch, const uint32_t *shard_lens, uint32_t uniform_shard_len,
-                               const uint8_t *valid, uint8_t *leaves, int leaves_verified, const uint8_t *roots,
-                               uint8_t *values_out, uint32_t value_pitch, uint8_t *digests, int32_t *status) {
     if (!c) return RBC_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(c->mu);  // shared decode workspace
     // the workspace holds a receive-step batch's regen list until its next call
     if (c->ws.rx_count > 0) return RBC_ERR_INVALID_ARG;
     RBC_HIP(hipSetDevice(c->device));
     return stage_interpolate(c, c->ws, as_stream(stream), count, shards, shard_pitch, shard_lens, uniform_shard_len,
-                             valid, leaves, leaves_verified, roots, values_out, value_pitch, digests, status, phases);
+                             valid, leaves, leaves_verified, roots, values_out, value_pitch, digests, status);
+}
+
+int rbc_dev_receive_step(rbc_ctx *c, void *stream, const rbc_rx_batch *cur, const rbc_rx_batch *prev,
+                         const rbc_rx_marks *marks) {
+    if (!c) return RBC_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);  // shared decode workspace
+    RBC_HIP(hipSetDevice(c->device));
+    return stage_receive_step(c, as_stream(stream), cur, prev, marks);
 }
 
 size_t rbc_val_message_size(int n, uint32_t shard_len, uint32_t index, int type) {
@@ -1313,7 +1228,7 @@ void flush_d2h(Slot &s) {
 }
 
 // Free slot for the next submission: create one while fewer than
-// host_slots() exist, else reuse an idle one, else retire the oldest
+// kHostSlots exist, else reuse an idle one, else retire the oldest
 // in-flight submission (its status is kept until the caller waits on it).
 int retire(rbc_ctx *c, Slot &s) {
     int st = RBC_OK;
@@ -1330,7 +1245,7 @@ int retire(rbc_ctx *c, Slot &s) {
 Slot *acquire_slot(rbc_ctx *c) {
     for (auto &sl : c->slots)
         if (!sl->busy) return sl.get();
-    if ((int)c->slots.size() < host_slots()) {
+    if ((int)c->slots.size() < kHostSlots) {
         auto sl = std::make_unique<Slot>();
         if (hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&sl->done, hipEventDisableTiming) != hipSuccess || !sl->ws.init()) {
@@ -1742,11 +1657,7 @@ int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t s
     // present mask first: the zero-copy gather reads it
     memcpy(i_pr, present, (size_t)count * n);
     RBC_HIP(hipMemcpyAsync(s.d_valid.p, i_pr, (size_t)count * n, hipMemcpyHostToDevice, st));
-    static const bool zc_env = [] {
-        const char *e = getenv("RBC_HOST_ZERO_COPY");
-        return !e || atoi(e) != 0;
-    }();
-    const uint8_t *zc = in_direct && zc_env ? host_zero_copy(shards, ((size_t)count * n - 1) * shard_pitch + Smax)
+    const uint8_t *zc = in_direct ? host_zero_copy(shards, ((size_t)count * n - 1) * shard_pitch + Smax)
                                             : nullptr;
     if (zc) {
         // only the received rows cross PCIe (N-f of N at the bench shape)
@@ -2039,15 +1950,16 @@ int rbc_rs_update(rbc_rs *rs, uint8_t *const *shards, const size_t *lens, int n_
                   const uint8_t *const *new_data, const size_t *new_lens, int n_new) {
     if (!rs || !shards || !lens || !new_data || !new_lens) return RBC_ERR_INVALID_ARG;
     rbc_ctx *c = rs->ctx;
-    if (n_shards < c->n) return RBC_ERR_TOO_FEW_SHARDS;
-    if (n_new < c->k) return RBC_ERR_TOO_FEW_SHARDS;
+    // Go: len(shards) != r.Shards, len(newDatashards) != r.DataShards -> ErrTooFewShards
+    if (n_shards != c->n) return RBC_ERR_TOO_FEW_SHARDS;
+    if (n_new != c->k) return RBC_ERR_TOO_FEW_SHARDS;
     size_t S = 0, S2 = 0;
     int rc = check_shards(lens, n_shards, true, &S);
     if (rc) return rc;
     rc = check_shards(new_lens, n_new, true, &S2);
     if (rc) return rc;
     for (int i = 0; i < n_new; ++i)
-        if (new_lens[i] && (i >= n_shards || !lens[i])) return RBC_ERR_INVALID_INPUT;
+        if (new_lens[i] && !lens[i]) return RBC_ERR_INVALID_INPUT;
     for (int r = c->k; r < c->n; ++r)
         if (!lens[r]) return RBC_ERR_INVALID_INPUT;
     std::vector<int> changed;
@@ -2089,7 +2001,7 @@ int rbc_rs_update(rbc_rs *rs, uint8_t *const *shards, const size_t *lens, int n_
     g.tiles = (int)((pitch + 4095) / 4096);
     g.R = P;
     g.K = K;
-    g.rc = rbc_gf_pick_rc(P, gf_rcmax());
+    g.rc = rbc_gf_pick_rc(P, kGfRcMax);
     g.mode = GF_MODE_DECODE;
     g.in = c->d_shards.as<uint8_t>();
     g.in_inst_pitch = rows_bytes;
@@ -2258,6 +2170,13 @@ int rbc_comm_info(rbc_ctx *c, int *nranks, int *rank, int *rccl_version, char *r
     return RBC_OK;
 }
 
+int rbc_device_mem_info(int device, size_t *free_bytes, size_t *total_bytes) {
+    if (!free_bytes || !total_bytes) return RBC_ERR_INVALID_ARG;
+    RBC_HIP(hipSetDevice(device));
+    RBC_HIP(hipMemGetInfo(free_bytes, total_bytes));
+    return RBC_OK;
+}
+
 int rbc_device_pci_bus_id(int device, char *out, int cap) {
     if (!out || cap < 13) return RBC_ERR_INVALID_ARG;
     RBC_HIP(hipDeviceGetPCIBusId(out, cap, device));
@@ -2320,6 +2239,22 @@ int rbc_dev_count_mismatch(int device, void *stream, const uint8_t *a, uint64_t 
     hipStream_t st = as_stream(stream);
     RBC_HIP(hipMemsetAsync(mismatch_dev, 0, sizeof(uint32_t), st));
     RBC_HIP(rbc_launch_count_mismatch(a, a_pitch, b, b_pitch, rows, len, mismatch_dev, st));
+    return RBC_OK;
+}
+
+int rbc_dev_count_mismatch_rows(int device, void *stream, const uint8_t *shards, uint64_t inst_pitch,
+                                uint32_t row_pitch, int k, uint32_t shard_len, const uint8_t *values,
+                                uint64_t value_pitch, uint32_t value_len, uint64_t count, uint32_t *mismatch_dev) {
+    if (!mismatch_dev || k <= 0 || (count && (!shards || !values))) return RBC_ERR_INVALID_ARG;
+    if (row_pitch % 16 || inst_pitch % 16 || (uintptr_t)shards % 16 || shard_len > row_pitch ||
+        value_pitch < (uint64_t)k * shard_len + 16 || value_pitch > 0x7fffffffULL ||
+        value_len > (uint64_t)k * shard_len || (uint64_t)k * row_pitch > inst_pitch)
+        return RBC_ERR_INVALID_ARG;
+    RBC_HIP(hipSetDevice(device));
+    hipStream_t st = as_stream(stream);
+    RBC_HIP(hipMemsetAsync(mismatch_dev, 0, sizeof(uint32_t), st));
+    RBC_HIP(rbc_launch_count_mismatch_rows(shards, inst_pitch, row_pitch, k, shard_len, values, value_pitch, value_len,
+                                           count, mismatch_dev, st));
     return RBC_OK;
 }
 

@@ -166,10 +166,6 @@ struct FftArgs {
     uint32_t *flags;           // [I][n]
     uint32_t *list;
     uint32_t *counter;
-    // decode: interpolate's value (data rows 0..k-1 concatenated, k*S bytes)
-    // written straight from the loaded data rows (nullable)
-    uint8_t *values_out;
-    uint32_t value_pitch_out;
     int prio;                  // wave issue priority 0..3 (set_wave_prio)
 };
 
@@ -219,3 +215,6 @@ hipError_t rbc_launch_gather_present(const uint8_t *host, uint64_t hpitch, uint3
                                      uint8_t *dev, uint32_t dpitch, uint32_t rows, hipStream_t st);
 hipError_t rbc_launch_count_mismatch(const uint8_t *a, uint64_t a_pitch, const uint8_t *b, uint64_t b_pitch,
                                      uint64_t rows, uint64_t len, uint32_t *counter, hipStream_t st);
+hipError_t rbc_launch_count_mismatch_rows(const uint8_t *shards, uint64_t inst_pitch, uint32_t row_pitch, int k,
+                                          uint32_t S, const uint8_t *values, uint64_t value_pitch, uint32_t B,
+                                          uint64_t count, uint32_t *counter, hipStream_t st);

@@ -1303,6 +1303,33 @@ __global__ __launch_bounds__(256) void count_mismatch_kernel(const uint8_t *a, u
     if (bad) atomicAdd(counter, bad);
 }
 
+// The row-view value check (interpolate with values_out == NULL leaves the
+// value as the k data rows of the shard set): count the 16-byte chunks of data
+// row j of each instance whose first min(16, S - 16q) bytes differ from the
+// value bytes at j*S + 16q, where value bytes at or past B compare as zero
+// (klauspost Split's pad).  The value side is read unaligned (gfx950 buffer
+// loads take any byte offset).
+__global__ __launch_bounds__(256) void count_mismatch_rows_kernel(const uint8_t *shards, uint64_t inst_pitch,
+                                                                  uint32_t row_pitch, int k, uint32_t S,
+                                                                  const uint8_t *values, uint64_t value_pitch,
+                                                                  uint32_t B, uint64_t count, uint32_t *counter) {
+    const uint64_t chunks = (S + 15) / 16, per_inst = (uint64_t)k * chunks, total = count * per_inst;
+    uint32_t bad = 0;
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < total;
+         c += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = c / per_inst, rem = c - i * per_inst, j = rem / chunks, q = rem - j * chunks;
+        uint4 x = *reinterpret_cast<const uint4 *>(shards + i * inst_pitch + j * row_pitch + 16 * q);
+        const uint32_t off = (uint32_t)(j * S + 16 * q);
+        uint4 y = bload16(make_rsrc(values + i * value_pitch, (uint32_t)value_pitch), off);
+        const int nrow = (int)min((uint64_t)16, S - 16 * q);
+        const int nval = min(nrow, (int)B - (int)off);
+        x = mask16(x, nrow);
+        y = mask16(y, nval);
+        bad += (x.x != y.x || x.y != y.y || x.z != y.z || x.w != y.w) ? 1u : 0u;
+    }
+    if (bad) atomicAdd(counter, bad);
+}
+
 // Host batch API, receiver side: move only the PRESENT shard rows of a pinned
 // caller batch into the device rows, reading the host memory directly over
 // PCIe (zero-copy; measured at the DMA engine's rate, tools/probes/
@@ -1372,11 +1399,7 @@ hipError_t rbc_launch_gather_present(const uint8_t *host, uint64_t hpitch, uint3
                                      uint8_t *dev, uint32_t dpitch, uint32_t rows, hipStream_t st) {
     if (rows == 0) return hipSuccess;
     if (dpitch % 16 || S > dpitch) return hipErrorInvalidValue;
-    static const uint32_t blocks_env = [] {
-        const char *e = getenv("RBC_GATHER_BLOCKS");
-        return e ? (uint32_t)atoi(e) : 64u;
-    }();
-    const uint32_t blocks = blocks_env ? std::min(rows, blocks_env) : rows;
+    const uint32_t blocks = std::min(rows, 64u);  // a few blocks per CU keep enough PCIe reads in flight
     hipLaunchKernelGGL(gather_present_kernel, dim3(blocks), dim3(256), 0, st, host, hpitch, S, present, dev, dpitch,
                        rows);
     return hipGetLastError();
@@ -1391,6 +1414,18 @@ hipError_t rbc_launch_count_mismatch(const uint8_t *a, uint64_t a_pitch, const u
                        counter);
     return hipGetLastError();
 }
+hipError_t rbc_launch_count_mismatch_rows(const uint8_t *shards, uint64_t inst_pitch, uint32_t row_pitch, int k,
+                                          uint32_t S, const uint8_t *values, uint64_t value_pitch, uint32_t B,
+                                          uint64_t count, uint32_t *counter, hipStream_t st) {
+    if (count == 0 || k <= 0 || S == 0) return hipSuccess;
+    if (row_pitch % 16 || inst_pitch % 16 || ((uintptr_t)shards % 16) || S > row_pitch ||
+        value_pitch < (uint64_t)k * S + 16 || value_pitch > 0x7fffffffull || B > (uint64_t)k * S)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(count_mismatch_rows_kernel, dim3(8192), dim3(256), 0, st, shards, inst_pitch, row_pitch, k, S,
+                       values, value_pitch, B, count, counter);
+    return hipGetLastError();
+}
+
 template <int RC, int TPB = 256>
 static hipError_t launch_gf_rc(const GfArgs &a, hipStream_t st) {
     const int KP = (a.K + 1) & ~1;
@@ -1458,18 +1493,10 @@ hipError_t rbc_launch_sha_rows(const ShaArgs &a, bool verify, hipStream_t st) {
     // plentiful -- C4 verify 5.47 -> 4.51 ms (4 M rows) -- and loses wherever
     // the leaf hashing streams HBM at ~1 wave per SIMD (C2 leaves 1.93 -> 2.13,
     // C2 verify 1.99 -> 2.18, C4 leaves 2.15 -> 2.38): it halves the waves
-    // that hide load latency.  RBC_SHA_ROWS: 1 never, 2 leaves+verify,
-    // 3 (default) verify only, from 4 waves per SIMD of one-row work.
-    static const int rows_env = [] {
-        const char *e = getenv("RBC_SHA_ROWS");
-        return e ? atoi(e) : 3;
-    }();
-    static const int tpb2 = [] {
-        const char *e = getenv("RBC_SHA2_TPB");
-        return e ? atoi(e) : 256;
-    }();
-    const bool two = (rows_env == 2 || (rows_env == 3 && verify)) && !a.list && !a.per_message &&
-                     a.rows_per_inst % 2 == 0 && (!verify || a.n % 2 == 0) &&
+    // that hide load latency.  So: verify only, from 4 waves per SIMD of
+    // one-row work.
+    constexpr int tpb2 = 256;
+    const bool two = verify && !a.list && !a.per_message && a.rows_per_inst % 2 == 0 && a.n % 2 == 0 &&
                      total >= 4L * 64 * 1024;
     if (two) {
         dim3 g2((unsigned)((total / 2 + tpb2 - 1) / tpb2));
@@ -1494,12 +1521,8 @@ hipError_t rbc_launch_sha_rx(const ShaArgs &v, const ShaArgs &r, bool v_walk, hi
     if ((v.count > 0 && (!v.rows || (v_walk && (!v.valid || !v.roots)))) || (r.count > 0 && (!r.list || !r.list_count)))
         return hipErrorInvalidValue;
     // one-wave blocks: 4.78-4.82 ms per C2 receive step against 5.03 with
-    // 256-thread blocks (tools/gpu_r02tpb.sh); RBC_RX_TPB overrides
-    static const int tpb = [] {
-        const char *e = getenv("RBC_RX_TPB");
-        const int x = e ? atoi(e) : 64;
-        return (x == 128 || x == 256) ? x : 64;
-    }();
+    // 256-thread blocks (tools/gpu_r02tpb.sh)
+    constexpr int tpb = 64;
     hipLaunchKernelGGL(sha_rx_kernel, dim3((unsigned)((total + tpb - 1) / tpb)), dim3(tpb), 0, st, v, r, v_walk ? 1 : 0);
     return hipGetLastError();
 }

@@ -349,25 +349,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void rs
         });
     } else {
         lch::sfor<0, K>([&](auto J) { v[decltype(J)::value] = row_load(decltype(J)::value); });
-        if (a.values_out) {
-            // interpolate's value = data rows concatenated (k*S bytes, pad
-            // kept): each lane writes its dword of every data row at j*S+off
-            // (unaligned stores are fine on gfx950); the lane holding a
-            // row's last, partial dword writes only the bytes below S
-            uint8_t *val = a.values_out + (size_t)inst * a.value_pitch_out;
-            const auto ro = __builtin_amdgcn_make_buffer_rsrc(val, (short)0, (int)a.value_pitch_out, 0x00020000);
-            const int tail = (int)S - (int)off;  // valid bytes of this lane's dword
-            lch::sfor<0, K>([&](auto J) {
-                constexpr int j = decltype(J)::value;
-                const int base = j * (int)S;
-                if (tail >= 4) {
-                    __builtin_amdgcn_raw_buffer_store_b32(v[j], ro, (int)off, base, 0);
-                } else if (tail > 0) {
-                    for (int b = 0; b < tail; ++b)
-                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v[j] >> (8 * b)), ro, (int)off + b, base, 0);
-                }
-            });
-        }
     }
 
     lch::solve<LOGW, 0, 0, K>(v);

@@ -34,10 +34,11 @@ def _ptr(a: np.ndarray) -> c_void_p:
     return c_void_p(a.ctypes.data)
 
 
-def cu_count(device: int = 0) -> int:
-    v = c_int(0)
-    check(lib.rbc_device_cu_count(device, byref(v)), "rbc_device_cu_count")
-    return v.value
+def mem_info(device: int = 0) -> tuple:
+    """(free, total) device memory in bytes (hipMemGetInfo)."""
+    free, total = c_size_t(0), c_size_t(0)
+    check(lib.rbc_device_mem_info(device, byref(free), byref(total)), "rbc_device_mem_info")
+    return free.value, total.value
 
 
 def pci_bus_id(device: int) -> str:
@@ -57,6 +58,15 @@ def count_mismatch(device: int, stream, a, a_pitch: int, b, b_pitch: int, rows: 
     their first `length` bytes (read it after the stream completes)."""
     check(lib.rbc_dev_count_mismatch(device, _dv(stream), _dv(a), a_pitch, _dv(b), b_pitch, rows, length,
                                      _dv(counter)), "rbc_dev_count_mismatch")
+
+
+def count_mismatch_rows(device: int, stream, shards, inst_pitch: int, row_pitch: int, k: int, shard_len: int,
+                        values, value_pitch: int, value_len: int, count: int, counter) -> None:
+    """Device counter <- 16-byte chunks where the k data rows of each instance
+    (the row-view value of interpolate) differ from its value bytes."""
+    check(lib.rbc_dev_count_mismatch_rows(device, _dv(stream), _dv(shards), inst_pitch, row_pitch, k, shard_len,
+                                          _dv(values), value_pitch, value_len, count, _dv(counter)),
+          "rbc_dev_count_mismatch_rows")
 
 
 def _bytes_array(x) -> np.ndarray:
@@ -108,18 +118,11 @@ class DeviceBuffer:
 
 
 class Stream:
-    def __init__(self, device: int = 0, priority: Optional[str] = None, cu_mask: Optional[Sequence[int]] = None):
+    def __init__(self, device: int = 0, priority: Optional[str] = None):
         """priority None: default stream priority; "high" / "low": the device's
-        greatest / least (rbc_stream_create_priority).  cu_mask: the CU ids
-        this stream's kernels may run on (rbc_stream_create_cu_mask)."""
+        greatest / least (rbc_stream_create_priority)."""
         p = c_void_p()
-        if cu_mask is not None:
-            words = np.zeros((max(cu_mask) // 32) + 1, dtype=np.uint32)
-            for cu in cu_mask:
-                words[cu // 32] |= np.uint32(1 << (cu % 32))
-            check(lib.rbc_stream_create_cu_mask(device, _ptr(words), len(words), byref(p)),
-                  "rbc_stream_create_cu_mask")
-        elif priority is None:
+        if priority is None:
             check(lib.rbc_stream_create(device, byref(p)), "rbc_stream_create")
         else:
             check(lib.rbc_stream_create_priority(device, 1 if priority == "high" else 0, byref(p)),
@@ -444,15 +447,6 @@ class Context:
                                       _dv(values_out), value_pitch, _dv(digests), _dv(status)),
               "rbc_dev_interpolate")
 
-    INTERP_DECODE, INTERP_REHASH, INTERP_CHECK, INTERP_FORK = 1, 2, 4, 8
-
-    def dev_interpolate_phases(self, stream, phases, count, shards, shard_pitch, shard_lens, uniform_len, valid,
-                               leaves, leaves_verified, roots, values_out, value_pitch, digests, status):
-        check(lib.rbc_dev_interpolate_phases(self._p, _dv(stream), phases, count, _dv(shards), shard_pitch,
-                                             _dv(shard_lens), uniform_len, _dv(valid), _dv(leaves),
-                                             int(leaves_verified), _dv(roots), _dv(values_out), value_pitch,
-                                             _dv(digests), _dv(status)), "rbc_dev_interpolate_phases")
-
     @staticmethod
     def rx_batch(count, shards, shard_pitch, shard_lens, uniform_len, branches, roots, present, valid, leaves,
                  values_out, value_pitch, digests, status) -> "_lib.RxBatch":
@@ -463,13 +457,17 @@ class Context:
         return _lib.RxBatch(count, v(shards), shard_pitch, v(shard_lens), uniform_len, v(branches), v(roots),
                             v(present), v(valid), v(leaves), v(values_out), value_pitch, v(digests), v(status))
 
-    def dev_receive_step(self, stream, cur=None, prev=None, hashed_event=None) -> None:
+    def dev_receive_step(self, stream, cur=None, prev=None, hashed=None, decode_begin=None, decoded=None) -> None:
         """Pipelined receiver: verify(cur) + rehash(prev) in one SHA launch,
-        prev's recheck + digest, cur's decode (rbc_dev_receive_step);
-        hashed_event (an Event) is recorded right after the hashing launch."""
+        prev's recheck + digest, cur's decode (rbc_dev_receive_step).  hashed /
+        decode_begin / decoded (Events, optional) are recorded after the
+        hashing launch, before cur's decode and after it (rbc_rx_marks)."""
+        marks = None
+        if hashed is not None or decode_begin is not None or decoded is not None:
+            ev = lambda e: e.ptr.value if e is not None else None  # noqa: E731
+            marks = ctypes.byref(_lib.RxMarks(ev(hashed), ev(decode_begin), ev(decoded)))
         check(lib.rbc_dev_receive_step(self._p, _dv(stream), ctypes.byref(cur) if cur is not None else None,
-                                       ctypes.byref(prev) if prev is not None else None,
-                                       hashed_event.ptr if hashed_event is not None else None),
+                                       ctypes.byref(prev) if prev is not None else None, marks),
               "rbc_dev_receive_step")
 
     def dev_marshal_val(self, stream, count, msg_type, shards, shard_pitch, shard_lens, uniform_len, branches,

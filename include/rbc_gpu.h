@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define RBC_ABI_VERSION 2
+#define RBC_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------- */
 #define RBC_OK 0
@@ -87,7 +87,7 @@ int rbc_ctx_codec(const rbc_ctx *ctx, int *codec); /* effective: MATRIX or FFT *
  * context's commit-side kernels (encode, leaf hashing, tree build) and
  * receive-side kernels (ECHO verify, interpolate).  Only matters when both
  * sides run concurrently on two streams; results are identical either way.
- * Defaults: RBC_TX_PRIO / RBC_RX_PRIO from the environment, else 0. */
+ * Default 0 / 0. */
 int rbc_ctx_set_wave_priority(rbc_ctx *ctx, int commit_prio, int receive_prio);
 
 /* ---- device memory / streams / events (so a host runtime needs no other
@@ -103,11 +103,6 @@ int rbc_stream_create(int device, void **stream);
 /* high != 0: the device's greatest stream priority (its waves are dispatched
  * ahead of normal-priority streams' when both have work queued), else the least. */
 int rbc_stream_create_priority(int device, int high, void **stream);
-/* A stream whose kernels run only on the CUs set in mask (bit i of word i/32 =
- * CU i, `words` 32-bit words; hipExtStreamCreateWithCUMask): lets two
- * concurrent pipeline stages own disjoint CUs instead of sharing every CU. */
-int rbc_stream_create_cu_mask(int device, const uint32_t *mask, int words, void **stream);
-int rbc_device_cu_count(int device, int *cus);
 int rbc_stream_destroy(void *stream);
 int rbc_stream_sync(void *stream);
 int rbc_event_create(void **event);
@@ -117,6 +112,9 @@ int rbc_event_elapsed_ms(void *start, void *stop, float *ms);
 /* Make later work on `stream` wait for `event` (cross-stream pipelining). */
 int rbc_stream_wait_event(void *stream, void *event);
 int rbc_device_sync(int device);
+/* hipMemGetInfo: free and total device memory in bytes (a host runtime sizes
+ * its batches and in-flight buffer sets from it). */
+int rbc_device_mem_info(int device, size_t *free_bytes, size_t *total_bytes);
 
 /* ---- device-resident batch stages -----------------------------------------
  * All buffers are device memory laid out per DESIGN.md section 4; `stream` is a
@@ -162,33 +160,15 @@ int rbc_dev_verify(rbc_ctx *ctx, void *stream, int count, const uint8_t *shards,
  * defined only where status[i] == RBC_OK).
  * status[i]: RBC_OK, RBC_ERR_TOO_FEW_SHARDS or RBC_ERR_ROOT_MISMATCH.
  * leaves_verified != 0: `leaves` already holds SHA-256 of the valid shards
- * (rbc_dev_verify output) and only regenerated rows are hashed; 0: all rows. */
+ * (rbc_dev_verify output) and only regenerated rows are hashed; 0: all rows.
+ * values_out == NULL (value_pitch ignored) is the row view: no value is
+ * assembled, and the value is the k data rows shards[i][0..k-1][0..S_i) as
+ * regenerated in place (a caller that copies per shard anyway -- the cgo
+ * side -- saves the k*S_i read + write of the join). */
 int rbc_dev_interpolate(rbc_ctx *ctx, void *stream, int count, uint8_t *shards, uint32_t shard_pitch,
                         const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *valid,
                         uint8_t *leaves, int leaves_verified, const uint8_t *roots, uint8_t *values_out,
                         uint32_t value_pitch, uint8_t *digests, int32_t *status);
-/* The same interpolate split into its three phases, for schedulers that
- * interleave batches (bench.py --pipeline 3 runs every SHA phase of three
- * batches together): phases is a mask of RBC_INTERP_DECODE (decode_prepare,
- * missing-data GF, FFT re-encode + compare of the valid-but-unused rows, value
- * join), RBC_INTERP_REHASH (SHA-256 of the regenerated rows) and
- * RBC_INTERP_CHECK (Merkle root recheck + batch digest).  A batch's phases
- * run in that order; between its DECODE and REHASH no other DECODE may run on
- * this context (they share its decode workspace).  status / values_out /
- * leaves are per batch and must stay untouched by other batches in between. */
-#define RBC_INTERP_DECODE 1
-#define RBC_INTERP_REHASH 2
-#define RBC_INTERP_CHECK 4
-/* RBC_INTERP_FORK (with DECODE): the value join runs on the context's aux
- * stream beside the batch's REHASH, and the batch's CHECK call joins it back
- * (values_out is complete when the CHECK work on `stream` is); no other
- * DECODE may run on this context in between.  rbc_dev_interpolate forks the
- * same way inside one call. */
-#define RBC_INTERP_FORK 8
-int rbc_dev_interpolate_phases(rbc_ctx *ctx, void *stream, int phases, int count, uint8_t *shards,
-                               uint32_t shard_pitch, const uint32_t *shard_lens, uint32_t uniform_shard_len,
-                               const uint8_t *valid, uint8_t *leaves, int leaves_verified, const uint8_t *roots,
-                               uint8_t *values_out, uint32_t value_pitch, uint8_t *digests, int32_t *status);
 /* Pipelined receiver, one call per batch:
  * rbc_dev_receive_step(ctx, stream, cur, prev) hashes the received ECHO
  * shards of `cur` (validateMessage, rbc/rbc.go:92-95) AND the rows
@@ -206,7 +186,11 @@ int rbc_dev_interpolate_phases(rbc_ctx *ctx, void *stream, int phases, int count
  * work is done.  While a batch is pending, rbc_dev_interpolate(_phases) on
  * the same context returns RBC_ERR_INVALID_ARG (they share its decode
  * workspace).  All pointers are device memory; present may be NULL (all
- * received). */
+ * received).  cur and prev may share no output buffer (shards, valid, leaves,
+ * status, values_out, digests): RBC_ERR_INVALID_ARG.  A call rejected by its
+ * argument checks enqueues nothing (prev stays pending); an error after
+ * prev's work was enqueued still completes prev once the call's work on
+ * `stream` is, and cur is then not pending (the next call passes prev = NULL). */
 typedef struct rbc_rx_batch {
     int count;
     uint8_t *shards;             /* [count][n][shard_pitch], regenerated in place */
@@ -218,15 +202,22 @@ typedef struct rbc_rx_batch {
     const uint8_t *present;      /* [count][n] received ECHOs (nullable) */
     uint8_t *valid;              /* [count][n] out */
     uint8_t *leaves;             /* [count][n][32] out (own buffer per batch in flight) */
-    uint8_t *values_out;         /* [count][value_pitch] out */
+    uint8_t *values_out;         /* [count][value_pitch] out; NULL: row view (rbc_dev_interpolate) */
     uint32_t value_pitch;
     uint8_t *digests;            /* [count][32] out (nullable) */
     int32_t *status;             /* [count] out */
 } rbc_rx_batch;
-/* hashed_event (nullable, rbc_event_create): recorded on `stream` right after
- * the hashing launch (and cur's shared-path walk), so a caller can time it. */
+/* Timing marks (each nullable, rbc_event_create events) recorded on `stream`:
+ * hashed after the hashing launch (and cur's shared-path walk), decode_begin
+ * after prev's recheck, decoded after cur's decode (prepare, missing-data GF,
+ * FFT re-encode + compare), so a caller can time each part live. */
+typedef struct rbc_rx_marks {
+    void *hashed;
+    void *decode_begin;
+    void *decoded;
+} rbc_rx_marks;
 int rbc_dev_receive_step(rbc_ctx *ctx, void *stream, const rbc_rx_batch *cur, const rbc_rx_batch *prev,
-                         void *hashed_event);
+                         const rbc_rx_marks *marks);
 /* Synthetic Byzantine input for tests/bench: shards[i][corrupt[i]][0] ^= 0x5a
  * for every i with corrupt[i] >= 0 (corrupt: device int32[count]). */
 int rbc_dev_inject_faults(rbc_ctx *ctx, void *stream, int count, uint8_t *shards, uint32_t shard_pitch,
@@ -311,9 +302,10 @@ int rbc_rs_reconstruct_data(rbc_rs *rs, uint8_t *const *shards, size_t *lens, in
 /* Split: out receives n*per bytes (shard i at i*per); *per_shard = per. */
 int rbc_rs_split(rbc_rs *rs, const uint8_t *data, size_t len, uint8_t *out, size_t out_cap, size_t *per_shard);
 /* Update(shards, newDatashards): parity shards += M[k+r][c] * (old_c ^ new_c)
- * for every changed data shard c (new_lens[c] != 0, first k entries used;
- * n_new >= k).  As in Go, shards[c] is left holding old_c ^ new_c.  Errors in
- * Go's order: ErrTooFewShards (n_shards < k+p or n_new < k), checkShards on
+ * for every changed data shard c (new_lens[c] != 0).  As in Go, shards[c] is
+ * left holding old_c ^ new_c.  Errors in Go's order: ErrTooFewShards
+ * (n_shards != k+p or n_new != k: len(shards) != r.Shards,
+ * len(newDatashards) != r.DataShards), checkShards on
  * both sets, ErrInvalidInput (a changed shard whose old shard is nil, or a
  * nil parity shard); a new shard of another size is ErrShardSize. */
 int rbc_rs_update(rbc_rs *rs, uint8_t *const *shards, const size_t *lens, int n_shards,
@@ -371,6 +363,14 @@ int rbc_dev_fill_random(int device, void *stream, uint8_t *dst, uint64_t first_r
  * which the first len bytes of rows a[r] and b[r] differ, r < rows. */
 int rbc_dev_count_mismatch(int device, void *stream, const uint8_t *a, uint64_t a_pitch, const uint8_t *b,
                            uint64_t b_pitch, uint64_t rows, uint64_t len, uint32_t *mismatch_dev);
+/* The row-view form: *mismatch_dev = number of 16-byte chunks of data row j
+ * (shards + i*inst_pitch + j*row_pitch, first min(16, S - 16q) bytes) that
+ * differ from value bytes [j*S + 16q, ...) of values + i*value_pitch, where
+ * value bytes at or past value_len compare as zero (the Split pad); i < count,
+ * j < k.  value_pitch >= k*S + 16. */
+int rbc_dev_count_mismatch_rows(int device, void *stream, const uint8_t *shards, uint64_t inst_pitch,
+                                uint32_t row_pitch, int k, uint32_t shard_len, const uint8_t *values,
+                                uint64_t value_pitch, uint32_t value_len, uint64_t count, uint32_t *mismatch_dev);
 
 #ifdef __cplusplus
 }

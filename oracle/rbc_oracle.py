@@ -363,15 +363,16 @@ class Encoder:
     # As in Go, the old data shard in `shards` is left holding old ^ new
     # (sliceXor(in, oldin) writes into oldin).
     def update(self, shards, new_data) -> None:
-        if len(shards) < self.shards:
+        # v1.9.1 reedsolomon.go Update: len(shards) != r.Shards and
+        # len(newDatashards) != r.DataShards are both ErrTooFewShards
+        if len(shards) != self.shards:
             raise ErrTooFewShards("too few shards given")
-        if len(new_data) < self.data_shards:
+        if len(new_data) != self.data_shards:
             raise ErrTooFewShards("too few shards given")
         _check_shards(shards, True)
         _check_shards(new_data, True)
         for i in range(len(new_data)):
-            if new_data[i] is not None and len(new_data[i]) and (
-                    i >= len(shards) or shards[i] is None or len(shards[i]) == 0):
+            if new_data[i] is not None and len(new_data[i]) and (shards[i] is None or len(shards[i]) == 0):
                 raise ErrInvalidInput("invalid input")
         for pi in range(self.data_shards, self.shards):
             if shards[pi] is None or len(shards[pi]) == 0:

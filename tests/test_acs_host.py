@@ -75,8 +75,9 @@ def _rdz_worker(world, rank, q):
     from cleisthenes_amd.rendezvous import Rendezvous
     rdz = Rendezvous(world, rank)  # key from the shared parent process
     got = {
-        "gather": rdz.allgather({"rank": rank, "blob": bytes([rank]) * (rank * 1000 + 1)}),
-        "bcast": rdz.broadcast(b"uid-from-rank0" if rank == 0 else None),
+        "gather": rdz.allgather({"rank": rank, "blob": "x" * (rank * 1000 + 1)}),
+        "raw": rdz.allgather_bytes(bytes([rank]) * (rank * 1000 + 1)),
+        "bcast": rdz.broadcast_bytes(b"uid-from-rank0" if rank == 0 else None),
         "max": rdz.max(float(rank) * 1.5),
         "sum": rdz.sum(rank + 1),
         "all": rdz.all(rank != 1),
@@ -101,6 +102,7 @@ def test_rendezvous_collectives(world):
         g = res[r]
         assert [x["rank"] for x in g["gather"]] == list(range(world))
         assert [len(x["blob"]) for x in g["gather"]] == [q_ * 1000 + 1 for q_ in range(world)]
+        assert g["raw"] == [bytes([q_]) * (q_ * 1000 + 1) for q_ in range(world)]
         assert g["bcast"] == b"uid-from-rank0"
         assert g["max"] == 1.5 * (world - 1)
         assert g["sum"] == world * (world + 1) // 2
@@ -112,3 +114,57 @@ def test_rendezvous_single_rank_is_local():
     rdz = Rendezvous(1, 0)
     assert rdz.allgather(5) == [5] and rdz.max(2.0) == 2.0 and rdz.all(True)
     rdz.barrier()
+
+
+def _rdz_rank0(key, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from cleisthenes_amd.rendezvous import Rendezvous
+    try:
+        rdz = Rendezvous(2, 0, key=key, timeout=5, connect_timeout=20)
+        q.put(("ok", rdz.allgather_bytes(b"r0")))
+    except Exception as e:  # noqa: BLE001
+        q.put(("err", repr(e)))
+
+
+def test_rendezvous_refuses_unauthenticated_peers_and_names_a_vanished_peer(tmp_path):
+    """A connection that does not present the launch's secret is dropped (it
+    cannot claim a rank); the real rank then joins, and a peer that has
+    exited makes the next collective raise at once, naming it."""
+    import socket
+    import struct
+    import time
+    import uuid
+    from cleisthenes_amd import rendezvous as rv
+    key = uuid.uuid4().hex
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rdz_rank0, args=(key, q))
+    p.start()
+    path = os.path.join(rv.private_dir(), key)
+    deadline = time.monotonic() + 60
+    while not os.path.exists(path):
+        assert time.monotonic() < deadline
+        time.sleep(0.05)
+    st = os.stat(rv.private_dir())
+    assert st.st_mode & 0o077 == 0 and os.stat(path).st_mode & 0o077 == 0
+    port = int(open(path).read().split()[0])
+    # an impostor: right rank id, wrong secret -> dropped, the rendezvous goes on
+    imp = socket.create_connection(("127.0.0.1", port))
+    imp.sendall(struct.pack("<i", 1) + b"0" * 64)
+    imp.settimeout(5)
+    assert imp.recv(1) == b""  # closed by rank 0
+    rdz = rv.Rendezvous(2, 1, key=key, timeout=5)
+    assert rdz.allgather_bytes(b"r1") == [b"r0", b"r1"]
+    assert q.get(timeout=30) == ("ok", [b"r0", b"r1"])
+    p.join(timeout=30)
+    # rank 0 is gone: the next collective fails at once with a named peer
+    with pytest.raises(ConnectionError, match="rank 0"):
+        rdz.barrier()
+
+
+def test_rendezvous_never_unpickles():
+    import inspect
+    from cleisthenes_amd import rendezvous as rv
+    src = inspect.getsource(rv)
+    assert "pickle" not in src.replace("nothing is unpickled", "")

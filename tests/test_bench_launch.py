@@ -1,20 +1,30 @@
-"""bench.py's own N-rank launch (no GPU): `python bench.py --gpus N` without
-WORLD_SIZE spawns N ranks with the torch.distributed.run environment before
-touching any GPU, they rendezvous over loopback TCP (no torch), and the first
-failing rank's status is the launcher's exit status."""
+"""The N-rank launch of bench.py, without a GPU: `python bench.py --gpus N`
+without WORLD_SIZE spawns N ranks with the torch.distributed.run environment
+before touching any GPU (cleisthenes_amd.launch.spawn_ranks), they rendezvous
+over loopback TCP (no torch), and the first failing rank's status is the
+launcher's exit status.  A rank that dies or hangs mid-run ends the whole job
+within its deadline, and the surviving ranks name the stage they were in
+(cleisthenes_amd.launch.Watchdog) -- the first multi-rank run on the 8-GPU
+node must fail loudly, not hang."""
+import json
 import os
+import subprocess
 import sys
 import textwrap
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+
+from cleisthenes_amd import launch  # noqa: E402
 
 
 def _script(tmp_path, body):
     p = tmp_path / "rank.py"
     p.write_text(textwrap.dedent(f"""
-        import json, os, sys
+        import json, os, signal, sys, time
         sys.path.insert(0, {ROOT!r})
+        from cleisthenes_amd.launch import Watchdog
         from cleisthenes_amd.rendezvous import Rendezvous
         world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
         assert os.environ["LOCAL_RANK"] == str(rank) and os.environ["MASTER_ADDR"] == "127.0.0.1"
@@ -24,32 +34,106 @@ def _script(tmp_path, body):
     return str(p)
 
 
+def _launcher(tmp_path, script, n, extra_env=None):
+    """Run spawn_ranks in a child process so the ranks' stderr is captured."""
+    p = tmp_path / "launch.py"
+    p.write_text(textwrap.dedent(f"""
+        import sys
+        sys.path.insert(0, {ROOT!r})
+        from cleisthenes_amd.launch import spawn_ranks
+        sys.exit(spawn_ranks({n}, [{str(tmp_path)!r}], {script!r}, grace_s=3))
+    """))
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, str(p)], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, **(extra_env or {})))
+    # the ranks share the stderr pipe: a report (one atomic write) may land
+    # inside another rank's traceback line, so decode from each occurrence
+    dec, reports, pos = json.JSONDecoder(), [], 0
+    while (pos := r.stderr.find('{"watchdog"', pos)) >= 0:
+        obj, end = dec.raw_decode(r.stderr, pos)
+        reports.append(obj)
+        pos = end
+    return r.returncode, time.monotonic() - t0, reports, r.stderr
+
+
 def test_spawn_ranks_rendezvous_and_exit_status(tmp_path):
-    import bench
     out = tmp_path / "out"
     out.mkdir()
     script = _script(tmp_path, """
         ranks = rdz.allgather(rank)
         t = rdz.max(0.5 * rank)
-        with open(os.path.join(out, f"r{rank}.json"), "w") as f:
+        with open(os.path.join(out, "out", f"r{rank}.json"), "w") as f:
             json.dump({"ranks": ranks, "max": t, "world": world, "torch": "torch" in sys.modules}, f)
         rdz.barrier()
     """)
-    assert bench.spawn_ranks(3, [str(out)], script=script) == 0
-    import json
+    assert launch.spawn_ranks(3, [str(tmp_path)], script) == 0
     res = [json.load(open(out / f"r{r}.json")) for r in range(3)]
     assert all(x == {"ranks": [0, 1, 2], "max": 1.0, "world": 3, "torch": False} for x in res)
 
 
 def test_spawn_ranks_propagates_failure(tmp_path):
-    import bench
     script = _script(tmp_path, """
         if rank == 1:
             sys.exit(7)
-        rdz.barrier()  # rank 0 would wait forever: the launcher terminates it
+        rdz.barrier()  # rank 0's peer is gone: it fails too, or the launcher terminates it
     """)
-    rc = bench.spawn_ranks(2, [str(tmp_path)], script=script)
-    assert rc != 0  # 7, or rank 0's own failure when its peer vanished first
+    assert launch.spawn_ranks(2, [str(tmp_path)], script) != 0
+
+
+def test_killed_rank_ends_the_job_and_the_others_name_their_stage(tmp_path):
+    """One rank is SIGKILLed in the middle of the timed loop: the job exits
+    non-zero well within the deadline, and every surviving rank reports the
+    stage it was in (its rendezvous peer vanished, or the launcher terminated
+    it)."""
+    script = _script(tmp_path, """
+        wd = Watchdog(rank, world)
+        with wd.stage("timed loop", 60):
+            for it in range(50):
+                if rank == 1 and it == 3:
+                    os.kill(os.getpid(), signal.SIGKILL)
+                rdz.barrier()
+                time.sleep(0.05)
+    """)
+    rc, secs, reports, err = _launcher(tmp_path, script, 3)
+    assert rc != 0 and secs < 40, (rc, secs, err[-2000:])
+    survivors = {r["rank"] for r in reports}
+    assert survivors == {0, 2}, err[-2000:]
+    assert all(r["stage"] == "timed loop" for r in reports)
+
+
+def test_hung_rank_hits_the_rendezvous_deadline(tmp_path):
+    """A rank that stops answering (alive, but stuck) makes its peers'
+    collective time out after RBC_RDZV_TIMEOUT seconds instead of hanging; the
+    launcher then terminates the stuck rank, whose watchdog thread still
+    reports its stage although its main thread never returns to Python."""
+    script = _script(tmp_path, """
+        import ctypes
+        wd = Watchdog(rank, world)
+        with wd.stage("timed loop", 60):
+            rdz.barrier()
+            if rank == 1:
+                wd.enter("stuck in a device call", 60)
+                ctypes.CDLL(None).sleep(100)  # a C call that never yields to the interpreter
+            rdz.barrier()
+    """)
+    rc, secs, reports, err = _launcher(tmp_path, script, 2, {"RBC_RDZV_TIMEOUT": "3"})
+    assert rc != 0 and secs < 40, (rc, secs, err[-2000:])
+    by_rank = {r["rank"]: r for r in reports}
+    assert by_rank[0]["stage"] == "timed loop" and "TimeoutError" in by_rank[0]["watchdog"], err[-2000:]
+    assert by_rank[1]["stage"] == "stuck in a device call" and "terminated" in by_rank[1]["watchdog"]
+
+
+def test_stage_deadline_exits_with_a_report(tmp_path):
+    script = _script(tmp_path, """
+        import ctypes
+        wd = Watchdog(rank, world)
+        wd.info["pci_bus_id"] = "0000:00:00.0"
+        wd.enter("rccl init", 1.0)
+        ctypes.CDLL(None).sleep(30)
+    """)
+    rc, secs, reports, err = _launcher(tmp_path, script, 1)
+    assert rc == launch.EXIT_DEADLINE and secs < 20, (rc, secs, err[-2000:])
+    assert reports[0]["stage"] == "rccl init" and reports[0]["pci_bus_id"] == "0000:00:00.0"
 
 
 def test_world_must_match_gpus(tmp_path, monkeypatch):
@@ -62,3 +146,23 @@ def test_world_must_match_gpus(tmp_path, monkeypatch):
         assert "WORLD_SIZE=2" in str(e)
     else:
         raise AssertionError("bench accepted WORLD_SIZE != --gpus")
+
+
+def test_hbm_plan_divides_free_memory_by_the_ranks_sharing_the_device():
+    """C3 with 8,192 instances: the pipelined plan (3 shard sets) does not fit
+    one 288 GB GPU and the serial one does; rehearsed as 2 ranks on one
+    device, each rank plans with half the free memory."""
+    import bench
+    n, f, B = 128, 42, 4 << 20
+    k = n - 2 * f
+    S = (B + k - 1) // k
+    sp, vp, op = bench.round_up(S, 128), bench.round_up(k * S + 32, 64), bench.round_up(k * S, 16)
+    free = 280e9
+    plan, need = bench.hbm_plan(8192, n, 7, sp, vp, op, False, 0, free, 1, 0)
+    assert need["pipelined"] > plan["budget_bytes"] >= need["serial"]
+    plan2, need2 = bench.hbm_plan(4096, n, 7, sp, vp, op, False, 0, free, 2, 0)
+    assert plan2["budget_bytes"] == int(free / 2 * 0.97) and need2["serial"] <= plan2["budget_bytes"]
+    assert 2 * need2["serial"] <= free
+    # the row view needs no value buffer: the joined form costs k*S more per instance
+    _, need3 = bench.hbm_plan(8192, n, 7, sp, vp, op, True, 0, free, 1, 0)
+    assert need3["serial"] - need["serial"] == 8192 * op

@@ -1,10 +1,12 @@
-"""bench.py end to end on the GPU at a small batch: every schedule
-(--pipeline 0 serial, 1 two-stream, 2 three-stream, 3 phase-aligned,
-4 split verify, 5 balanced, 6 commit from the receiver's decode, 7 two-stream with
-rbc_dev_receive_step, the default) must pass the bench's own correctness guard (all instances decode, every
-decoded value equals its input, sampled roots / digests equal the C oracle;
-the bench exits 3 otherwise) and print exactly one JSON line with the
-contract keys."""
+"""bench.py end to end on the GPU.  Every run must pass the bench's own
+correctness guard (all instances decode, every decoded value equals its
+input, sampled roots / digests equal the C oracle, gathered records equal
+what each rank holds; the bench exits 3 otherwise) and print exactly one JSON
+line with the contract keys.  Covered: both schedules (0 serial, 7 the
+two-stream default) in both value forms, BASELINE configs[3] at its stated
+size (C3, 8,192 x 4 MiB) on one GPU and partitioned over two ranks, C4 at
+SURVEY section 8d's 16,384 instances, the 1-rank RCCL gather, the 3-rank
+ragged rehearsal and the HBM-plan fallback."""
 import json
 import os
 import subprocess
@@ -14,32 +16,65 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+QUICK = ["--no-cpu-baseline", "--no-pcie", "--oracle-samples", "4"]
 
 
-@pytest.mark.parametrize("pipeline", [0, 1, 2, 3, 4, 5, 6, 7])
-def test_bench_schedules_pass_their_guard(pipeline):
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "3", "--instances", "96",
-           "--pipeline", str(pipeline), "--no-cpu-baseline", "--no-pcie", "--oracle-samples", "4"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0, r.stderr[-3000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
-    assert len(lines) == 1, r.stdout
-    d = json.loads(lines[0])
-    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
-                "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
-        assert key in d, key
-    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["value"] > 0
-    assert d["decoded_ok"] == 96 and d["values_ok"] and d["oracle_sample_ok"] and d["oracle_samples_checked"] == 4
-    assert 0 < d["roofline"]["frac"] < 1 and d["roofline"]["avg_ms"] > 0
-
-
-def _run(args, timeout=300, env=None):
+def _run(args, timeout=300):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
-                       timeout=timeout, env=env)
+                       timeout=timeout)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, r.stdout
     return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("pipeline,join", [(0, False), (7, False), (7, True)])
+def test_bench_schedules_pass_their_guard(pipeline, join):
+    d = _run(["--steps", "3", "--warmup", "3", "--instances", "96", "--pipeline", str(pipeline)]
+             + (["--join"] if join else []) + QUICK)
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "ranks"):
+        assert key in d, key
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["value"] > 0
+    assert d["decoded_ok"] == 96 and d["values_ok"] and d["oracle_sample_ok"] and d["oracle_samples_checked"] == 4
+    assert 0 < d["roofline"]["frac"] < 1 and d["roofline"]["avg_ms"] > 0
+    assert d["config"]["hbm_plan"]["schedule"] == ("pipelined" if pipeline else "serial")
+    assert d["config"]["value_form"].startswith("joined" if join else "row view")
+    if pipeline:
+        rd = d["roofline_decode"]
+        assert rd["avg_ms"] > 0 and 0 < rd["frac"] < 1 and rd["algorithmic_bytes_per_launch"] > 0
+
+
+def test_bench_c3_8192_instances_on_one_gpu():
+    """BASELINE configs[3] at its stated size on one GPU: 8,192 x 4 MiB.  The
+    HBM plan (free device memory) cannot hold the pipeline's three shard sets
+    and runs the serial schedule; every instance decodes."""
+    d = _run(["--config", "c3", "--total-instances", "8192", "--steps", "2", "--warmup", "1"] + QUICK, timeout=600)
+    assert d["decoded_ok"] == 8192 and d["values_ok"] and d["oracle_sample_ok"] and d["oracle_samples_checked"] == 4
+    plan = d["config"]["hbm_plan"]
+    assert plan["schedule"] == "serial" and plan["ranks_sharing_device"] == 1
+    assert plan["need_bytes"]["pipelined"] > plan["budget_bytes"] >= plan["need_bytes"]["serial"]
+    assert d["config"]["instances_total"] == 8192 and d["scaling"] == "strong"
+
+
+def test_bench_c3_8192_partitioned_over_two_ranks():
+    """configs[3]'s partition: 8,192 instances over 2 ranks (4,096 each),
+    rehearsed on this one GPU -- both ranks plan with half the free memory,
+    and the records of every rank are checked through the rendezvous."""
+    d = _run(["--config", "c3", "--total-instances", "8192", "--gpus", "2", "--rehearse-on-one-gpu", "--steps", "2",
+              "--warmup", "1", "--no-isolated"] + QUICK, timeout=900)
+    assert d["n_gpus"] == 2 and d["config"]["instances_per_gpu"] == 4096
+    assert d["decoded_ok"] == 8192 and d["values_ok"] and d["gather_ok"] and d["oracle_sample_ok"]
+    assert d["config"]["hbm_plan"]["ranks_sharing_device"] == 2
+    assert [r["rank"] for r in d["ranks"]] == [0, 1] and all(r["pci_bus_id"] for r in d["ranks"])
+
+
+def test_bench_c4_16384_instances():
+    """C4 (N=256, f=85, 64 KiB) at SURVEY section 8d's 16,384 instances:
+    every instance decodes to its input under the default schedule."""
+    d = _run(["--config", "c4", "--steps", "3", "--warmup", "3", "--no-isolated"] + QUICK)
+    assert d["config"]["instances_per_gpu"] == 16384
+    assert d["decoded_ok"] == 16384 and d["values_ok"] and d["value_mismatch_chunks"] == 0 and d["oracle_sample_ok"]
 
 
 def test_bench_multi_rank_rehearsal_ragged_strong_scaling():
@@ -48,29 +83,26 @@ def test_bench_multi_rank_rehearsal_ragged_strong_scaling():
     every rank's decodes, values, gathered records (through the torch-free
     rendezvous) and oracle samples; the line reports the whole job."""
     d = _run(["--gpus", "3", "--rehearse-on-one-gpu", "--total-instances", "250", "--steps", "3", "--warmup", "3",
-              "--no-cpu-baseline", "--no-pcie", "--no-isolated", "--oracle-samples", "4"])
+              "--no-isolated"] + QUICK)
     assert d["n_gpus"] == 3 and d["scaling"] == "strong"
     assert d["config"]["instances_total"] == 250 and "rehearsal" in d["config"]
     assert d["decoded_ok"] == 250 and d["values_ok"] and d["gather_ok"] and d["oracle_sample_ok"]
+    assert [r["rank"] for r in d["ranks"]] == [0, 1, 2]
 
 
 def test_bench_one_rank_rccl_gather():
     """--force-gather runs the RCCL record all-gather in the timed step on one
     rank: the line names the ROCm 7.2 RCCL that was mapped and the guard
     checks the gathered records against the device results."""
-    d = _run(["--force-gather", "--instances", "64", "--steps", "3", "--warmup", "3", "--no-cpu-baseline",
-              "--no-pcie", "--no-isolated", "--oracle-samples", "4"])
-    assert d["rccl"] is not None and d["rccl"]["nranks"] == 1
+    d = _run(["--force-gather", "--instances", "64", "--steps", "3", "--warmup", "3", "--no-isolated"] + QUICK)
+    assert d["rccl"] is not None and d["rccl"]["nranks"] == 1 and d["ranks"][0]["rccl_nranks"] == 1
     assert "torch" not in d["rccl"]["lib"]
     assert d["decoded_ok"] == 64 and d["values_ok"] and d["gather_ok"]
 
 
 def test_bench_falls_back_to_serial_when_the_shard_sets_do_not_fit():
-    """C3 with all 8,192 instances on one GPU cannot hold the pipeline's shard
-    sets: with an HBM budget below one set the default schedule must fall back
-    to the serial one and still pass its guard."""
-    env = dict(os.environ, RBC_BENCH_HBM_BUDGET="1e6")
-    d = _run(["--instances", "64", "--steps", "3", "--warmup", "2", "--no-cpu-baseline", "--no-pcie",
-              "--oracle-samples", "4"], env=env)
-    assert d["config"]["pipeline"] == "serial"
+    """With an HBM budget below the pipeline's three shard sets the default
+    schedule falls back to the serial one and still passes its guard."""
+    d = _run(["--instances", "64", "--steps", "3", "--warmup", "2", "--hbm-budget", "1.5e9"] + QUICK)
+    assert d["config"]["pipeline"] == "serial" and d["config"]["hbm_plan"]["schedule"] == "serial"
     assert d["decoded_ok"] == 64 and d["values_ok"] and d["oracle_sample_ok"]

@@ -46,6 +46,8 @@ def test_update_argument_checks_follow_go_order(gpu):
     cases = [
         (sh[:4], new, -3),                                                    # ErrTooFewShards
         (sh, new[:2], -3),
+        (sh + [np.ones(S, np.uint8)], new, -3),                               # len(shards) != Shards
+        (sh, new + [None], -3),                                               # len(new) != DataShards
         (sh, [None, None, None], -4),                                         # ErrShardNoData
         ([np.ones(S, np.uint8)] * 4 + [np.ones(S + 1, np.uint8)], new, -5),   # ErrShardSize (shards)
         ([None] + sh[1:], new, -13),                                          # ErrInvalidInput

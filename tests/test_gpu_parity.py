@@ -1236,42 +1236,116 @@ def test_receive_step_pipeline_equals_verify_then_interpolate(gpu, ref, n, f, B,
 
 
 @pytest.mark.parametrize("n,f,B,I", [(128, 42, 1 << 16, 96), (16, 5, 3001, 64), (256, 85, 86 * 40, 48)])
-def test_interpolate_phases_equal_one_shot(gpu, ref, n, f, B, I):
-    """rbc_dev_interpolate_phases (decode, rehash, check as three calls,
-    as --pipeline 3 schedules them) produces exactly the one-shot
-    rbc_dev_interpolate's values, digests, statuses and leaves, corrupted
-    ECHO shards and wrong committed roots included; sampled instances are
-    also checked against the C oracle."""
+def test_row_view_interpolate_equals_joined_value(gpu, ref, n, f, B, I):
+    """interpolate with values_out = NULL (the row view: no join) leaves the
+    same statuses, digests and leaves as the joined form, and its k data rows
+    ARE the joined value (rbc_dev_count_mismatch_rows finds no difference;
+    the host compares them too); wrong committed roots and corrupted ECHOs
+    included.  The receive step's row view gives the same."""
     outs = []
-    for phased in (False, True):
+    for mode in ("joined", "view", "step_view"):
         pl = Pipeline(gpu, n, f, B, I, seed=n + B, corrupt_frac=0.3)
         pl.commit()
         b, c = pl.b, pl.ctx
         c.dev_inject_faults(None, I, b["shards"], pl.spitch, b["corrupt"])
-        c.dev_verify(None, I, b["shards"], pl.spitch, None, pl.S, b["branches"], b["roots"], b["present"],
-                     b["valid"], b["leaves_r"])
         roots = pl.arr("roots", shape=(I, 32)).copy()
-        roots[::7, 0] ^= 0x80  # interpolate's recheck against a wrong root every 7th instance
+        roots[::7, 0] ^= 0x80  # the recheck against a wrong root every 7th instance
         b["roots"].upload(roots)
-        args = (I, b["shards"], pl.spitch, None, pl.S, b["valid"], b["leaves_r"], 1, b["roots"], b["out"],
-                pl.opitch, b["digests"], b["status"])
-        if phased:
-            for ph in (c.INTERP_DECODE, c.INTERP_REHASH, c.INTERP_CHECK):
-                c.dev_interpolate_phases(None, ph, *args)
+        if mode == "step_view":
+            rb = c.rx_batch(I, b["shards"], pl.spitch, None, pl.S, b["branches"], b["roots"], b["present"],
+                            b["valid"], b["leaves_r"], None, 0, b["digests"], b["status"])
+            c.dev_receive_step(None, rb, None)
+            c.dev_receive_step(None, None, rb)
         else:
-            c.dev_interpolate(None, *args)
+            c.dev_verify(None, I, b["shards"], pl.spitch, None, pl.S, b["branches"], b["roots"], b["present"],
+                         b["valid"], b["leaves_r"])
+            c.dev_interpolate(None, I, b["shards"], pl.spitch, None, pl.S, b["valid"], b["leaves_r"], 1, b["roots"],
+                              b["out"] if mode == "joined" else None, pl.opitch if mode == "joined" else 0,
+                              b["digests"], b["status"])
+        cnt = gpu.DeviceBuffer(16)
+        gpu.rbc.count_mismatch_rows(0, None, b["shards"], pl.n * pl.spitch, pl.spitch, pl.k, pl.S, b["values"],
+                                    pl.vpitch, B, I, cnt)
         gpu.rbc.lib.rbc_device_sync(0)
         st = pl.arr("status", np.int32)
         ok = st == 0
-        outs.append((st, pl.arr("out", shape=(I, pl.opitch))[:, : pl.k * pl.S][ok],
-                     pl.arr("digests", shape=(I, 32))[ok], pl.arr("leaves_r", shape=(I, n, 32)), pl))
-    (s0, v0, d0, l0, pl), (s1, v1, d1, l1, _) = outs
-    assert np.array_equal(s0, s1) and set(s0[::7]) == {-8} and (s0[np.arange(I) % 7 != 0] == 0).all()
-    assert np.array_equal(v0, v1) and np.array_equal(d0, d1) and np.array_equal(l0, l1)
-    for i in (1, 2, I - 1):
-        if i % 7 == 0:
-            continue
-        assert bytes(pl.values[i, :B]) == bytes(v1[np.cumsum(s1 == 0)[i] - 1][:B])
+        rows = pl.shards()[:, : pl.k, : pl.S].reshape(I, pl.k * pl.S)
+        outs.append((st, rows[ok], pl.arr("digests", shape=(I, 32))[ok], pl.arr("leaves_r", shape=(I, n, 32))[ok],
+                     pl.arr("out", shape=(I, pl.opitch))[:, : pl.k * pl.S][ok], pl, int(cnt.download(4).view(np.uint32)[0])))
+    (s0, r0, d0, l0, v0, _, mism0), = outs[:1]
+    assert set(s0[::7]) == {-8} and (s0[np.arange(I) % 7 != 0] == 0).all()
+    assert np.array_equal(r0, v0)  # the joined value is the data rows
+    for (s1, r1, d1, l1, _, pl1, mism) in outs:
+        assert np.array_equal(s0, s1) and np.array_equal(r0, r1) and np.array_equal(d0, d1)
+        assert np.array_equal(l0, l1)
+        ok = np.flatnonzero(s1 == 0)
+        assert all(bytes(pl1.values[i, :B]) == bytes(r1[t, :B]) for t, i in enumerate(ok))
+        # the decode ran on every instance (the wrong roots fail only the recheck afterwards),
+        # so every instance's data rows are its input with the Split pad
+        assert mism == 0
+
+
+def test_count_mismatch_rows_finds_single_byte_differences(gpu):
+    """The bench guard's row-view check: a value split into k rows (zero pad
+    past B) compares equal to its rows, and one flipped byte in a data row,
+    in the pad or at the last valid byte is one mismatching chunk."""
+    n, f, B, I = 16, 5, 1001, 6
+    k = n - 2 * f
+    S = (B + k - 1) // k
+    spitch, vpitch = rup(S, 64), rup(k * S + 32, 64)
+    rng = np.random.default_rng(3)
+    values = rng.integers(0, 256, (I, vpitch), dtype=np.uint8)
+    rows = np.zeros((I, n, spitch), np.uint8)
+    for i in range(I):
+        v = np.zeros(k * S, np.uint8)
+        v[:B] = values[i, :B]
+        rows[i, :k, :S] = v.reshape(k, S)
+    for i, (j, x) in {1: (0, 0), 2: (k - 1, S - 1), 3: (3, 17), 5: ((B - 1) // S, (B - 1) % S)}.items():
+        rows[i, j, x] ^= 0x40
+    d_rows, d_vals, cnt = gpu.DeviceBuffer(rows.nbytes), gpu.DeviceBuffer(values.nbytes), gpu.DeviceBuffer(16)
+    d_rows.upload(rows)
+    d_vals.upload(values)
+    gpu.rbc.count_mismatch_rows(0, None, d_rows, n * spitch, spitch, k, S, d_vals, vpitch, B, I, cnt)
+    gpu.rbc.lib.rbc_device_sync(0)
+    assert int(cnt.download(4).view(np.uint32)[0]) == 4
+
+
+def test_receive_step_rejects_aliased_batches(gpu, ref):
+    """cur and prev sharing an output buffer (leaves, status, valid, values,
+    digests) is rejected before any work, as is a cur that fails its argument
+    checks; prev then stays pending and a later call completes it with the
+    statuses, values and digests of verify + interpolate."""
+    n, f, B, I = 16, 5, 2000, 24
+    pls = []
+    for bi in range(2):
+        pl = Pipeline(gpu, n, f, B, I, seed=77 + bi, corrupt_frac=0.3)
+        pl.commit()
+        pl.ctx.dev_inject_faults(None, I, pl.b["shards"], pl.spitch, pl.b["corrupt"])
+        pls.append(pl)
+    rx = gpu.Context(n, f)
+
+    def rb(pl, **over):
+        b = dict(pl.b, **over)
+        return rx.rx_batch(I, b["shards"], pl.spitch, None, pl.S, b["branches"], b["roots"], b["present"], b["valid"],
+                           b["leaves_r"], b["out"], pl.opitch, b["digests"], b["status"])
+    p0 = rb(pls[0])
+    rx.dev_receive_step(None, p0, None)
+    for key in ("leaves_r", "status", "valid", "out", "digests"):
+        with pytest.raises(gpu.RBCError):
+            rx.dev_receive_step(None, rb(pls[1], **{key: pls[0].b[key]}), p0)
+    bad = rb(pls[1])
+    bad.uniform_shard_len = pls[1].spitch + 64  # > shard_pitch: rejected by cur's checks before any launch
+    with pytest.raises(gpu.RBCError):
+        rx.dev_receive_step(None, bad, p0)
+    rx.dev_receive_step(None, None, p0)  # prev still pending: complete it
+    gpu.rbc.lib.rbc_device_sync(0)
+    want = Pipeline(gpu, n, f, B, I, seed=77, corrupt_frac=0.3)
+    want.commit()
+    want.receive()
+    gpu.rbc.lib.rbc_device_sync(0)
+    for name in ("status", "digests", "valid"):
+        assert np.array_equal(want.arr(name), pls[0].arr(name)), name
+    ok = want.arr("status", np.int32) == 0
+    assert np.array_equal(want.arr("out", shape=(I, want.opitch))[ok], pls[0].arr("out", shape=(I, want.opitch))[ok])
 
 
 def test_wave_priority_changes_no_result(gpu, ref):

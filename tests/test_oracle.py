@@ -344,6 +344,10 @@ def test_oracle_update_argument_checks():
         enc.update(sh[:4], new)
     with pytest.raises(orc.ErrTooFewShards):
         enc.update(sh, new[:2])
+    with pytest.raises(orc.ErrTooFewShards):  # Go compares with != (len(shards) != r.Shards)
+        enc.update(sh + [np.ones(S, np.uint8)], new)
+    with pytest.raises(orc.ErrTooFewShards):  # len(newDatashards) != r.DataShards
+        enc.update(sh, new + [None])
     with pytest.raises(orc.ErrShardNoData):
         enc.update(sh, [None, None, None])
     with pytest.raises(orc.ErrShardSize):
