@@ -562,7 +562,11 @@ struct rbc_node {
         ops.push_back(std::move(op));
     }
 
-    // our VAL (own or received) proved our shard: ECHO it to everyone
+    // our VAL (own or received) proved our shard: ECHO it to every other node,
+    // the proposer included, and count our own ECHO here.  HBBFT's "multicast
+    // ECHO" (Miller et al. 2016, Algorithm RBC), not docs/RBC-EN.md:34 ("except
+    // the sender and itself"): without ECHOs the proposer could never decode
+    // (RBC-EN.md:42) and would not deliver its own value
     void on_val(const Request &r) {
         send(-1, RBC_MSG_ECHO,
              json_val((const uint8_t *)r.root.data(), r.root.size(), (const uint8_t *)r.branch.data(),

@@ -17,7 +17,16 @@ What it restates, independently of that C++ (pure Python over
   handleValueRequest / handleEchoRequest / handleReadyRequest, Value,
   Messages):
     - VAL(h, b_i, s_i) from the proposer: validateMessage at our own index,
-      then ECHO(h, b_i, s_i) to every other node (RBC-EN.md:34);
+      then ECHO(h, b_i, s_i) to every other node, the proposer included,
+      and our own ECHO counted locally.  This is the HBBFT paper's rule
+      (Miller et al. 2016, Algorithm RBC: "multicast ECHO(h, b_i, s_i)",
+      i.e. to all parties) and deliberately NOT docs/RBC-EN.md:34, which
+      sends ECHO "to the node except the sender and itself": a proposer that
+      receives no ECHO can never reach step 5 (RBC-EN.md:42, "wait for N-2f
+      ECHO messages and decode"), so it would not deliver its own broadcast
+      and totality fails; and a node that does not count its own shard needs
+      N-f ECHOs from only N-1 peers.  The product does the same
+      (csrc/rbc_node.cpp on_val); DESIGN.md section 5.7 records the deviation;
     - ECHO from node j counts iff validateMessage proves s_j at leaf j
       under h (RBC-EN.md:35); one VAL / ECHO / READY per sender;
     - N-f valid ECHOs for h: interpolate, and on a root match READY(h)
