@@ -6,7 +6,7 @@
 // kernels.hip.  Argument checks and error values follow klauspost/reedsolomon
 // v1.9.1 (reedsolomon.go: New, Split, Encode, Verify, Reconstruct, Join).
 #include <dlfcn.h>
-#include <hip/hip_runtime.h>
+#include <hip/hip_runtime_api.h>
 #include <limits.h>
 #include <rccl/rccl.h>
 #include <stdio.h>
@@ -861,7 +861,10 @@ int host_reconstruct(rbc_ctx *c, uint8_t *const *shards, size_t *lens, int n_sha
     int rc = check_shards(lens, n_shards, true, &S);
     if (rc) return rc;
     int present = 0;
-    for (int i = 0; i < c->n; ++i) present += lens[i] != 0;
+    for (int i = 0; i < c->n; ++i) {
+        if (lens[i] && !shards[i]) return RBC_ERR_INVALID_ARG;  // a present shard needs its bytes
+        present += lens[i] != 0;
+    }
     if (present == c->n) return RBC_OK;
     if (present < c->k) return RBC_ERR_TOO_FEW_SHARDS;
     if (S > 0x7fffffffULL / (size_t)c->n) return RBC_ERR_INVALID_ARG;
@@ -1652,8 +1655,10 @@ int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t s
     const size_t in_stage = in_direct ? 0 : sh_bytes, out_stage = out_direct ? 0 : (size_t)count * vpitch;
     RBC_HIP(s.h_in.ensure(in_stage + (size_t)count * (n + 32 + 4)));
     RBC_HIP(s.h_out.ensure(out_stage + (size_t)count * (32 + 4)));
-    uint8_t *i_sh = s.h_in.as<uint8_t>(), *i_pr = i_sh + in_stage, *i_rt = i_pr + (size_t)count * n;
-    uint32_t *ln = reinterpret_cast<uint32_t *>(i_rt + (size_t)count * 32);
+    // [shard staging][lens u32][roots][present]: the u32 lens stay aligned for any n
+    uint8_t *i_sh = s.h_in.as<uint8_t>();
+    uint32_t *ln = reinterpret_cast<uint32_t *>(i_sh + in_stage);
+    uint8_t *i_rt = reinterpret_cast<uint8_t *>(ln + count), *i_pr = i_rt + (size_t)count * 32;
     // present mask first: the zero-copy gather reads it
     memcpy(i_pr, present, (size_t)count * n);
     RBC_HIP(hipMemcpyAsync(s.d_valid.p, i_pr, (size_t)count * n, hipMemcpyHostToDevice, st));

@@ -1,10 +1,11 @@
 // kernels.h -- argument blocks and launchers of the batched RBC kernels
 // (host side of kernels.hip).  Plain structs passed by value to the kernels.
 #pragma once
-#include <hip/hip_runtime.h>
+#include <hip/hip_runtime_api.h>
 #include <stdint.h>
 
 #include "../../include/rbc_gpu.h"
+#include "host_shared.h"
 
 enum { GF_MODE_ENCODE = 0, GF_MODE_DECODE = 1 };
 
@@ -169,7 +170,6 @@ struct FftArgs {
     int prio;                  // wave issue priority 0..3 (set_wave_prio)
 };
 
-bool rbc_fft_supported(int n, int k);
 // VAL / ECHO marshaling (wire.hip): message (i, j) = pb.Message bytes of
 // the request for shard j of instance i, at out + (i*n + j)*out_pitch.
 struct WireArgs {
@@ -186,7 +186,6 @@ struct WireArgs {
     uint32_t *out_lens;  // [count*n], nullable
 };
 hipError_t rbc_launch_marshal_val(const WireArgs &a, hipStream_t st);
-size_t rbc_val_message_bytes(int n, int depth, uint32_t S, uint32_t index, int type);
 
 hipError_t rbc_launch_rs_fft(const FftArgs &a, hipStream_t st);
 

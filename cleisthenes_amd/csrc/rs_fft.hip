@@ -433,23 +433,6 @@ hipError_t launch_fft(const FftArgs &a, hipStream_t st) {
 
 }  // namespace
 
-// Geometries with a specialised transform: N = 3f+1 (the BFT maximum f) for
-// the benchmark sizes.  Other (N, k) fall back to gf_rows_kernel.
-#define RBC_FFT_GEOMS(X) \
-    X(2, 2, 4)           \
-    X(4, 6, 16)          \
-    X(6, 22, 64)         \
-    X(7, 44, 128)        \
-    X(8, 86, 256)
-
-bool rbc_fft_supported(int n, int k) {
-#define RBC_FFT_SUP(lw, kk, nn) \
-    if (n == nn && k == kk) return true;
-    RBC_FFT_GEOMS(RBC_FFT_SUP)
-#undef RBC_FFT_SUP
-    return false;
-}
-
 hipError_t rbc_launch_rs_fft(const FftArgs &a, hipStream_t st) {
     if (a.count <= 0) return hipSuccess;
     if (a.row_pitch % 4) return hipErrorInvalidValue;

@@ -221,20 +221,4 @@ hipError_t rbc_launch_marshal_val(const WireArgs &a, hipStream_t st) {
     return hipGetLastError();
 }
 
-// Host mirror of layout().total for sizing out_pitch.
-size_t rbc_val_message_bytes(int n, int depth, uint32_t S, uint32_t index, int type) {
-    auto b64 = [](uint64_t x) { return (x + 2) / 3 * 4; };
-    auto vl = [](uint64_t v) {
-        uint64_t l = 1;
-        while (v >= 0x80) {
-            v >>= 7;
-            ++l;
-        }
-        return l;
-    };
-    const bool empty0 = depth > 0 && (int)(index ^ 1u) >= n;
-    const uint64_t br = 32u * (uint64_t)(depth - (empty0 ? 1 : 0));
-    const uint64_t J = br ? 84 + b64(br) + b64(S) : 86 + b64(S);
-    const uint64_t R = 1 + vl(J) + J + (type ? 2 : 0);
-    return (size_t)(1 + vl(R) + R);
-}
+

@@ -12,6 +12,13 @@ ThreadSanitizer and under ASan + UBSan against an oracle-backed stand-in for
 the context's asynchronous batch API (tests/cpp/batcher_race.cpp): client
 threads submit random shard / validate / interpolate requests and complete
 them by wait or poll, every result checked against the C oracle.
+
+The host runtime behind the C ABI (csrc/capi.cpp: argument checks, pinned
+staging and slots, tickets, rbc_acs_*, the reedsolomon.Encoder mirror, the
+receive step's batch checks) is built with ASan + UBSan against a host-memory
+stand-in for HIP, RCCL and the kernel launchers (tests/cpp/hip_stub.cpp: the
+stub kernels touch exactly what the real ones write) and driven with random
+arguments by tests/cpp/capi_fuzz.cpp.
 CPU only; no GPU code is built or run."""
 import os
 import shutil
@@ -79,3 +86,26 @@ def test_batcher_clean_under_sanitizers(tmp_path, san):
     for bad in ("ThreadSanitizer", "AddressSanitizer", "runtime error", "FAIL"):
         assert bad not in r.stderr, r.stderr[-4000:]
     assert r.stdout.rstrip().endswith("ok"), r.stdout
+
+
+def test_capi_host_runtime_clean_under_asan_ubsan(tmp_path):
+    """Random arguments through every host-side entry point of the C ABI;
+    caller buffers are exactly as large as the contract asks, so a read or
+    write past them, or past a buffer the runtime sized itself, is reported."""
+    if not shutil.which("g++"):
+        pytest.skip("g++ not available")
+    exe = str(tmp_path / "capi_fuzz")
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+           "-fno-sanitize-recover=all", "-Wall", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", "-o", exe,
+           os.path.join(CPP, "capi_fuzz.cpp"), os.path.join(CPP, "hip_stub.cpp"),
+           os.path.join(ROOT, "cleisthenes_amd", "csrc", "capi.cpp"), "-ldl", "-lpthread"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0:halt_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    for seed in ("1", "20261017", "77"):
+        r = subprocess.run([exe, "30000", seed], capture_output=True, text=True, timeout=600, env=env)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+        for bad in ("AddressSanitizer", "runtime error", "FAIL"):
+            assert bad not in r.stderr, r.stderr[-4000:]
+        assert r.stdout.startswith("ok"), r.stdout
