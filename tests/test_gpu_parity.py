@@ -1249,16 +1249,19 @@ def test_row_view_interpolate_equals_joined_value(gpu, ref, n, f, B, I):
         b, c = pl.b, pl.ctx
         c.dev_inject_faults(None, I, b["shards"], pl.spitch, b["corrupt"])
         roots = pl.arr("roots", shape=(I, 32)).copy()
-        roots[::7, 0] ^= 0x80  # the recheck against a wrong root every 7th instance
-        b["roots"].upload(roots)
+        roots[::7, 0] ^= 0x80  # after the verify: the recheck against a wrong root every 7th instance
         if mode == "step_view":
             rb = c.rx_batch(I, b["shards"], pl.spitch, None, pl.S, b["branches"], b["roots"], b["present"],
                             b["valid"], b["leaves_r"], None, 0, b["digests"], b["status"])
-            c.dev_receive_step(None, rb, None)
-            c.dev_receive_step(None, None, rb)
+            c.dev_receive_step(None, rb, None)  # verify + decode
+            gpu.rbc.lib.rbc_device_sync(0)
+            b["roots"].upload(roots)
+            c.dev_receive_step(None, None, rb)  # rehash + recheck
         else:
             c.dev_verify(None, I, b["shards"], pl.spitch, None, pl.S, b["branches"], b["roots"], b["present"],
                          b["valid"], b["leaves_r"])
+            gpu.rbc.lib.rbc_device_sync(0)
+            b["roots"].upload(roots)
             c.dev_interpolate(None, I, b["shards"], pl.spitch, None, pl.S, b["valid"], b["leaves_r"], 1, b["roots"],
                               b["out"] if mode == "joined" else None, pl.opitch if mode == "joined" else 0,
                               b["digests"], b["status"])
