@@ -34,6 +34,13 @@ RBC_DEV uint4 bload16(rsrc_t r, uint32_t off) {
     auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
     return make_uint4(v[0], v[1], v[2], v[3]);
 }
+// per-lane offset + a wave-uniform one (a row start), which the buffer
+// instruction takes as its scalar soffset: no per-lane address arithmetic
+RBC_DEV uint4 bload16s(rsrc_t r, uint32_t voff, uint32_t soff) {
+    auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+RBC_DEV uint32_t uniform(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 RBC_DEV uint32_t inst_len(const uint32_t *lens, uint32_t uniform, int i) { return lens ? lens[i] : uniform; }
 
 // byte mask keeping the first `nv` bytes (little-endian) of a word
@@ -124,9 +131,8 @@ __global__ __launch_bounds__(TPB, (RC <= 21 ? 3 : 2)) void gf_rows_kernel(GfArgs
             }
             return v;
         } else {
-            const uint32_t pos = s_in[j];
-            uint4 v = bload16(rin, pos * a.in_row_pitch + my_off);
-            return v;
+            // the row position is wave-uniform: row start in SGPRs (s_mul), not a per-lane v_mul_lo
+            return bload16s(rin, my_off, uniform(s_in[j]) * a.in_row_pitch);
         }
     };
 
@@ -157,11 +163,8 @@ __global__ __launch_bounds__(TPB, (RC <= 21 ? 3 : 2)) void gf_rows_kernel(GfArgs
         for (int r = 0; r < RC; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0;
 
         const bool do_copy = (c == 0) && a.copy && my_store;
-        // two input pairs in flight ahead of the pair being multiplied
-        uint4 xa = load_row(0), xb = load_row(1);
-        uint4 pa = load_row(2), pb = load_row(3);
-        for (int j = 0; j < KP; j += 2) {
-            const uint4 na = load_row(j + 4), nb = load_row(j + 5);
+        // one input pair (rows j, j+1) into all RC accumulators
+        auto mac_pair = [&](int j, const uint4 &xa, const uint4 &xb) {
             if (do_copy) {
                 const uint32_t pa = (a.mode == GF_MODE_ENCODE) ? (uint32_t)j : s_in[j];
                 *reinterpret_cast<uint4 *>(a.copy + (size_t)inst * a.out_inst_pitch +
@@ -185,10 +188,19 @@ __global__ __launch_bounds__(TPB, (RC <= 21 ? 3 : 2)) void gf_rows_kernel(GfArgs
                 acc[r][2] = xor3(acc[r][2], gf_mul4(ta, t2.x, sa2), gf_mul4(tb, t2.y, sb2));
                 acc[r][3] = xor3(acc[r][3], gf_mul4(ta, t2.x, sa3), gf_mul4(tb, t2.y, sb3));
             }
-            xa = pa;
-            xb = pb;
-            pa = na;
-            pb = nb;
+        };
+        // two buffers of an input pair each: B's loads are in flight while A is
+        // multiplied and the other way round (no register rotation, so the
+        // wait before a pair's use leaves the other pair's loads outstanding)
+        uint4 a0 = load_row(0), a1 = load_row(1);
+        uint4 b0 = load_row(2), b1 = load_row(3);
+        for (int j = 0; j < KP; j += 4) {
+            mac_pair(j, a0, a1);
+            a0 = load_row(j + 4);
+            a1 = load_row(j + 5);
+            if (j + 2 < KP) mac_pair(j + 2, b0, b1);
+            b0 = load_row(j + 6);
+            b1 = load_row(j + 7);
         }
         if (my_store) {
             const int nvalid = (int)S - (int)my_off;  // zero the bytes past S
@@ -229,7 +241,7 @@ __global__ __launch_bounds__(64) void gf_short_kernel(GfArgs a) {
     set_wave_prio(a.prio);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int TPB = 64;
-    const int KP = (a.K + 1) & ~1;
+    const int KP = (a.K + 3) & ~3;  // the loop takes two input pairs per trip
     uint4 *s_t01 = reinterpret_cast<uint4 *>(smem);
     uint32_t *s_t2 = reinterpret_cast<uint32_t *>(smem + (size_t)16 * RC * KP);
     uint8_t *s_in = reinterpret_cast<uint8_t *>(smem + (size_t)20 * RC * KP);
@@ -252,6 +264,9 @@ __global__ __launch_bounds__(64) void gf_short_kernel(GfArgs a) {
     uint8_t *out_inst = a.out + (size_t)inst * a.out_inst_pitch;
     const rsrc_t rin = make_rsrc(in_inst, a.in_inst_bytes);
     for (int t = tid; t < a.K; t += TPB) s_in[t] = a.in_idx[(size_t)inst * a.idx_stride + t];
+    // rows K .. K+7 (the prefetch past the end) read row 0: unconditional loads
+    // keep the waits counted, and their products are never accumulated
+    for (int t = a.K + tid; t < a.K + 8; t += TPB) s_in[t] = 0;
     for (int t = tid; t < a.R; t += TPB) s_out[t] = a.out_idx[(size_t)inst * a.idx_stride2 + t];
     const int r0 = c * RC;
     const int rows = min(RC, rlim - r0);
@@ -267,17 +282,14 @@ __global__ __launch_bounds__(64) void gf_short_kernel(GfArgs a) {
     }
     __syncthreads();
     auto load_row = [&](int j) -> uint3 {
-        if (j >= a.K) return make_uint3(0, 0, 0);
-        auto v = __builtin_amdgcn_raw_buffer_load_b96(rin, (int)(s_in[j] * a.in_row_pitch + my_off), 0, 0);
+        // wave-uniform row start as the scalar soffset (no per-lane v_mul_lo)
+        auto v = __builtin_amdgcn_raw_buffer_load_b96(rin, (int)my_off, (int)(uniform(s_in[j]) * a.in_row_pitch), 0);
         return make_uint3(v[0], v[1], v[2]);
     };
     uint32_t acc[RC][3];
 #pragma unroll
     for (int r = 0; r < RC; ++r) acc[r][0] = acc[r][1] = acc[r][2] = 0;
-    uint3 xa = load_row(0), xb = load_row(1);
-    uint3 pa = load_row(2), pb = load_row(3);
-    for (int j = 0; j < KP; j += 2) {
-        const uint3 na = load_row(j + 4), nb = load_row(j + 5);
+    auto mac_pair = [&](int j, const uint3 &xa, const uint3 &xb) {
         const GfSel sa0 = gf_sel(xa.x), sa1 = gf_sel(xa.y), sa2 = gf_sel(xa.z);
         const GfSel sb0 = gf_sel(xb.x), sb1 = gf_sel(xb.y), sb2 = gf_sel(xb.z);
 #pragma unroll
@@ -290,10 +302,17 @@ __global__ __launch_bounds__(64) void gf_short_kernel(GfArgs a) {
             acc[r][1] = xor3(acc[r][1], gf_mul4(ta, t2.x, sa1), gf_mul4(tb, t2.y, sb1));
             acc[r][2] = xor3(acc[r][2], gf_mul4(ta, t2.x, sa2), gf_mul4(tb, t2.y, sb2));
         }
-        xa = pa;
-        xb = pb;
-        pa = na;
-        pb = nb;
+    };
+    // two buffers of an input pair each (see gf_rows_kernel)
+    uint3 a0 = load_row(0), a1 = load_row(1);
+    uint3 b0 = load_row(2), b1 = load_row(3);
+    for (int j = 0; j < KP; j += 4) {
+        mac_pair(j, a0, a1);
+        a0 = load_row(j + 4);
+        a1 = load_row(j + 5);
+        mac_pair(j + 2, b0, b1);
+        b0 = load_row(j + 6);
+        b1 = load_row(j + 7);
     }
     // zero the bytes past S; never write past the row pitch (word granular)
     const int nvalid = (int)S - (int)my_off;
@@ -1456,13 +1475,21 @@ hipError_t rbc_launch_gf_rows(const GfArgs &a, hipStream_t st) {
     if (a.count <= 0 || (a.R <= 0 && !a.copy)) return hipSuccess;
     if (a.tpb == 64 && a.wpt == 3) {  // short rows, 12 bytes per lane (decode, no compare / copy)
         if (a.mode != GF_MODE_DECODE || a.nmiss || a.copy) return hipErrorInvalidValue;
-        const int KP = (a.K + 1) & ~1;
-        const size_t lds = (size_t)20 * a.rc * KP + 512;
-        const int chunks = (a.R + a.rc - 1) / a.rc;
-        const long items = (long)a.count * a.tiles;
+#ifdef RBC_AB_SHORT_RC  // A/B builds (tools/build_ab.sh): another row chunk for the short-row kernel
+        GfArgs b = a;
+        b.rc = RBC_AB_SHORT_RC;
+#else
+        const GfArgs &b = a;
+#endif
+        if (b.K > 248) return hipErrorInvalidValue;  // the prefetch pad rows K .. K+7 fit s_in
+        const int KP = (b.K + 3) & ~3;
+        const size_t lds = (size_t)20 * b.rc * KP + 512;
+        const int chunks = (b.R + b.rc - 1) / b.rc;
+        const long items = (long)b.count * b.tiles;
         dim3 grid((unsigned)(((items + 7) / 8) * 8 * chunks));
-        if (a.rc == 8) hipLaunchKernelGGL(gf_short_kernel<8>, grid, dim3(64), lds, st, a);
-        else if (a.rc == 4) hipLaunchKernelGGL(gf_short_kernel<4>, grid, dim3(64), lds, st, a);
+        if (b.rc == 16) hipLaunchKernelGGL(gf_short_kernel<16>, grid, dim3(64), lds, st, b);
+        else if (b.rc == 8) hipLaunchKernelGGL(gf_short_kernel<8>, grid, dim3(64), lds, st, b);
+        else if (b.rc == 4) hipLaunchKernelGGL(gf_short_kernel<4>, grid, dim3(64), lds, st, b);
         else return hipErrorInvalidValue;
         return hipGetLastError();
     }
@@ -1472,8 +1499,14 @@ hipError_t rbc_launch_gf_rows(const GfArgs &a, hipStream_t st) {
         return hipErrorInvalidValue;
     }
     if (a.tpb != 0 && a.tpb != 256) return hipErrorInvalidValue;
-    switch (a.rc) {
-#define RBC_RC_CASE(x) case x: return launch_gf_rc<x>(a, st);
+#ifdef RBC_AB_LONG_RC  // A/B builds: another row chunk for interpolate's missing data rows (FFT codec)
+    GfArgs b = a;
+    if (a.rcount) b.rc = RBC_AB_LONG_RC;
+#else
+    const GfArgs &b = a;
+#endif
+    switch (b.rc) {
+#define RBC_RC_CASE(x) case x: return launch_gf_rc<x>(b, st);
         RBC_RC_CASE(1) RBC_RC_CASE(2) RBC_RC_CASE(3) RBC_RC_CASE(4) RBC_RC_CASE(5) RBC_RC_CASE(6)
         RBC_RC_CASE(7) RBC_RC_CASE(8) RBC_RC_CASE(9) RBC_RC_CASE(10) RBC_RC_CASE(11) RBC_RC_CASE(12)
         RBC_RC_CASE(13) RBC_RC_CASE(14) RBC_RC_CASE(15) RBC_RC_CASE(16) RBC_RC_CASE(17) RBC_RC_CASE(18)

@@ -56,6 +56,8 @@ def main():
     ap.add_argument("--last", type=int, default=20)
     ap.add_argument("--json")
     ap.add_argument("--traffic")
+    ap.add_argument("--value-form", default="row view", choices=("row view", "joined"),
+                    help="the bench's interpolate value form in the profiled run (bench.py --join: joined)")
     a = ap.parse_args()
     n, f = CONFIGS[a.config]
     k = n - 2 * f
@@ -95,13 +97,24 @@ def main():
     if a.json:
         json.dump(rows, open(a.json, "w"), indent=1)
     if a.traffic:
-        out = {"config": a.config, "instances": a.instances, "source": os.path.relpath(a.dir), "kernels": {}}
+        out = {"config": a.config, "instances": a.instances, "value_form": a.value_form,
+               "source": os.path.relpath(a.dir), "kernels": {}}
         for rl, r in rows.items():
             if "hbm_read_bytes" in r and "hbm_write_bytes" in r:
                 out["kernels"][rl] = {"hbm_bytes_per_launch": r["hbm_read_bytes"] + r["hbm_write_bytes"],
                                       "hbm_read_bytes": r["hbm_read_bytes"], "hbm_write_bytes": r["hbm_write_bytes"],
                                       "avg_ms_traced": r["avg_ms_traced"], "SQ_INSTS_VALU": r.get("SQ_INSTS_VALU"),
                                       "valu_per_compression": r.get("valu_per_compression")}
+        # roofline_decode's unit (bench.py): the receive step's decode kernels together
+        parts = [rl for rl in out["kernels"] if "[grid" not in rl and (
+            rl.startswith(("decode_prepare", "gf_rows_kernel", "gf_short_kernel")) or rl == "rs_fft_kernel<decode>")]
+        if len(parts) == 3:
+            ks = [out["kernels"][p_] for p_ in parts]
+            out["kernels"]["decode: prepare + gf_rows_kernel + rs_fft_kernel<decode>"] = {
+                "hbm_bytes_per_launch": sum(x["hbm_bytes_per_launch"] for x in ks),
+                "hbm_read_bytes": sum(x["hbm_read_bytes"] for x in ks),
+                "hbm_write_bytes": sum(x["hbm_write_bytes"] for x in ks),
+                "avg_ms_traced": round(sum(x["avg_ms_traced"] or 0 for x in ks), 4), "parts": parts}
         json.dump(out, open(a.traffic, "w"), indent=1)
 
 
