@@ -52,7 +52,7 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--instances", type=int, default=1024)
-    ap.add_argument("--value-bytes", type=int, default=1 << 20)
+    ap.add_argument("--value-bytes", type=int, default=0, help="default: the config's (bench.py CONFIGS)")
     ap.add_argument("--last", type=int, default=20)
     ap.add_argument("--json")
     ap.add_argument("--traffic")
@@ -61,7 +61,8 @@ def main():
     a = ap.parse_args()
     n, f = CONFIGS[a.config]
     k = n - 2 * f
-    S = (a.value_bytes + k - 1) // k
+    vb = a.value_bytes or {"c1": 1 << 20, "c2": 1 << 20, "c3": 4 << 20, "c4": 64 << 10}[a.config]
+    S = (vb + k - 1) // k
     d = 0
     while (1 << d) < n:
         d += 1
