@@ -189,18 +189,17 @@ __global__ __launch_bounds__(TPB, (RC <= 21 ? 3 : 2)) void gf_rows_kernel(GfArgs
                 acc[r][3] = xor3(acc[r][3], gf_mul4(ta, t2.x, sa3), gf_mul4(tb, t2.y, sb3));
             }
         };
-        // two buffers of an input pair each: B's loads are in flight while A is
-        // multiplied and the other way round (no register rotation, so the
-        // wait before a pair's use leaves the other pair's loads outstanding)
-        uint4 a0 = load_row(0), a1 = load_row(1);
-        uint4 b0 = load_row(2), b1 = load_row(3);
+        // two buffers of an input pair each, every load issued one pair of
+        // multiplies ahead of its use and no register rotation: the compiler's
+        // wait at the loop top then covers loads issued a whole pair earlier
+        uint4 a0 = load_row(0), a1 = load_row(1), b0, b1;
         for (int j = 0; j < KP; j += 4) {
+            b0 = load_row(j + 2);
+            b1 = load_row(j + 3);
             mac_pair(j, a0, a1);
             a0 = load_row(j + 4);
             a1 = load_row(j + 5);
             if (j + 2 < KP) mac_pair(j + 2, b0, b1);
-            b0 = load_row(j + 6);
-            b1 = load_row(j + 7);
         }
         if (my_store) {
             const int nvalid = (int)S - (int)my_off;  // zero the bytes past S
@@ -304,15 +303,14 @@ __global__ __launch_bounds__(64) void gf_short_kernel(GfArgs a) {
         }
     };
     // two buffers of an input pair each (see gf_rows_kernel)
-    uint3 a0 = load_row(0), a1 = load_row(1);
-    uint3 b0 = load_row(2), b1 = load_row(3);
+    uint3 a0 = load_row(0), a1 = load_row(1), b0, b1;
     for (int j = 0; j < KP; j += 4) {
+        b0 = load_row(j + 2);
+        b1 = load_row(j + 3);
         mac_pair(j, a0, a1);
         a0 = load_row(j + 4);
         a1 = load_row(j + 5);
         mac_pair(j + 2, b0, b1);
-        b0 = load_row(j + 6);
-        b1 = load_row(j + 7);
     }
     // zero the bytes past S; never write past the row pitch (word granular)
     const int nvalid = (int)S - (int)my_off;
