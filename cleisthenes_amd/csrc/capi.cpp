@@ -35,11 +35,6 @@ inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // Rows per GF chunk (accumulators held in VGPRs) of the matrix codec.
 constexpr int kGfRcMax = 21;
 
-// Rows per chunk of the FFT codec's missing-data GF pass: 8 with 4 KiB
-// column tiles; 4 with the one-wave tiles of short rows (C4: twice the blocks
-// per CU for the 64-thread blocks, 2.32 -> 2.00 ms).
-int gf_md_rcmax(uint32_t shard_pitch) { return shard_pitch <= 2048 ? 4 : 8; }
-
 int tree_width(int n) {
     int w = 1;
     while (w < n) w <<= 1;
@@ -158,6 +153,11 @@ struct rbc_ctx {
     // (encode, leaves, tree build) and the receive-side ones (verify,
     // interpolate); rbc_ctx_set_wave_priority, default 0
     int tx_prio = 0, rx_prio = 0;
+    // interpolate's GF transforms (missing-data rows, re-encode) issue at the
+    // commit side's level, like the commit side's own transform: at the
+    // receive level they took the SIMDs from the commit side's leaf hashing
+    // (C2 489 vs 509, C1 411 vs 473 GB/s; tools/gpu_runs/gpu_r03j.sh)
+    int dec_prio() const { return tx_prio; }
     std::vector<uint8_t> h_M;      // n x k encode matrix
     uint8_t *d_M = nullptr;        // device copy; parity rows at d_M + k*k
     std::mutex mu;
@@ -468,22 +468,14 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
         g.count = count;
         g.R = rmax;
         g.K = c->k;
-        g.rc = rbc_gf_pick_rc(rmax, gf_md_rcmax(shard_pitch));
-        // short rows (C4: 763 B) would leave most of a 4 KiB tile idle
-        g.tpb = ((g.rc == 8 || g.rc == 4) && shard_pitch <= 2048) ? 64 : 256;
-        g.tiles = (int)((shard_pitch + 16 * g.tpb - 1) / (16 * g.tpb));
-        if (g.tpb == 64) {
-            // 12 bytes per lane when that keeps more lanes busy (C4: S = 763 ->
-            // 64 of 64 lanes instead of 48); rows shorter than a 16-B tile's
-            // share keep the 16-byte form
-            const uint32_t S = shard_lens ? (uint32_t)shard_pitch : uniform_shard_len;
-            const double u16 = (double)S / (1024.0 * ((S + 1023) / 1024));
-            const double u12 = (double)S / (768.0 * ((S + 767) / 768));
-            if (u12 > u16 + 0.05) {
-                g.wpt = 3;
-                g.tiles = (int)((shard_pitch + 767) / 768);
-            }
-        }
+        // gf_regen_kernel: 1 KiB column tiles (16 B per lane), or 768 B (12 B
+        // per lane) where that keeps more lanes busy (C4: S = 763 -> 64 of 64
+        // lanes instead of 48)
+        const uint32_t S = shard_lens ? (uint32_t)shard_pitch : uniform_shard_len;
+        const double u16 = (double)S / (1024.0 * ((S + 1023) / 1024));
+        const double u12 = (double)S / (768.0 * ((S + 767) / 768));
+        g.wpt = u12 > u16 + 0.05 ? 3 : 4;
+        g.tiles = (int)((shard_pitch + 256 * g.wpt - 1) / (256 * g.wpt));
         g.mode = GF_MODE_DECODE;
         g.in = shards;
         g.in_inst_pitch = (uint64_t)c->n * shard_pitch;
@@ -502,8 +494,8 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
         g.idx_stride2 = pa.regen_stride;
         g.status = status;
         g.rcount = pa.rcount;
-        g.prio = c->rx_prio;
-        RBC_HIP(rbc_launch_gf_rows(g, st));
+        g.prio = c->dec_prio();
+        RBC_HIP(rbc_launch_gf_regen(g, st));
         // 2) parity positions: additive-FFT re-encode of the completed data half
         FftArgs a{};
         a.count = count;
@@ -523,7 +515,7 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
             a.list = pa.list;
             a.counter = pa.counter;
         }
-        a.prio = c->rx_prio;
+        a.prio = c->dec_prio();
         RBC_HIP(rbc_launch_rs_fft(a, st));
     } else if (nr > 0) {
         GfArgs g{};
@@ -557,7 +549,7 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
             g.counter = pa.counter;
             g.n = c->n;
         }
-        g.prio = c->rx_prio;
+        g.prio = c->dec_prio();
         RBC_HIP(rbc_launch_gf_rows(g, st));
     }
     return RBC_OK;

@@ -229,99 +229,163 @@ __global__ __launch_bounds__(TPB, (RC <= 21 ? 3 : 2)) void gf_rows_kernel(GfArgs
 }
 
 // ============================================================================
-// gf_short: interpolate's missing data rows (FFT codec, decode mode, no
-// compare / copy) for SHORT rows: one wave per (instance, 768-byte column
-// tile, RC-row chunk), 12 bytes (3 packed words) per lane.  With 16 bytes per
-// lane a 763-byte C4 row keeps 48 of 64 lanes busy; 12 keeps 64.  Same LDS
-// tables, block -> (item, chunk) mapping and pipelined loads as gf_rows.
+// gf_regen: interpolate's missing data rows with the FFT codec (decode mode,
+// no compare / copy): out[r] = XOR_j D[r][j] * in[j] for the rcount[i] <= R
+// missing rows of each instance.
+//
+// One block per (instance, column tile); a tile is 64 lanes x W words.  The
+// block's two waves split the instance's m missing rows between them
+// (ceil(m/2) and floor(m/2), at most RC each; m > 2 RC takes further passes),
+// so every input row is read from HBM once per tile and the second wave's
+// copy of it hits the CU's L1: reads are the algorithmic k*S (gf_rows /
+// round 2's RC-row chunk blocks re-read all k inputs for every chunk).  The five perm
+// tables of each coefficient sit in a per-wave LDS region, built for JC
+// inputs at a time by the wave itself (no block barrier: one wave's LDS
+// operations complete in order), and read by wave-uniform broadcast at a
+// VGPR base with immediate offsets.  Byte selectors of an input word are
+// computed once per wave and shared by up to RC rows.
 // ============================================================================
-template <int RC>
-__global__ __launch_bounds__(64) void gf_short_kernel(GfArgs a) {
+template <int W>
+struct GfVec {
+    uint32_t v[W];
+};
+template <int V>
+struct IntC {
+    static constexpr int value = V;
+};
+
+// <= 128 VGPRs (4 waves per SIMD); a cap of 2 waves measured the same
+// under the pipeline (tools/gpu_runs/gpu_r03j.sh)
+template <int W, int RC, int JC>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void gf_regen_kernel(GfArgs a) {
+    static_assert(JC % 4 == 0 && RC % 4 == 0, "two input pairs per trip, rows in groups of 4");
     set_wave_prio(a.prio);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int TPB = 64;
-    const int KP = (a.K + 3) & ~3;  // the loop takes two input pairs per trip
-    uint4 *s_t01 = reinterpret_cast<uint4 *>(smem);
-    uint32_t *s_t2 = reinterpret_cast<uint32_t *>(smem + (size_t)16 * RC * KP);
-    uint8_t *s_in = reinterpret_cast<uint8_t *>(smem + (size_t)20 * RC * KP);
-    uint8_t *s_out = s_in + 256;
-    const int chunks = (a.R + RC - 1) / RC;
-    const int grp = blockIdx.x / (8 * chunks), rem = blockIdx.x - grp * 8 * chunks;
-    const int c = rem >> 3;
-    const int item = grp * 8 + (rem & 7);
-    if (item >= a.count * a.tiles) return;
-    const int inst = item / a.tiles;
-    const int tile = item - inst * a.tiles;
-    const int tid = threadIdx.x;
+    // the wave index is uniform per wave: readfirstlane tells the compiler,
+    // so the per-wave row split below stays in SGPRs and scalar branches
+    const int wave = (int)uniform(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+    const int inst = (int)blockIdx.x / a.tiles;
+    const int tile = (int)blockIdx.x - inst * a.tiles;
+    if (inst >= a.count) return;
     if (a.status && a.status[inst] != 0) return;
-    const int rlim = a.rcount ? min(a.rcount[inst], a.R) : a.R;
-    if (c * RC >= rlim) return;
+    const int m = min(a.rcount[inst], a.R);
+    if (m <= 0) return;
+    const uint32_t tile0 = (uint32_t)tile * (256u * W);
+    if (tile0 >= a.out_row_pitch) return;
+    const uint32_t my_off = tile0 + 4u * W * (uint32_t)lane;
     const uint32_t S = inst_len(a.lens, a.uniform_len, inst);
-    const uint32_t my_off = (uint32_t)tile * (12u * TPB) + 12u * tid;
-    if ((uint32_t)tile * (12u * TPB) >= a.out_row_pitch) return;
+    const int K = a.K;
+    const int KP = (K + 3) & ~3;
+    constexpr uint32_t T01_B = 16u * RC * JC, T2_B = 8u * RC * (JC / 2);
+    const uint32_t wave_b = T01_B + T2_B + 4u * (uint32_t)(KP + 8);  // % 16 == 0 (KP % 4 == 0)
+    unsigned char *wbase = smem + (size_t)wave * wave_b;
+    uint4 *s_t01 = reinterpret_cast<uint4 *>(wbase);
+    uint2 *s_t2 = reinterpret_cast<uint2 *>(wbase + T01_B);
+    uint32_t *s_off = reinterpret_cast<uint32_t *>(wbase + T01_B + T2_B);
     const uint8_t *in_inst = a.in + (size_t)inst * a.in_inst_pitch;
     uint8_t *out_inst = a.out + (size_t)inst * a.out_inst_pitch;
     const rsrc_t rin = make_rsrc(in_inst, a.in_inst_bytes);
-    for (int t = tid; t < a.K; t += TPB) s_in[t] = a.in_idx[(size_t)inst * a.idx_stride + t];
-    // rows K .. K+7 (the prefetch past the end) read row 0: unconditional loads
-    // keep the waits counted, and their products are never accumulated
-    for (int t = a.K + tid; t < a.K + 8; t += TPB) s_in[t] = 0;
-    for (int t = tid; t < a.R; t += TPB) s_out[t] = a.out_idx[(size_t)inst * a.idx_stride2 + t];
-    const int r0 = c * RC;
-    const int rows = min(RC, rlim - r0);
-    for (int e = tid; e < RC * KP; e += TPB) {
-        const int r = e / KP, j = e - r * KP;
-        uint32_t cf = 0;
-        if (r < rows && j < a.K) cf = a.coef[(size_t)inst * a.coef_inst_stride + (size_t)(r0 + r) * a.K + j];
-        uint4 t01;
-        uint32_t t2;
-        gf_tables(cf, t01, t2);
-        s_t01[j * RC + r] = t01;
-        s_t2[((j >> 1) * RC + r) * 2 + (j & 1)] = t2;
-    }
-    __syncthreads();
-    auto load_row = [&](int j) -> uint3 {
-        // wave-uniform row start as the scalar soffset (no per-lane v_mul_lo)
-        auto v = __builtin_amdgcn_raw_buffer_load_b96(rin, (int)my_off, (int)(uniform(s_in[j]) * a.in_row_pitch), 0);
-        return make_uint3(v[0], v[1], v[2]);
+    const uint8_t *idx = a.in_idx + (size_t)inst * a.idx_stride;
+    // input row starts; the prefetch past K reads row 0 (never accumulated)
+    for (int t = lane; t < KP + 8; t += 64) s_off[t] = (t < K ? (uint32_t)idx[t] : 0u) * a.in_row_pitch;
+    const uint8_t *coef = a.coef + (size_t)inst * a.coef_inst_stride;
+
+    auto load_row = [&](int j) -> GfVec<W> {
+        const uint32_t so = uniform(s_off[j]);
+        GfVec<W> x;
+        if constexpr (W == 4) {
+            auto v = __builtin_amdgcn_raw_buffer_load_b128(rin, (int)my_off, (int)so, 0);
+            x.v[0] = v[0]; x.v[1] = v[1]; x.v[2] = v[2]; x.v[3] = v[3];
+        } else {
+            static_assert(W == 3, "W = 3 or 4");
+            auto v = __builtin_amdgcn_raw_buffer_load_b96(rin, (int)my_off, (int)so, 0);
+            x.v[0] = v[0]; x.v[1] = v[1]; x.v[2] = v[2];
+        }
+        return x;
     };
-    uint32_t acc[RC][3];
+
+    // one pass = up to 2 RC rows: ceil / floor of half to waves 0 / 1
+    // (wave-uniform).  The pass body is instantiated per count of 4-row
+    // groups NG, so the unrolled multiply-accumulate is straight-line: a
+    // per-row exit inside it costs the compiler ~2x the registers (spills).
+    auto pass = [&](auto ngc, int r0, int rows) {
+        constexpr int NG = decltype(ngc)::value, RG = 4 * NG;
+        uint32_t acc[RG][W];
 #pragma unroll
-    for (int r = 0; r < RC; ++r) acc[r][0] = acc[r][1] = acc[r][2] = 0;
-    auto mac_pair = [&](int j, const uint3 &xa, const uint3 &xb) {
-        const GfSel sa0 = gf_sel(xa.x), sa1 = gf_sel(xa.y), sa2 = gf_sel(xa.z);
-        const GfSel sb0 = gf_sel(xb.x), sb1 = gf_sel(xb.y), sb2 = gf_sel(xb.z);
+        for (int r = 0; r < RG; ++r)
 #pragma unroll
-        for (int r = 0; r < RC; ++r) {
-            if (r >= rows) break;  // block-uniform (see gf_rows_kernel)
-            const uint4 ta = s_t01[j * RC + r];
-            const uint4 tb = s_t01[(j + 1) * RC + r];
-            const uint2 t2 = *reinterpret_cast<const uint2 *>(&s_t2[((j >> 1) * RC + r) * 2]);
-            acc[r][0] = xor3(acc[r][0], gf_mul4(ta, t2.x, sa0), gf_mul4(tb, t2.y, sb0));
-            acc[r][1] = xor3(acc[r][1], gf_mul4(ta, t2.x, sa1), gf_mul4(tb, t2.y, sb1));
-            acc[r][2] = xor3(acc[r][2], gf_mul4(ta, t2.x, sa2), gf_mul4(tb, t2.y, sb2));
+            for (int w = 0; w < W; ++w) acc[r][w] = 0;
+        // tables of inputs [j0, j0 + JC) for the RG rows, layout [j][r] (t2
+        // as {j even, j odd} pairs), zero past `rows`: one VGPR base plus
+        // immediates per input pair in the loop
+        auto build = [&](int j0) {
+            for (int e = lane; e < RG * JC; e += 64) {
+                const int r = e / JC, jl = e - r * JC, j = j0 + jl;
+                const uint32_t cf = (j < K && r < rows) ? coef[(size_t)(r0 + r) * K + j] : 0u;
+                uint4 t01;
+                uint32_t t2;
+                gf_tables(cf, t01, t2);
+                s_t01[jl * RC + r] = t01;
+                reinterpret_cast<uint32_t *>(s_t2)[((jl >> 1) * RC + r) * 2 + (jl & 1)] = t2;
+            }
+        };
+        auto mac_pair = [&](int jl, const GfVec<W> &xa, const GfVec<W> &xb) {
+            GfSel sa[W], sb[W];
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                sa[w] = gf_sel(xa.v[w]);
+                sb[w] = gf_sel(xb.v[w]);
+            }
+            uint32_t o01 = (uint32_t)jl * (16u * RC), o2 = (uint32_t)(jl >> 1) * (8u * RC);
+            asm volatile("" : "+v"(o01), "+v"(o2));  // VGPR base: no per-read v_mov of an SGPR address
+            const unsigned char *p01 = reinterpret_cast<const unsigned char *>(s_t01) + o01;
+            const unsigned char *p2 = reinterpret_cast<const unsigned char *>(s_t2) + o2;
+#pragma unroll
+            for (int r = 0; r < RG; ++r) {
+                const uint4 ta = *reinterpret_cast<const uint4 *>(p01 + 16 * r);
+                const uint4 tb = *reinterpret_cast<const uint4 *>(p01 + 16 * (RC + r));
+                const uint2 t2 = *reinterpret_cast<const uint2 *>(p2 + 8 * r);
+#pragma unroll
+                for (int w = 0; w < W; ++w)
+                    acc[r][w] = xor3(acc[r][w], gf_mul4(ta, t2.x, sa[w]), gf_mul4(tb, t2.y, sb[w]));
+            }
+        };
+        // two buffers of an input pair each, every load issued one pair of
+        // multiplies ahead of its use (see gf_rows_kernel)
+        GfVec<W> a0 = load_row(0), a1 = load_row(1), b0, b1;
+        for (int j = 0; j < KP; j += 4) {
+            b0 = load_row(j + 2);
+            b1 = load_row(j + 3);
+            const int jl = j % JC;  // JC % 4 == 0: a chunk starts at a trip
+            if (jl == 0) build(j);
+            mac_pair(jl, a0, a1);
+            a0 = load_row(j + 4);
+            a1 = load_row(j + 5);
+            mac_pair(jl + 2, b0, b1);
+        }
+        // zero the bytes past S; never write past the row pitch (word granular)
+        const int nvalid = (int)S - (int)my_off;
+        const uint8_t *oidx = a.out_idx + (size_t)inst * a.idx_stride2 + r0;
+#pragma unroll
+        for (int r = 0; r < RG; ++r) {
+            if (r < rows) {
+                uint32_t *dst = reinterpret_cast<uint32_t *>(out_inst + (size_t)oidx[r] * a.out_row_pitch + my_off);
+#pragma unroll
+                for (int w = 0; w < W; ++w)
+                    if (my_off + 4u * w < a.out_row_pitch) dst[w] = acc[r][w] & keep_bytes(nvalid - 4 * w);
+            }
         }
     };
-    // two buffers of an input pair each (see gf_rows_kernel)
-    uint3 a0 = load_row(0), a1 = load_row(1), b0, b1;
-    for (int j = 0; j < KP; j += 4) {
-        b0 = load_row(j + 2);
-        b1 = load_row(j + 3);
-        mac_pair(j, a0, a1);
-        a0 = load_row(j + 4);
-        a1 = load_row(j + 5);
-        mac_pair(j + 2, b0, b1);
-    }
-    // zero the bytes past S; never write past the row pitch (word granular)
-    const int nvalid = (int)S - (int)my_off;
-#pragma unroll
-    for (int r = 0; r < RC; ++r) {
-        if (r < rows) {
-            uint32_t *dst = reinterpret_cast<uint32_t *>(out_inst + (size_t)s_out[r0 + r] * a.out_row_pitch + my_off);
-#pragma unroll
-            for (int w = 0; w < 3; ++w)
-                if (my_off + 4u * w < a.out_row_pitch) dst[w] = acc[r][w] & keep_bytes(nvalid - 4 * w);
-        }
+    for (int base = 0; base < m; base += 2 * RC) {
+        const int mp = min(2 * RC, m - base);
+        const int r0 = base + (wave ? (mp + 1) / 2 : 0);
+        const int rows = wave ? mp / 2 : (mp + 1) / 2;
+        const int ng = (rows + 3) >> 2;
+        static_assert(RC <= 16, "up to 4 row groups per wave");
+        if (ng == 1) pass(IntC<1>{}, r0, rows);
+        else if (ng == 2) pass(IntC<2>{}, r0, rows);
+        else if (RC >= 12 && ng == 3) pass(IntC<(RC >= 12 ? 3 : 1)>{}, r0, rows);
+        else if (RC >= 16 && ng == 4) pass(IntC<(RC >= 16 ? 4 : 1)>{}, r0, rows);
     }
 }
 
@@ -1471,40 +1535,9 @@ int rbc_gf_pick_rc(int R, int rcmax) {
 
 hipError_t rbc_launch_gf_rows(const GfArgs &a, hipStream_t st) {
     if (a.count <= 0 || (a.R <= 0 && !a.copy)) return hipSuccess;
-    if (a.tpb == 64 && a.wpt == 3) {  // short rows, 12 bytes per lane (decode, no compare / copy)
-        if (a.mode != GF_MODE_DECODE || a.nmiss || a.copy) return hipErrorInvalidValue;
-#ifdef RBC_AB_SHORT_RC  // A/B builds (tools/build_ab.sh): another row chunk for the short-row kernel
-        GfArgs b = a;
-        b.rc = RBC_AB_SHORT_RC;
-#else
-        const GfArgs &b = a;
-#endif
-        if (b.K > 248) return hipErrorInvalidValue;  // the prefetch pad rows K .. K+7 fit s_in
-        const int KP = (b.K + 3) & ~3;
-        const size_t lds = (size_t)20 * b.rc * KP + 512;
-        const int chunks = (b.R + b.rc - 1) / b.rc;
-        const long items = (long)b.count * b.tiles;
-        dim3 grid((unsigned)(((items + 7) / 8) * 8 * chunks));
-        if (b.rc == 16) hipLaunchKernelGGL(gf_short_kernel<16>, grid, dim3(64), lds, st, b);
-        else if (b.rc == 8) hipLaunchKernelGGL(gf_short_kernel<8>, grid, dim3(64), lds, st, b);
-        else if (b.rc == 4) hipLaunchKernelGGL(gf_short_kernel<4>, grid, dim3(64), lds, st, b);
-        else return hipErrorInvalidValue;
-        return hipGetLastError();
-    }
-    if (a.tpb == 64) {  // short rows: 1 KiB column tiles (one wave per block)
-        if (a.rc == 8) return launch_gf_rc<8, 64>(a, st);
-        if (a.rc == 4) return launch_gf_rc<4, 64>(a, st);
-        return hipErrorInvalidValue;
-    }
     if (a.tpb != 0 && a.tpb != 256) return hipErrorInvalidValue;
-#ifdef RBC_AB_LONG_RC  // A/B builds: another row chunk for interpolate's missing data rows (FFT codec)
-    GfArgs b = a;
-    if (a.rcount) b.rc = RBC_AB_LONG_RC;
-#else
-    const GfArgs &b = a;
-#endif
-    switch (b.rc) {
-#define RBC_RC_CASE(x) case x: return launch_gf_rc<x>(b, st);
+    switch (a.rc) {
+#define RBC_RC_CASE(x) case x: return launch_gf_rc<x>(a, st);
         RBC_RC_CASE(1) RBC_RC_CASE(2) RBC_RC_CASE(3) RBC_RC_CASE(4) RBC_RC_CASE(5) RBC_RC_CASE(6)
         RBC_RC_CASE(7) RBC_RC_CASE(8) RBC_RC_CASE(9) RBC_RC_CASE(10) RBC_RC_CASE(11) RBC_RC_CASE(12)
         RBC_RC_CASE(13) RBC_RC_CASE(14) RBC_RC_CASE(15) RBC_RC_CASE(16) RBC_RC_CASE(17) RBC_RC_CASE(18)
@@ -1514,6 +1547,29 @@ hipError_t rbc_launch_gf_rows(const GfArgs &a, hipStream_t st) {
 #undef RBC_RC_CASE
         default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t rbc_launch_gf_regen(const GfArgs &a, hipStream_t st) {
+    if (a.count <= 0 || a.R <= 0) return hipSuccess;
+    if (a.mode != GF_MODE_DECODE || !a.rcount || a.nmiss || a.copy || a.K < 1 || a.K > 248 || a.tiles < 1)
+        return hipErrorInvalidValue;
+    const int W = a.wpt == 3 ? 3 : 4;
+    if ((uint64_t)a.tiles * 256u * W < a.out_row_pitch) return hipErrorInvalidValue;
+    const uint64_t blocks = (uint64_t)a.count * a.tiles;
+    if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+    constexpr int JC = 16;
+    const int KP = (a.K + 3) & ~3;
+    const dim3 grid((unsigned)blocks), block(128);
+    if (W == 3) {
+        constexpr int RC = 16;  // C4 (m ~ 29 of k = 86): one pass for m <= 32
+        const size_t lds = 2 * ((size_t)20 * RC * JC + 4 * (KP + 8));
+        hipLaunchKernelGGL((gf_regen_kernel<3, RC, JC>), grid, block, lds, st, a);
+    } else {
+        constexpr int RC = 12;  // C1-C3 (m ~ 7-15 of k = 22-44): one pass for m <= 24
+        const size_t lds = 2 * ((size_t)20 * RC * JC + 4 * (KP + 8));
+        hipLaunchKernelGGL((gf_regen_kernel<4, RC, JC>), grid, block, lds, st, a);
+    }
+    return hipGetLastError();
 }
 
 hipError_t rbc_launch_sha_rows(const ShaArgs &a, bool verify, hipStream_t st) {

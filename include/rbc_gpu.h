@@ -85,9 +85,11 @@ int rbc_ctx_set_codec(rbc_ctx *ctx, int codec);
 int rbc_ctx_codec(const rbc_ctx *ctx, int *codec); /* effective: MATRIX or FFT */
 /* Wave issue priority (0..3, the SIMD arbiter's s_setprio level) of this
  * context's commit-side kernels (encode, leaf hashing, tree build) and
- * receive-side kernels (ECHO verify, interpolate).  Only matters when both
- * sides run concurrently on two streams; results are identical either way.
- * Default 0 / 0. */
+ * receive-side kernels (ECHO verify, interpolate's hashing, root recheck,
+ * digest).  Interpolate's GF transforms (missing-data rows, re-encode) take
+ * the commit level, like the commit side's own transform.  Only matters when
+ * both sides run concurrently on two streams; results are identical either
+ * way.  Default 0 / 0. */
 int rbc_ctx_set_wave_priority(rbc_ctx *ctx, int commit_prio, int receive_prio);
 
 /* ---- device memory / streams / events (so a host runtime needs no other
