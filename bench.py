@@ -456,7 +456,7 @@ def report(args, ctx, I, n, k, d, S, present_h, corrupt_h, stage_ms, iso, elapse
              R * (bps + 2 * d) + (regen * bps if pipe else 0)),
     }
     if pipe:
-        kern["decode: prepare + gf_rows_kernel + rs_fft_kernel<decode>"] = (
+        kern["decode: prepare + gf_regen_kernel + rs_fft_kernel<decode>"] = (
             "decode", decode_bytes(n, k, S, present_h, corrupt_h), 0)
     pm, pmc_path = {}, None
     for cand in sorted((x for x in os.listdir(os.path.join(ROOT, "profiles")) if x.startswith("pmc_traffic_r")),
@@ -504,7 +504,7 @@ def report(args, ctx, I, n, k, d, S, present_h, corrupt_h, stage_ms, iso, elapse
     out = {"stage_ms": {kk: round(v, 4) for kk, v in stage_ms.items()}, "roofline": roofline(dom),
            "roofline_encode": roofline(enc_kernel)}
     out["roofline_decode"] = roofline(
-        "decode: prepare + gf_rows_kernel + rs_fft_kernel<decode>",
+        "decode: prepare + gf_regen_kernel + rs_fft_kernel<decode>",
         "receive step's decode_begin -> decoded marks (rbc_rx_marks) on the receiver stream") if pipe else None
     step_comp = I * n * bps + R * (bps + 2 * d) + regen * bps
     step_cps = step_comp / (elapsed_max / args.steps)

@@ -234,13 +234,15 @@ __global__ __launch_bounds__(TPB, (RC <= 21 ? 3 : 2)) void gf_rows_kernel(GfArgs
 // missing rows of each instance.
 //
 // One block per (instance, column tile); a tile is 64 lanes x W words.  The
-// block's two waves split the instance's m missing rows between them
-// (ceil(m/2) and floor(m/2), at most RC each; m > 2 RC takes further passes),
-// so every input row is read from HBM once per tile and the second wave's
-// copy of it hits the CU's L1: reads are the algorithmic k*S (gf_rows /
-// round 2's RC-row chunk blocks re-read all k inputs for every chunk).  The five perm
+// block's NW waves split the instance's m missing rows between them in groups
+// of 4 (at most RC rows a wave; a pass holds NW * RC rows, i.e. all but a
+// few C1-C4 instances in one), and each reads the k input rows of the tile.
+// They share them through the CU's L1 / the XCD's L2 only as far as they stay
+// in step: PMC reads are 1.29x (C2) / 1.68x (C4) of the algorithmic k*S.  A block
+// barrier every trip keeps them in step (1.08x / 1.12x) and costs 0.5-2 % of
+// the pipelined step (tools/gpu_runs/gpu_r03q.sh), so there is none.  The five perm
 // tables of each coefficient sit in a per-wave LDS region, built for JC
-// inputs at a time by the wave itself (no block barrier: one wave's LDS
+// inputs at a time by the wave itself (no barrier for them: one wave's LDS
 // operations complete in order), and read by wave-uniform broadcast at a
 // VGPR base with immediate offsets.  Byte selectors of an input word are
 // computed once per wave and shared by up to RC rows.
@@ -256,8 +258,8 @@ struct IntC {
 
 // <= 128 VGPRs (4 waves per SIMD); a cap of 2 waves measured the same
 // under the pipeline (tools/gpu_runs/gpu_r03j.sh)
-template <int W, int RC, int JC>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void gf_regen_kernel(GfArgs a) {
+template <int W, int RC, int JC, int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) void gf_regen_kernel(GfArgs a) {
     static_assert(JC % 4 == 0 && RC % 4 == 0, "two input pairs per trip, rows in groups of 4");
     set_wave_prio(a.prio);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -304,8 +306,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void g
         return x;
     };
 
-    // one pass = up to 2 RC rows: ceil / floor of half to waves 0 / 1
-    // (wave-uniform).  The pass body is instantiated per count of 4-row
+    // one pass = up to 2 RC rows, split between the waves (wave-uniform;
+    // see the loop below).  The pass body is instantiated per count of 4-row
     // groups NG, so the unrolled multiply-accumulate is straight-line: a
     // per-row exit inside it costs the compiler ~2x the registers (spills).
     auto pass = [&](auto ngc, int r0, int rows) {
@@ -376,16 +378,24 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void g
             }
         }
     };
-    for (int base = 0; base < m; base += 2 * RC) {
-        const int mp = min(2 * RC, m - base);
-        const int r0 = base + (wave ? (mp + 1) / 2 : 0);
-        const int rows = wave ? mp / 2 : (mp + 1) / 2;
-        const int ng = (rows + 3) >> 2;
+    // a pass covers up to NW * RC rows: its G groups of 4 (the last one
+    // padded with zero-table rows) go evenly to the fewest waves that hold
+    // them; a wave left idle ends at once (every pass but the last is full)
+    constexpr int GPW = RC / 4;  // groups per wave at most
+    for (int base = 0; base < m; base += NW * RC) {
+        const int mp = min(NW * RC, m - base);
+        const int G = (mp + 3) >> 2;
+        const int nw = (G + GPW - 1) / GPW;  // active waves (block-uniform)
+        const int q = G / nw, rem = G - q * nw;
+        const int g0 = wave * q + min(wave, rem), ng = wave < nw ? q + (wave < rem) : 0;
+        const int r0 = base + 4 * g0;
+        const int rows = min(4 * ng, mp - 4 * g0);
         static_assert(RC <= 16, "up to 4 row groups per wave");
         if (ng == 1) pass(IntC<1>{}, r0, rows);
         else if (ng == 2) pass(IntC<2>{}, r0, rows);
         else if (RC >= 12 && ng == 3) pass(IntC<(RC >= 12 ? 3 : 1)>{}, r0, rows);
         else if (RC >= 16 && ng == 4) pass(IntC<(RC >= 16 ? 4 : 1)>{}, r0, rows);
+        else return;  // idle: only in the last pass
     }
 }
 
@@ -1559,15 +1569,17 @@ hipError_t rbc_launch_gf_regen(const GfArgs &a, hipStream_t st) {
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
     constexpr int JC = 16;
     const int KP = (a.K + 3) & ~3;
-    const dim3 grid((unsigned)blocks), block(128);
+    const dim3 grid((unsigned)blocks);
     if (W == 3) {
-        constexpr int RC = 16;  // C4 (m ~ 29 of k = 86): one pass for m <= 32
-        const size_t lds = 2 * ((size_t)20 * RC * JC + 4 * (KP + 8));
-        hipLaunchKernelGGL((gf_regen_kernel<3, RC, JC>), grid, block, lds, st, a);
+        // C4 (m ~ 29 +- 4.4 of k = 86): up to 48 rows in one pass, so every
+        // input row is read once per tile; two waves hold m <= 32
+        constexpr int RC = 16, NW = 3;
+        const size_t lds = NW * ((size_t)20 * RC * JC + 4 * (KP + 8));
+        hipLaunchKernelGGL((gf_regen_kernel<3, RC, JC, NW>), grid, dim3(64 * NW), lds, st, a);
     } else {
-        constexpr int RC = 12;  // C1-C3 (m ~ 7-15 of k = 22-44): one pass for m <= 24
-        const size_t lds = 2 * ((size_t)20 * RC * JC + 4 * (KP + 8));
-        hipLaunchKernelGGL((gf_regen_kernel<4, RC, JC>), grid, block, lds, st, a);
+        constexpr int RC = 12, NW = 2;  // C1-C3 (m ~ 7-15 of k = 22-44): one pass for m <= 24
+        const size_t lds = NW * ((size_t)20 * RC * JC + 4 * (KP + 8));
+        hipLaunchKernelGGL((gf_regen_kernel<4, RC, JC, NW>), grid, dim3(64 * NW), lds, st, a);
     }
     return hipGetLastError();
 }

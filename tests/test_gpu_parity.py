@@ -1072,6 +1072,51 @@ def test_host_interpolate_zero_copy_reads_present_rows_only(gpu, ref, n, f, B, p
         assert rc == 0 and np.array_equal(res["values"][i], value) and bytes(res["digests"][i]) == dig, i
 
 
+REGEN_COUNTS = [
+    # (n, f, S, missing data rows per instance): gf_regen_kernel splits an
+    # instance's m rows over the waves of a block in groups of 4 (12 B per lane
+    # for short rows: 3 waves x 16 rows per pass; 16 B per lane: 2 x 12), so
+    # the counts straddle every group, wave and pass boundary of both forms
+    (256, 85, 763, [1, 3, 4, 5, 12, 13, 16, 17, 29, 32, 33, 47, 48, 49, 64, 86]),
+    (128, 42, 23832, [1, 4, 5, 11, 12, 13, 23, 24, 25, 44]),
+    (128, 42, 700, [1, 4, 16, 17, 32, 33, 44]),
+]
+
+
+@pytest.mark.parametrize("n,f,S,ms", REGEN_COUNTS, ids=["n256-short", "n128-long", "n128-short"])
+def test_device_regen_missing_data_row_counts(gpu, n, f, S, ms):
+    """Interpolate with exactly m missing data rows per instance (every parity
+    row present, so the first-k set is the k - m data rows plus the first m
+    parity rows): each regenerated row equals the committed one, zero past S,
+    and the value is the input."""
+    k = n - 2 * f
+    I = len(ms)
+    pl = Pipeline(gpu, n, f, k * S, I, seed=n + S, corrupt_frac=0.0)
+    rng = np.random.default_rng(S)
+    pl.present[:] = 1
+    for i, m in enumerate(ms):
+        pl.present[i, rng.permutation(k)[:m]] = 0
+    pl.b["present"].upload(pl.present)
+    pl.commit()
+    committed = pl.shards().copy()
+    # the absent rows hold garbage, so only the regeneration can restore them
+    garbled = committed.copy()
+    for i in range(I):
+        gone = np.flatnonzero(pl.present[i] == 0)
+        garbled[i][gone] = rng.integers(0, 256, size=(len(gone), pl.spitch), dtype=np.uint8)
+    pl.b["shards"].upload(garbled)
+    pl.receive()
+    assert (pl.arr("status", np.int32) == 0).all()
+    out = pl.arr("out", shape=(I, pl.opitch))
+    assert np.array_equal(out[:, : pl.B], pl.values[:, : pl.B])
+    after = pl.shards()
+    for i, m in enumerate(ms):
+        miss = np.flatnonzero(pl.present[i, :k] == 0)
+        assert len(miss) == m
+        assert np.array_equal(after[i][miss], committed[i][miss]), (i, m)
+        assert not after[i][miss, S:].any(), (i, m)
+
+
 @pytest.mark.parametrize("S", [763, 100, 1400, 1500, 2000])
 def test_device_interpolate_short_rows(gpu, S):
     """Missing-data GF rows for short shards (one-wave tiles: 12 bytes per

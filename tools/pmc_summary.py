@@ -108,10 +108,10 @@ def main():
                                       "valu_per_compression": r.get("valu_per_compression")}
         # roofline_decode's unit (bench.py): the receive step's decode kernels together
         parts = [rl for rl in out["kernels"] if "[grid" not in rl and (
-            rl.startswith(("decode_prepare", "gf_rows_kernel", "gf_short_kernel")) or rl == "rs_fft_kernel<decode>")]
+            rl.startswith(("decode_prepare", "gf_regen_kernel")) or rl == "rs_fft_kernel<decode>")]
         if len(parts) == 3:
             ks = [out["kernels"][p_] for p_ in parts]
-            out["kernels"]["decode: prepare + gf_rows_kernel + rs_fft_kernel<decode>"] = {
+            out["kernels"]["decode: prepare + gf_regen_kernel + rs_fft_kernel<decode>"] = {
                 "hbm_bytes_per_launch": sum(x["hbm_bytes_per_launch"] for x in ks),
                 "hbm_read_bytes": sum(x["hbm_read_bytes"] for x in ks),
                 "hbm_write_bytes": sum(x["hbm_write_bytes"] for x in ks),
