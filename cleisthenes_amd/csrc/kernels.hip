@@ -321,8 +321,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) vo
         // as {j even, j odd} pairs), zero past `rows`: one VGPR base plus
         // immediates per input pair in the loop
         auto build = [&](int j0) {
+            // consecutive lanes take consecutive rows of one input: their
+            // 16-byte table stores are adjacent in LDS (input-major lanes
+            // stored RC * 16 bytes apart, a 16-way bank conflict)
             for (int e = lane; e < RG * JC; e += 64) {
-                const int r = e / JC, jl = e - r * JC, j = j0 + jl;
+                const int jl = e / RG, r = e - jl * RG, j = j0 + jl;
                 const uint32_t cf = (j < K && r < rows) ? coef[(size_t)(r0 + r) * K + j] : 0u;
                 uint4 t01;
                 uint32_t t2;
