@@ -51,6 +51,12 @@ CONFIGS = {
     "c3": (128, 42, 4 << 20, 1024, "N=128 f=42 4MiB"),
     "c4": (256, 85, 64 << 10, 16384, "N=256 f=85 64KiB"),
 }
+# Issue level of interpolate's missing-data GEMV and FFT re-encode under the
+# pipelined schedule ("c": the commit side's, "r": the receive side's).  The
+# GEMV siding with the receiver balances the streams at N = 128 (C2 +3 %, C3
+# +2 %) and starves the leaf hashing at C1, whose 1,024 leaf waves are one per
+# SIMD (-8 %); C4 is indifferent (tools/gpu_runs/gpu_r03t.sh).
+DECODE_PRIO = {"c1": "c,c", "c2": "r,c", "c3": "r,c", "c4": "r,c"}
 METRIC = "RBC shard GB/s (RS encode+decode + Merkle verify) per GPU & node, N=128"
 SEED = 20261015
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
@@ -87,6 +93,9 @@ def parse_args(argv):
                     help="stream that injects the corrupted ECHO shards (synthetic input)")
     ap.add_argument("--wave-prio", default="",
                     help="commit,receive s_setprio levels (default 0,2 pipelined, 0,0 serial)")
+    ap.add_argument("--decode-prio", default="",
+                    help="gemv,reencode levels of interpolate's GF transforms: c (commit level), r (receive "
+                         "level) or 0..3 (default per config, DECODE_PRIO; serial: commit level)")
     ap.add_argument("--hbm-budget", type=float, default=0,
                     help="bytes of HBM this rank may use (default: free device memory / ranks sharing the device)")
     ap.add_argument("--shard-align", type=int, default=128,
@@ -184,6 +193,10 @@ def run(args, world, rank, local_rank, wd, out):
     plan["schedule"] = "pipelined" if pipe else "serial"
     tx, rx = (int(x) for x in (args.wave_prio or ("0,2" if pipe else "0,0")).split(","))
     ctx.set_wave_priority(tx, rx)
+    lv = {"c": tx, "r": rx}
+    gv, rv = (lv[x] if x in lv else int(x)
+              for x in (args.decode_prio or (DECODE_PRIO[args.config] if pipe else "c,c")).split(","))
+    ctx.set_decode_priority(gv, rv)
     stream = ca.Stream(dev)
     mb = lambda x: ca.DeviceBuffer(x, device=dev)  # noqa: E731
     # ---- synthetic inputs: values on the device (the global instance id
@@ -382,7 +395,8 @@ def run(args, world, rank, local_rank, wd, out):
                    "instances_per_gpu": I,
                    "parallelism": f"instances partitioned over {world} GPU(s) in contiguous blocks"
                                   + (", RCCL all-gather of {root,digest} records" if gather else ""),
-                   "gf_codec": ctx.codec, "wave_priority": {"commit": tx, "receive": rx},
+                   "gf_codec": ctx.codec,
+                   "wave_priority": {"commit": tx, "receive": rx, "decode_gemv": gv, "decode_reencode": rv},
                    "value_form": "joined (k*S bytes per instance)" if args.join else
                                  "row view (the k data rows of the shard set, no join)",
                    "faults_on": args.faults_on, "hbm_plan": plan,

@@ -153,11 +153,12 @@ struct rbc_ctx {
     // (encode, leaves, tree build) and the receive-side ones (verify,
     // interpolate); rbc_ctx_set_wave_priority, default 0
     int tx_prio = 0, rx_prio = 0;
-    // interpolate's GF transforms (missing-data rows, re-encode) issue at the
-    // commit side's level, like the commit side's own transform: at the
-    // receive level they took the SIMDs from the commit side's leaf hashing
-    // (C2 489 vs 509, C1 411 vs 473 GB/s; tools/gpu_runs/gpu_r03j.sh)
-    int dec_prio() const { return tx_prio; }
+    // interpolate's two GF transforms (missing-data GEMV, FFT re-encode):
+    // rbc_ctx_set_decode_priority, default -1 = the commit side's level, like
+    // the commit side's own transform
+    int gemv_prio_ = -1, reencode_prio_ = -1;
+    int gemv_prio() const { return gemv_prio_ < 0 ? tx_prio : gemv_prio_; }
+    int reencode_prio() const { return reencode_prio_ < 0 ? tx_prio : reencode_prio_; }
     std::vector<uint8_t> h_M;      // n x k encode matrix
     uint8_t *d_M = nullptr;        // device copy; parity rows at d_M + k*k
     std::mutex mu;
@@ -494,7 +495,7 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
         g.idx_stride2 = pa.regen_stride;
         g.status = status;
         g.rcount = pa.rcount;
-        g.prio = c->dec_prio();
+        g.prio = c->gemv_prio();
         RBC_HIP(rbc_launch_gf_regen(g, st));
         // 2) parity positions: additive-FFT re-encode of the completed data half
         FftArgs a{};
@@ -515,7 +516,7 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
             a.list = pa.list;
             a.counter = pa.counter;
         }
-        a.prio = c->dec_prio();
+        a.prio = c->reencode_prio();
         RBC_HIP(rbc_launch_rs_fft(a, st));
     } else if (nr > 0) {
         GfArgs g{};
@@ -549,7 +550,7 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
             g.counter = pa.counter;
             g.n = c->n;
         }
-        g.prio = c->dec_prio();
+        g.prio = c->reencode_prio();  // the matrix codec's one decode product
         RBC_HIP(rbc_launch_gf_rows(g, st));
     }
     return RBC_OK;
@@ -972,6 +973,13 @@ int rbc_ctx_set_wave_priority(rbc_ctx *c, int commit_prio, int receive_prio) {
     if (!c || commit_prio < 0 || commit_prio > 3 || receive_prio < 0 || receive_prio > 3) return RBC_ERR_INVALID_ARG;
     c->tx_prio = commit_prio;
     c->rx_prio = receive_prio;
+    return RBC_OK;
+}
+
+int rbc_ctx_set_decode_priority(rbc_ctx *c, int gemv_prio, int reencode_prio) {
+    if (!c || gemv_prio < -1 || gemv_prio > 3 || reencode_prio < -1 || reencode_prio > 3) return RBC_ERR_INVALID_ARG;
+    c->gemv_prio_ = gemv_prio;
+    c->reencode_prio_ = reencode_prio;
     return RBC_OK;
 }
 

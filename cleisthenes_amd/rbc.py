@@ -249,6 +249,10 @@ class Context:
         """s_setprio level (0..3) of the commit-side / receive-side kernels."""
         check(lib.rbc_ctx_set_wave_priority(self._p, commit, receive), "rbc_ctx_set_wave_priority")
 
+    def set_decode_priority(self, gemv: int, reencode: int) -> None:
+        """s_setprio level (0..3, -1 = the commit level) of interpolate's GF transforms."""
+        check(lib.rbc_ctx_set_decode_priority(self._p, gemv, reencode), "rbc_ctx_set_decode_priority")
+
     def set_codec(self, codec: str) -> None:
         check(lib.rbc_ctx_set_codec(self._p, {"auto": 0, "matrix": 1, "fft": 2}[codec]), "rbc_ctx_set_codec")
 

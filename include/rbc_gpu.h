@@ -86,11 +86,15 @@ int rbc_ctx_codec(const rbc_ctx *ctx, int *codec); /* effective: MATRIX or FFT *
 /* Wave issue priority (0..3, the SIMD arbiter's s_setprio level) of this
  * context's commit-side kernels (encode, leaf hashing, tree build) and
  * receive-side kernels (ECHO verify, interpolate's hashing, root recheck,
- * digest).  Interpolate's GF transforms (missing-data rows, re-encode) take
- * the commit level, like the commit side's own transform.  Only matters when
- * both sides run concurrently on two streams; results are identical either
- * way.  Default 0 / 0. */
+ * digest).  Only matters when both sides run concurrently on two streams;
+ * results are identical either way.  Default 0 / 0. */
 int rbc_ctx_set_wave_priority(rbc_ctx *ctx, int commit_prio, int receive_prio);
+/* Levels of interpolate's two GF transforms: the missing-data-row GEMV and
+ * the FFT re-encode (the matrix codec's decode product takes the second).
+ * -1 = the commit side's level (default), like the commit side's own
+ * transform.  Which side they should side with depends on which stream
+ * limits the pipelined step. */
+int rbc_ctx_set_decode_priority(rbc_ctx *ctx, int gemv_prio, int reencode_prio);
 
 /* ---- device memory / streams / events (so a host runtime needs no other
  *      GPU library to drive the rbc_dev_* path) ---------------------------- */

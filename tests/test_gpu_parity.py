@@ -1397,15 +1397,17 @@ def test_receive_step_rejects_aliased_batches(gpu, ref):
 
 
 def test_wave_priority_changes_no_result(gpu, ref):
-    """rbc_ctx_set_wave_priority only reorders issue on the SIMDs: commit and
-    receive at priority 0/0 and 3/3 (and the bench's 0/2) give identical
-    shards, roots, branches, valid masks, values, digests and statuses; a
-    level outside 0..3 is rejected."""
+    """rbc_ctx_set_wave_priority / rbc_ctx_set_decode_priority only reorder
+    issue on the SIMDs: commit and receive at 0/0 and 3/3, the bench's 0/2 with
+    the GEMV at the receive level, and mixed levels give identical shards,
+    roots, branches, valid masks, values, digests and statuses; a level outside
+    0..3 (-1 allowed for the decode levels) is rejected."""
     n, f, B, I = 128, 42, 1 << 16, 64
     outs = []
-    for tx, rx in ((0, 0), (3, 3), (0, 2)):
+    for tx, rx, gv, rv in ((0, 0, -1, -1), (3, 3, -1, -1), (0, 2, 2, -1), (1, 0, 3, 2)):
         pl = Pipeline(gpu, n, f, B, I, seed=4242, corrupt_frac=0.3)
         pl.ctx.set_wave_priority(tx, rx)
+        pl.ctx.set_decode_priority(gv, rv)
         pl.commit()
         pl.receive()
         gpu.rbc.lib.rbc_device_sync(0)
@@ -1417,6 +1419,9 @@ def test_wave_priority_changes_no_result(gpu, ref):
     for bad in ((4, 0), (0, -1)):
         with pytest.raises(gpu.RBCError):
             pl.ctx.set_wave_priority(*bad)
+    for bad in ((4, 0), (0, -2)):
+        with pytest.raises(gpu.RBCError):
+            pl.ctx.set_decode_priority(*bad)
 
 
 @pytest.mark.parametrize("n,f", [(16, 5), (256, 85)])
