@@ -1623,7 +1623,9 @@ hipError_t rbc_launch_sha_rx(const ShaArgs &v, const ShaArgs &r, bool v_walk, hi
     if ((v.count > 0 && (!v.rows || (v_walk && (!v.valid || !v.roots)))) || (r.count > 0 && (!r.list || !r.list_count)))
         return hipErrorInvalidValue;
     // one-wave blocks: 4.78-4.82 ms per C2 receive step against 5.03 with
-    // 256-thread blocks (tools/gpu_r02tpb.sh)
+    // 256-thread blocks (tools/gpu_r02tpb.sh); in round 3's pipeline, C2
+    // 526-531 GB/s against 477-486 (256) and 439-447 (128), C1 and C4 within
+    // 3 % (tools/gpu_runs/gpu_r03y.sh)
     constexpr int tpb = 64;
     hipLaunchKernelGGL(sha_rx_kernel, dim3((unsigned)((total + tpb - 1) / tpb)), dim3(tpb), 0, st, v, r, v_walk ? 1 : 0);
     return hipGetLastError();
