@@ -308,6 +308,12 @@ void rbc_batcher::finish(Pending &P) {
         });
     }
     if (P.pin) pool.push_back(std::move(P.pin));  // the launch is complete: its buffers are free
+    {  // count the launch before any of its requests reads as done: a client
+       // that saw its last request complete then sees it in rbc_batcher_stats
+        std::lock_guard<std::mutex> lk(mu);
+        batches++;
+        requests += count;
+    }
     uint64_t touched = 0;  // bit per shard
     for (int i = 0; i < count; ++i) {
         const int sh = (int)(b[i].ticket % kShards);
@@ -317,9 +323,6 @@ void rbc_batcher::finish(Pending &P) {
     }
     for (int sh = 0; sh < kShards; ++sh)
         if (touched >> sh & 1) shard[sh].cv.notify_all();
-    std::lock_guard<std::mutex> lk(mu);
-    batches++;
-    requests += count;
 }
 
 // Worker: coalesce, submit asynchronously, and complete launches in order.

@@ -348,6 +348,13 @@ int main(int argc, char **argv) {
             default: fuzz_receive_step(g); break;
         }
         EXPECT(rbc_strerror((int)rnd(40) - 30) != nullptr);
+        {  // issue levels: 0..3, and -1 (the commit level) for the decode transforms
+            const int a = (int)rnd(7) - 2, b = (int)rnd(7) - 2;
+            const bool ok_w = a >= 0 && a <= 3 && b >= 0 && b <= 3, ok_d = a >= -1 && a <= 3 && b >= -1 && b <= 3;
+            EXPECT(rbc_ctx_set_wave_priority(g.ctx, a, b) == (ok_w ? RBC_OK : RBC_ERR_INVALID_ARG));
+            EXPECT(rbc_ctx_set_decode_priority(g.ctx, b, a) == (ok_d ? RBC_OK : RBC_ERR_INVALID_ARG));
+            EXPECT(rbc_ctx_set_decode_priority(nullptr, 0, 0) == RBC_ERR_INVALID_ARG);
+        }
         EXPECT(rbc_wait(g.ctx, 0) == RBC_ERR_INVALID_ARG);
         EXPECT(rbc_wait(g.ctx, (uint64_t)1 << 60) == RBC_ERR_INVALID_ARG);
     }
