@@ -115,7 +115,18 @@ def parse_args(argv):
     ap.add_argument("--oracle-samples", type=int, default=16,
                     help="instances whose root and digest are checked against the C oracle after timing")
     ap.add_argument("--watchdog-scale", type=float, default=1.0, help="multiplies every stage deadline")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    # checked before any rank starts or touches a GPU
+    if args.wave_prio and not _levels_ok(args.wave_prio, ()):
+        ap.error("--wave-prio takes two levels 0..3, e.g. 0,2")
+    if args.decode_prio and not _levels_ok(args.decode_prio, ("c", "r")):
+        ap.error("--decode-prio takes two of c, r or 0..3, e.g. r,c")
+    return args
+
+
+def _levels_ok(text, names):
+    parts = text.split(",")
+    return len(parts) == 2 and all(x in names or x in ("0", "1", "2", "3") for x in parts)
 
 
 def hbm_plan(I, n, d, spitch, vpitch, opitch, join, world_gather, free, sharing, budget_arg):
