@@ -51,11 +51,9 @@ CONFIGS = {
     "c3": (128, 42, 4 << 20, 1024, "N=128 f=42 4MiB"),
     "c4": (256, 85, 64 << 10, 16384, "N=256 f=85 64KiB"),
 }
-# Issue level of interpolate's missing-data GEMV and FFT re-encode under the
-# pipelined schedule ("c": the commit side's, "r": the receive side's).  The
-# GEMV siding with the receiver balances the streams at N = 128 (C2 +3 %, C3
-# +2 %) and starves the leaf hashing at C1, whose 1,024 leaf waves are one per
-# SIMD (-8 %); C4 is indifferent (tools/gpu_runs/gpu_r03t.sh).
+# Pipelined issue level of interpolate's GEMV / FFT re-encode (c: commit side, r: receive side):
+# the GEMV at r balances the streams at N = 128 and starves C1's one-wave-per-SIMD leaf hashing
+# (tools/gpu_runs/gpu_r03t.sh)
 DECODE_PRIO = {"c1": "c,c", "c2": "r,c", "c3": "r,c", "c4": "r,c"}
 METRIC = "RBC shard GB/s (RS encode+decode + Merkle verify) per GPU & node, N=128"
 SEED = 20261015
