@@ -123,8 +123,7 @@ def parse_args(argv):
 
 
 def _levels_ok(text, names):
-    parts = text.split(",")
-    return len(parts) == 2 and all(x in names or x in ("0", "1", "2", "3") for x in parts)
+    return len(text.split(",")) == 2 and all(x in names + ("0", "1", "2", "3") for x in text.split(","))
 
 
 def hbm_plan(I, n, d, spitch, vpitch, opitch, join, world_gather, free, sharing, budget_arg):
