@@ -26,7 +26,7 @@
 // Modes: ENCODE reads data row j straight from the value bytes at j*S (Split,
 // zero pad by masking) and writes data + parity rows; DECODE reads the k data
 // rows of an already completed data half (interpolate: the missing data rows
-// are regenerated first by gf_rows_kernel) and writes the parity positions by
+// are regenerated first by gf_regen_kernel) and writes the parity positions by
 // class: 0 skip (used), 1 store (missing), 2 compare (valid but unused: store,
 // flag and queue for re-hash only if the re-encoding differs).
 #include <utility>
