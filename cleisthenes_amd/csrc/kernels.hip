@@ -1610,6 +1610,9 @@ hipError_t rbc_launch_sha_rows(const ShaArgs &a, bool verify, hipStream_t st) {
     // the kernel's time is set by the SIMD that holds the most waves, and
     // 4-wave blocks spread them evenly (C2 leaves alone: 2.07 ms; one-wave
     // blocks 2.97, 128-thread 3.05; tools/gpu_r02shatpb.sh)
+    // (under round 3's pipeline too: one-wave / 128-thread blocks for the
+    // leaf hashing give C2 497-503 against 529-532 GB/s, C1 374-392 against
+    // 469-477; tools/gpu_runs/gpu_r03ze.sh)
     dim3 grid((unsigned)((total + 255) / 256));
     if (verify) hipLaunchKernelGGL(sha_rows_kernel<true>, grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(sha_rows_kernel<false>, grid, dim3(256), 0, st, a);
