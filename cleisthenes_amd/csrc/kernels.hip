@@ -234,9 +234,9 @@ __global__ __launch_bounds__(TPB, (RC <= 21 ? 3 : 2)) void gf_rows_kernel(GfArgs
 // missing rows of each instance.
 //
 // One block per (instance, column tile); a tile is 64 lanes x W words.  The
-// block's NW waves split the instance's m missing rows between them in groups
-// of 4 (at most RC rows a wave; a pass holds NW * RC rows, i.e. all but a
-// few C1-C4 instances in one), and each reads the k input rows of the tile.
+// block's NW waves split the instance's m missing rows evenly between them
+// (at most RC rows a wave; a pass holds NW * RC rows, i.e. all but a few
+// C1-C4 instances in one), and each reads the k input rows of the tile.
 // They share them through the CU's L1 / the XCD's L2 only as far as they stay
 // in step: PMC reads are 1.29x (C2) / 1.68x (C4) of the algorithmic k*S.  A block
 // barrier every trip keeps them in step (1.08x / 1.12x) and costs 0.5-2 % of
@@ -255,12 +255,20 @@ template <int V>
 struct IntC {
     static constexpr int value = V;
 };
+// f(IntC<rows>{}) for a runtime rows in [I, MAX]
+template <int I, int MAX, class F>
+__device__ __forceinline__ void dispatch_rows(int rows, F &&f) {
+    if constexpr (I <= MAX) {
+        if (rows == I) f(IntC<I>{});
+        else dispatch_rows<I + 1, MAX>(rows, f);
+    }
+}
 
 // <= 128 VGPRs (4 waves per SIMD); a cap of 2 waves measured the same
 // under the pipeline (tools/gpu_runs/gpu_r03j.sh)
 template <int W, int RC, int JC, int NW>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) void gf_regen_kernel(GfArgs a) {
-    static_assert(JC % 4 == 0 && RC % 4 == 0, "two input pairs per trip, rows in groups of 4");
+    static_assert(JC % 4 == 0, "two input pairs per trip");
     set_wave_prio(a.prio);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // the wave index is uniform per wave: readfirstlane tells the compiler,
@@ -306,12 +314,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) vo
         return x;
     };
 
-    // one pass = up to 2 RC rows, split between the waves (wave-uniform;
-    // see the loop below).  The pass body is instantiated per count of 4-row
-    // groups NG, so the unrolled multiply-accumulate is straight-line: a
-    // per-row exit inside it costs the compiler ~2x the registers (spills).
-    auto pass = [&](auto ngc, int r0, int rows) {
-        constexpr int NG = decltype(ngc)::value, RG = 4 * NG;
+    // one pass = up to NW * RC rows, split between the waves (wave-uniform;
+    // see the loop below).  The pass body is instantiated per row count RG,
+    // so the unrolled multiply-accumulate is straight-line: a per-row exit
+    // inside it costs the compiler ~2x the registers (spills).
+    auto pass = [&](auto rgc, int r0, int rows) {
+        constexpr int RG = decltype(rgc)::value;
         uint32_t acc[RG][W];
 #pragma unroll
         for (int r = 0; r < RG; ++r)
@@ -381,24 +389,20 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) vo
             }
         }
     };
-    // a pass covers up to NW * RC rows: its G groups of 4 (the last one
-    // padded with zero-table rows) go evenly to the fewest waves that hold
-    // them; a wave left idle ends at once (every pass but the last is full)
-    constexpr int GPW = RC / 4;  // groups per wave at most
+    // a pass covers up to NW * RC rows; they go evenly to the fewest waves
+    // that hold them, each wave running the body for exactly its row count
+    // (round 3's 4-row groups padded ~1.5 zero-table rows a pass: ~10 % of
+    // the multiplies at C1-C4); a wave left idle ends at once (every pass
+    // but the last is full)
     for (int base = 0; base < m; base += NW * RC) {
         const int mp = min(NW * RC, m - base);
-        const int G = (mp + 3) >> 2;
-        const int nw = (G + GPW - 1) / GPW;  // active waves (block-uniform)
-        const int q = G / nw, rem = G - q * nw;
-        const int g0 = wave * q + min(wave, rem), ng = wave < nw ? q + (wave < rem) : 0;
-        const int r0 = base + 4 * g0;
-        const int rows = min(4 * ng, mp - 4 * g0);
-        static_assert(RC <= 16, "up to 4 row groups per wave");
-        if (ng == 1) pass(IntC<1>{}, r0, rows);
-        else if (ng == 2) pass(IntC<2>{}, r0, rows);
-        else if (RC >= 12 && ng == 3) pass(IntC<(RC >= 12 ? 3 : 1)>{}, r0, rows);
-        else if (RC >= 16 && ng == 4) pass(IntC<(RC >= 16 ? 4 : 1)>{}, r0, rows);
-        else return;  // idle: only in the last pass
+        const int nw = (mp + RC - 1) / RC;  // active waves (block-uniform)
+        const int q = mp / nw, rem = mp - q * nw;
+        const int rows = wave < nw ? q + (wave < rem) : 0;
+        if (rows == 0) return;  // idle: only in the last pass
+        const int r0 = base + wave * q + min(wave, rem);
+        static_assert(RC <= 16, "up to 16 rows per wave");
+        dispatch_rows<1, RC>(rows, [&](auto rgc) { pass(rgc, r0, rows); });
     }
 }
 
