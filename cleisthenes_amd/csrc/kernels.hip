@@ -416,13 +416,7 @@ template <bool VERIFY>
 // SHA launches (2,048 waves each at C2) must be resident together, 4 waves
 // per SIMD, so every kernel that hashes rows is held to <= 128 VGPRs
 // (the verify walk then spills 36 B per lane, outside the block loop)
-#ifndef RBC_SHA_WPE
-#define RBC_SHA_WPE 4
-#endif
-#ifndef RBC_RX_WPE
-#define RBC_RX_WPE 4
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RBC_SHA_WPE))) void sha_rows_kernel(ShaArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void sha_rows_kernel(ShaArgs a) {
     set_wave_prio(a.prio);
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     int inst, pos;
@@ -495,7 +489,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RBC_SHA_WPE
 // t-1's regen hashing is a latency-bound tail (42 rows x 1024 instances at
 // C2 = 672 waves of 373 serial compressions for 1,024 SIMDs) and the
 // verify 1,376 waves; together they are 2,048 waves, as full as the leaves.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RBC_RX_WPE))) void sha_rx_kernel(ShaArgs v, ShaArgs r, int v_walk) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void sha_rx_kernel(ShaArgs v, ShaArgs r, int v_walk) {
     set_wave_prio(v.prio);
     int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int nv = v.count <= 0 ? 0 : (v.list ? (int)*v.list_count : v.count * v.rows_per_inst);

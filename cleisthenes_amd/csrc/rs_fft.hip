@@ -133,10 +133,7 @@ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 template <int V>
 using IC = std::integral_constant<int, V>;
 
-#ifndef RBC_FFT_SB
-#define RBC_FFT_SB 4
-#endif
-constexpr int SB = RBC_FFT_SB;  // sub-transforms of >= 2^SB rows are scheduled one after the other
+constexpr int SB = 4;  // sub-transforms of >= 2^SB rows are scheduled one after the other
 
 // All 2^M evaluations on coset LAM + V_M, in place, of the polynomial whose
 // novel coefficients are v[OFF .. OFF+2^M) (rows >= NZ are zero, never read).
@@ -274,10 +271,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void rs
     set_wave_prio(a.prio);
     constexpr int W = 1 << LOGW;
     constexpr int G = 3;   // encode: outputs are stored in groups of 2^G rows
-#ifndef RBC_FFT_GD
-#define RBC_FFT_GD 2
-#endif
-    constexpr int GD = RBC_FFT_GD;  // decode: compare-pipeline group (VGPRs: 1 -> 143, 2 -> 157, 3 -> 181)
+    constexpr int GD = 2;  // decode: compare-pipeline group (VGPRs: 1 -> 143, 2 -> 157, 3 -> 181)
     static_assert(K >= 1 && K <= N && N <= W && 2 * N > W, "geometry");
     // XCD-aware tile order: the dispatcher deals workgroups round-robin over
     // the 8 XCDs (linear id % 8), so neighbouring column tiles of one instance
@@ -287,10 +281,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void rs
     // gives each XCD a contiguous run of tiles, so the shared lines hit in
     // that XCD's L2 instead of being fetched twice from HBM.
     uint32_t tile_x = blockIdx.x, tile_y = blockIdx.y;
-#ifndef RBC_XCD_REMAP
-#define RBC_XCD_REMAP 1
-#endif
-    if constexpr (MODE == GF_MODE_ENCODE && RBC_XCD_REMAP) {
+    if constexpr (MODE == GF_MODE_ENCODE) {
         const uint32_t gx = gridDim.x, total = gx * gridDim.y, t8 = total & ~7u;
         uint32_t lin = blockIdx.y * gx + blockIdx.x;
         if (lin < t8) lin = (lin & 7u) * (t8 >> 3) + (lin >> 3);
