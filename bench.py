@@ -365,8 +365,38 @@ def run(args, world, rank, local_rank, wd, out):
     else:
         last, rb_last = sets[0], rxb[0]
     stage_ms = spans(ev_sets[: args.steps], args.faults_on if pipe else None)
-    checks = check_results(args, ca, synth, acs, rdz, dev, stream, world, first, I, total, slots, n, f, k, B, S,
-                           spitch, vpitch, opitch, d_values, last, rb_last, d_gather, d_count, gather)
+    timed = check_batch(args, ca, dev, stream, I, n, k, B, S, spitch, vpitch, opitch, d_values, last, rb_last,
+                        d_count)
+
+    def poisoned_receive():
+        """The receive guard: a fresh commit whose every row the receiver must
+        regenerate (absent, or the corrupted ECHO) is overwritten with seeded
+        garbage before the same receive path runs on it, so a decode that
+        skips a row cannot pass on the proposer's intact bytes."""
+        sp, rb = sets[0], rxb[0]
+        if args.join:  # the joined values of the timed batch are this input's too: overwrite them first
+            ca.rbc.fill_random(dev, stream.ptr, rb["out"], 0, I, opitch, SEED + 2)
+        commit(stream, sp, None)
+        ca.rbc.poison_rows(dev, stream.ptr, sp["shards"], n * spitch, spitch, n, d_present, d_corrupt, I, SEED + 1)
+        ctx.dev_inject_faults(stream.ptr, I, sp["shards"], spitch, d_corrupt)
+        if pipe:  # the timed receiver: rbc_dev_receive_step, then the flush that completes the batch
+            cur = ctx.rx_batch(I, sp["shards"], spitch, None, S, sp["branches"], sp["roots"], d_present, rb["valid"],
+                               rb["leaves_r"], *vpo(rb), rb["digests"], rb["status"])
+            ctx.dev_receive_step(stream.ptr, cur, None)
+            ctx.dev_receive_step(stream.ptr, None, cur)
+        else:
+            ctx.dev_verify(stream.ptr, I, sp["shards"], spitch, None, S, sp["branches"], sp["roots"], d_present,
+                           rb["valid"], rb["leaves_r"])
+            ctx.dev_interpolate(stream.ptr, I, sp["shards"], spitch, None, S, rb["valid"], rb["leaves_r"], 1,
+                                sp["roots"], *vpo(rb), rb["digests"], rb["status"])
+        return sp, rb
+
+    # the timed batch's gathered records are checked before its buffers are reused
+    checks = check_results(args, synth, acs, rdz, world, first, I, total, slots, n, f, k, B, vpitch, last, timed,
+                           d_gather, gather)
+    pset, prb = poisoned_receive()
+    poisoned = check_batch(args, ca, dev, stream, I, n, k, B, S, spitch, vpitch, opitch, d_values, pset, prb, d_count)
+    checks = fold_guard(args, synth, rdz, first, I, total, n, f, k, B, vpitch, checks, timed, poisoned)
 
     ms_per_step = elapsed_max * 1000.0 / args.steps
     value = total * n * S * args.steps / elapsed_max / 1e9
@@ -388,7 +418,7 @@ def run(args, world, rank, local_rank, wd, out):
         import host_bench
         pcie = host_bench.measure(ca, n, f, B, batch=64, batches=8, inflight=2, pinned=True, device=dev)
         pcie["unit"] = "GB/s of committed shard bytes (N*S per instance), host memory in and out"
-    ranks = rdz.allgather(me)
+    ranks, skew = rank_timing(rdz, me, elapsed, args.steps, stage_ms)
     line = {
         "metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
         "warmup": warm, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": scaling,
@@ -414,12 +444,14 @@ def run(args, world, rank, local_rank, wd, out):
                                 f"recheck(t-2), decode(t-1) (rbc_dev_receive_step), two streams, {nsets} shard "
                                 "sets") if pipe else "serial"},
         **rep, **checks, "cpu_baseline": cpu, "pcie_inclusive": pcie, "rccl": rccl, "ranks": ranks,
+        "rank_skew": skew, "library": ca.rbc.library_path(),
         "host": {kk: host[kk] for kk in ("cpu_model", "nproc", "cgroup_cpu_quota", "affinity_cpus")},
     }
     ok = all(checks[c] for c in ("values_ok", "oracle_sample_ok", "gather_ok")) and checks["decoded_ok"] == total
     wd.leave()
     if not ok:
-        print(json.dumps({"error": "correctness check failed", **checks}), file=sys.stderr, flush=True)
+        print(json.dumps({"error": "correctness check failed", **checks, "library": line["library"]}),
+              file=sys.stderr, flush=True)
         rdz.close()
         return 3
     if rank == 0:
@@ -427,6 +459,21 @@ def run(args, world, rank, local_rank, wd, out):
     rdz.barrier()
     rdz.close()
     return 0
+
+
+def rank_timing(rdz, me, elapsed, steps, stage_ms):
+    """Every rank's record (device, bus, NUMA node, RCCL ranks) with its own
+    timed wall time, ms per step and stage spans, gathered to all ranks, and
+    the skew between the slowest and the fastest rank: a slow or mis-placed
+    rank of a multi-GPU run shows by name, not only in the max."""
+    me = dict(me, elapsed_s=round(elapsed, 6), ms_per_step=round(elapsed * 1000.0 / steps, 4),
+              stage_ms={kk: round(v, 4) for kk, v in stage_ms.items()})
+    ranks = rdz.allgather(me)
+    el = [r["elapsed_s"] for r in ranks]
+    skew = {"elapsed_min_s": min(el), "elapsed_max_s": max(el), "slowest_rank": ranks[int(np.argmax(el))]["rank"],
+            "fastest_rank": ranks[int(np.argmin(el))]["rank"],
+            "max_over_min": round(max(el) / min(el), 4) if min(el) > 0 else None}
+    return ranks, skew
 
 
 def spans(ev_sets, faults_on):
@@ -551,25 +598,29 @@ def report(args, ctx, I, n, k, d, S, present_h, corrupt_h, stage_ms, iso, elapse
     return out
 
 
-def check_results(args, ca, synth, acs, rdz, dev, stream, world, first, I, total, slots, n, f, k, B, S, spitch,
-                  vpitch, opitch, d_values, last, rb, d_gather, d_count, gather):
-    """After the timed loop: every instance decoded, every decoded value equals
-    its input, the gathered records of every rank are what that rank holds,
-    and sampled roots / digests equal the C oracle's (checker only: nothing
-    here is timed or shipped)."""
+def check_batch(args, ca, dev, stream, I, n, k, B, S, spitch, vpitch, opitch, d_values, sp, rb, d_count):
+    """One received batch on the device: statuses, and every decoded value
+    against its input (the joined value, or the row view's k data rows)."""
     stream.sync()
-    status = rb["status"].download(I * 4).view(np.int32)
-    n_ok = rdz.sum(int((status == 0).sum()))
+    status = rb["status"].download(I * 4).view(np.int32).copy()
     if args.join:
         ca.rbc.count_mismatch(dev, stream.ptr, rb["out"], opitch, d_values, vpitch, I, B, d_count)
     else:  # the row view: the k data rows of the shard set are the value
-        ca.rbc.count_mismatch_rows(dev, stream.ptr, last["shards"], n * spitch, spitch, k, S, d_values, vpitch, B, I,
+        ca.rbc.count_mismatch_rows(dev, stream.ptr, sp["shards"], n * spitch, spitch, k, S, d_values, vpitch, B, I,
                                    d_count)
     stream.sync()
-    mism = int(d_count.download(4).view(np.uint32)[0])
-    values_ok = rdz.all(mism == 0)
-    roots = last["roots"].download(I * 32).reshape(I, 32)
-    digests = rb["digests"].download(I * 32).reshape(I, 32)
+    return {"status": status, "mism": int(d_count.download(4).view(np.uint32)[0]),
+            "roots": sp["roots"].download(I * 32).reshape(I, 32),
+            "digests": rb["digests"].download(I * 32).reshape(I, 32)}
+
+
+def check_results(args, synth, acs, rdz, world, first, I, total, slots, n, f, k, B, vpitch, last, timed, d_gather,
+                  gather):
+    """After the timed loop, the last timed batch: every instance decoded,
+    every decoded value equals its input, the gathered records of every rank
+    are what that rank holds, and sampled roots / digests equal the C
+    oracle's (checker only: nothing here is timed or shipped)."""
+    status, roots, digests = timed["status"], timed["roots"], timed["digests"]
     gather_ok = True
     if gather:
         mine = acs.pack_records(roots, digests, slots, status)
@@ -579,20 +630,47 @@ def check_results(args, ca, synth, acs, rdz, dev, stream, world, first, I, total
                         for r in range(world))
         gather_ok = rdz.all(gather_ok and [o["instance"] for o in acs.assemble_output_set(g, total, world)]
                             == list(range(total)))
-    sample_ok, checked = True, 0
-    if args.oracle_samples > 0:  # evenly spaced global ids, each checked by its owner
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import rbc_ref
-        for g_id in sorted(set(np.linspace(0, total - 1, min(args.oracle_samples, total)).astype(int).tolist())):
-            if first <= g_id < first + I:
-                i = g_id - first
-                _, root, _, leaves = rbc_ref.encode_commit(n, f, synth.row(SEED, g_id, vpitch, B))
-                dig = rbc_ref.sha256(np.ascontiguousarray(leaves[:k]).tobytes())
-                sample_ok = sample_ok and bytes(roots[i]) == root and bytes(digests[i]) == dig and status[i] == 0
-                checked += 1
-        sample_ok, checked = rdz.all(sample_ok), rdz.sum(checked)
-    return {"decoded_ok": n_ok, "values_ok": values_ok, "value_mismatch_chunks": mism, "gather_ok": gather_ok,
-            "oracle_sample_ok": sample_ok, "oracle_samples_checked": checked}
+    return {"gather_ok": gather_ok}
+
+
+def oracle_samples(args, synth, first, I, total, n, f, k, B, vpitch, batches):
+    """Evenly spaced global ids, each checked by its owner: the root and the
+    digest of every given batch against the C restatement."""
+    ok, checked = True, 0
+    if args.oracle_samples <= 0:
+        return ok, checked
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import rbc_ref
+    for g_id in sorted(set(np.linspace(0, total - 1, min(args.oracle_samples, total)).astype(int).tolist())):
+        if first <= g_id < first + I:
+            i = g_id - first
+            _, root, _, leaves = rbc_ref.encode_commit(n, f, synth.row(SEED, g_id, vpitch, B))
+            dig = rbc_ref.sha256(np.ascontiguousarray(leaves[:k]).tobytes())
+            for b in batches:
+                ok = ok and bytes(b["roots"][i]) == root and bytes(b["digests"][i]) == dig and b["status"][i] == 0
+            checked += 1
+    return ok, checked
+
+
+def fold_guard(args, synth, rdz, first, I, total, n, f, k, B, vpitch, checks, timed, poisoned):
+    """decoded_ok / values_ok / oracle_sample_ok hold for BOTH the last timed
+    batch and the poisoned receive (an instance counts as decoded only if it
+    decoded in both); each batch's own figures are kept under `guard`."""
+    both_ok = (timed["status"] == 0) & (poisoned["status"] == 0)
+    sample_ok, checked = oracle_samples(args, synth, first, I, total, n, f, k, B, vpitch, (timed, poisoned))
+    out = {"decoded_ok": rdz.sum(int(both_ok.sum())),
+           "values_ok": rdz.all(timed["mism"] == 0 and poisoned["mism"] == 0),
+           "value_mismatch_chunks": rdz.sum(timed["mism"] + poisoned["mism"]),
+           "gather_ok": checks["gather_ok"],
+           "oracle_sample_ok": rdz.all(sample_ok), "oracle_samples_checked": rdz.sum(checked)}
+    out["guard"] = {
+        "timed_batch": {"decoded": rdz.sum(int((timed["status"] == 0).sum())),
+                        "value_mismatch_chunks": rdz.sum(timed["mism"])},
+        "poisoned_batch": {"decoded": rdz.sum(int((poisoned["status"] == 0).sum())),
+                           "value_mismatch_chunks": rdz.sum(poisoned["mism"]),
+                           "note": "a fresh commit whose absent and corrupted rows were overwritten with seeded "
+                                   "garbage (rbc_dev_poison_rows) before the receive path ran on it"}}
+    return out
 
 
 def cpu_baseline(args, host):

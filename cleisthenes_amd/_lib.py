@@ -11,8 +11,10 @@ import re
 from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# RBC_GPU_LIB_AB: an alternative build of the same library for A/B runs (tools/build_ab.sh)
-LIB_PATH = os.environ.get("RBC_GPU_LIB_AB") or os.path.join(_HERE, "librbc_gpu.so")
+# RBC_GPU_LIB: another build of the same ABI (an A/B candidate from tools/build_ab.sh, or a
+# test-only mutant from tests/mutants that the guard tests expect to FAIL); the bench line
+# records the file actually mapped (rbc_library_path, dladdr) so a run says what it measured
+LIB_PATH = os.environ.get("RBC_GPU_LIB") or os.path.join(_HERE, "librbc_gpu.so")
 INCLUDE_DIR = os.path.join(os.path.dirname(_HERE), "include")
 HEADER_PATH = os.path.join(INCLUDE_DIR, "rbc_gpu.h")
 
@@ -46,6 +48,7 @@ class RxMarks(ctypes.Structure):
 _SIGS = {
     "rbc_strerror": (c_char_p, [c_int]),
     "rbc_abi_version": (c_int, []),
+    "rbc_library_path": (c_int, [c_char_p, c_size_t]),
     "rbc_device_count": (c_int, [POINTER(c_int)]),
     "rbc_ctx_create": (c_int, [c_int, c_int, c_int, POINTER(c_void_p)]),
     "rbc_ctx_destroy": (None, [c_void_p]),
@@ -134,6 +137,8 @@ _SIGS = {
                                        c_void_p]),
     "rbc_dev_count_mismatch_rows": (c_int, [c_int, c_void_p, c_void_p, c_uint64, c_uint32, c_int, c_uint32, c_void_p,
                                             c_uint64, c_uint32, c_uint64, c_void_p]),
+    "rbc_dev_poison_rows": (c_int, [c_int, c_void_p, c_void_p, c_uint64, c_uint32, c_int, c_void_p, c_void_p,
+                                    c_uint64, c_uint64]),
     # include/rbc_protocol.h
     "rbc_pb_encode_rbc": (c_size_t, [c_int, c_void_p, c_size_t, c_void_p, c_size_t]),
     "rbc_pb_decode_rbc": (c_int, [c_void_p, c_size_t, POINTER(c_int), POINTER(c_void_p), szp]),

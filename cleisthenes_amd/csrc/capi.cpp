@@ -496,7 +496,9 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
         g.status = status;
         g.rcount = pa.rcount;
         g.prio = c->gemv_prio();
+#ifndef RBC_MUTANT_SKIP_REGEN  // tests/mutants only: a build that never regenerates, which the guards must catch
         RBC_HIP(rbc_launch_gf_regen(g, st));
+#endif
         // 2) parity positions: additive-FFT re-encode of the completed data half
         FftArgs a{};
         a.count = count;
@@ -924,6 +926,16 @@ const char *rbc_strerror(int s) {
 }
 
 int rbc_abi_version(void) { return RBC_ABI_VERSION; }
+
+int rbc_library_path(char *out, size_t cap) {
+    if (!out || cap == 0) return RBC_ERR_INVALID_ARG;
+    Dl_info info;
+    if (!dladdr(reinterpret_cast<void *>(&rbc_library_path), &info) || !info.dli_fname) return RBC_ERR_INVALID_ARG;
+    char real[PATH_MAX];
+    const char *p = realpath(info.dli_fname, real) ? real : info.dli_fname;
+    snprintf(out, cap, "%s", p);
+    return RBC_OK;
+}
 
 int rbc_device_count(int *count) {
     if (!count) return RBC_ERR_INVALID_ARG;
@@ -2260,6 +2272,17 @@ int rbc_dev_count_mismatch_rows(int device, void *stream, const uint8_t *shards,
     RBC_HIP(hipMemsetAsync(mismatch_dev, 0, sizeof(uint32_t), st));
     RBC_HIP(rbc_launch_count_mismatch_rows(shards, inst_pitch, row_pitch, k, shard_len, values, value_pitch, value_len,
                                            count, mismatch_dev, st));
+    return RBC_OK;
+}
+
+int rbc_dev_poison_rows(int device, void *stream, uint8_t *shards, uint64_t inst_pitch, uint32_t row_pitch, int n,
+                        const uint8_t *present, const int32_t *corrupt, uint64_t count, uint64_t seed) {
+    if (n <= 0 || (count && !shards) || row_pitch % 16 || inst_pitch % 16 || (uintptr_t)shards % 16 ||
+        (uint64_t)n * row_pitch > inst_pitch)
+        return RBC_ERR_INVALID_ARG;
+    RBC_HIP(hipSetDevice(device));
+    RBC_HIP(rbc_launch_poison_rows(shards, inst_pitch, row_pitch, n, present, corrupt, count, seed,
+                                   as_stream(stream)));
     return RBC_OK;
 }
 

@@ -220,3 +220,7 @@ hipError_t rbc_launch_count_mismatch(const uint8_t *a, uint64_t a_pitch, const u
 hipError_t rbc_launch_count_mismatch_rows(const uint8_t *shards, uint64_t inst_pitch, uint32_t row_pitch, int k,
                                           uint32_t S, const uint8_t *values, uint64_t value_pitch, uint32_t B,
                                           uint64_t count, uint32_t *counter, hipStream_t st);
+// receive-guard input: absent rows (present == 0) and corrupt[i] filled with seeded garbage
+hipError_t rbc_launch_poison_rows(uint8_t *shards, uint64_t inst_pitch, uint32_t row_pitch, int n,
+                                  const uint8_t *present, const int32_t *corrupt, uint64_t count, uint64_t seed,
+                                  hipStream_t st);

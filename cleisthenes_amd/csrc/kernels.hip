@@ -25,6 +25,8 @@ using namespace rbcdev;
 namespace {
 
 using rsrc_t = __amdgpu_buffer_rsrc_t;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
 constexpr int RBC_RSRC_DW3 = 0x00020000;  // gfx9 raw buffer, bounds-checked
 
 RBC_DEV rsrc_t make_rsrc(const void *p, uint32_t bytes) {
@@ -295,6 +297,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) vo
     const uint8_t *in_inst = a.in + (size_t)inst * a.in_inst_pitch;
     uint8_t *out_inst = a.out + (size_t)inst * a.out_inst_pitch;
     const rsrc_t rin = make_rsrc(in_inst, a.in_inst_bytes);
+    const rsrc_t rout = make_rsrc(out_inst, (uint32_t)a.out_inst_pitch);
     const uint8_t *idx = a.in_idx + (size_t)inst * a.idx_stride;
     // input row starts; the prefetch past K reads row 0 (never accumulated)
     for (int t = lane; t < KP + 8; t += 64) s_off[t] = (t < K ? (uint32_t)idx[t] : 0u) * a.in_row_pitch;
@@ -376,16 +379,38 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) vo
             a1 = load_row(j + 5);
             mac_pair(jl + 2, b0, b1);
         }
-        // zero the bytes past S; never write past the row pitch (word granular)
+        // zero the bytes past S; never write past the row pitch.  Each lane
+        // stores its W words as ONE dwordx4 / dwordx3 (a wave's store then
+        // fills whole 128-B lines; per-word stores wrote a quarter of every
+        // line they touched and PMC showed 1.9x the missing rows' bytes
+        // written).  The pitch is a multiple of 64 B, so only a W = 3 lane of
+        // the row's last tile can straddle it, and only that lane takes the
+        // word-guarded path.
         const int nvalid = (int)S - (int)my_off;
         const uint8_t *oidx = a.out_idx + (size_t)inst * a.idx_stride2 + r0;
+        const bool whole = my_off + 4u * W <= a.out_row_pitch;
+        const bool part = !whole && my_off < a.out_row_pitch;
 #pragma unroll
         for (int r = 0; r < RG; ++r) {
             if (r < rows) {
-                uint32_t *dst = reinterpret_cast<uint32_t *>(out_inst + (size_t)oidx[r] * a.out_row_pitch + my_off);
+                const uint32_t so = uniform((uint32_t)oidx[r] * a.out_row_pitch);
+                uint32_t v[W];
 #pragma unroll
-                for (int w = 0; w < W; ++w)
-                    if (my_off + 4u * w < a.out_row_pitch) dst[w] = acc[r][w] & keep_bytes(nvalid - 4 * w);
+                for (int w = 0; w < W; ++w) v[w] = acc[r][w] & keep_bytes(nvalid - 4 * w);
+                if (whole) {
+                    if constexpr (W == 4) {
+                        __builtin_amdgcn_raw_buffer_store_b128(u32x4{v[0], v[1], v[2], v[3]}, rout, (int)my_off,
+                                                               (int)so, 0);
+                    } else {
+                        __builtin_amdgcn_raw_buffer_store_b96(u32x3{v[0], v[1], v[2]}, rout, (int)my_off, (int)so,
+                                                              0);
+                    }
+                } else if (part) {
+#pragma unroll
+                    for (int w = 0; w < W; ++w)
+                        if (my_off + 4u * w < a.out_row_pitch)
+                            __builtin_amdgcn_raw_buffer_store_b32(v[w], rout, (int)(my_off + 4u * w), (int)so, 0);
+                }
             }
         }
     };
@@ -1422,6 +1447,27 @@ __global__ __launch_bounds__(256) void count_mismatch_rows_kernel(const uint8_t 
     if (bad) atomicAdd(counter, bad);
 }
 
+// The receive guard's input (bench / tests): every row a receiver must
+// regenerate -- absent (present[i][j] == 0) or the one Byzantine row
+// corrupt[i] -- is overwritten across its whole pitch with splitmix64 bytes
+// keyed by (seed, instance, row), so only interpolate's regeneration can put
+// the committed bytes back.  One 16-byte chunk per thread, grid-stride.
+__global__ __launch_bounds__(256) void poison_rows_kernel(uint8_t *shards, uint64_t inst_pitch, uint32_t row_pitch,
+                                                          int n, const uint8_t *present, const int32_t *corrupt,
+                                                          uint64_t count, uint64_t seed) {
+    const uint64_t chunks = row_pitch / 16, per_inst = (uint64_t)n * chunks, total = count * per_inst;
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < total;
+         c += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = c / per_inst, rem = c - i * per_inst, j = rem / chunks, q = rem - j * chunks;
+        const bool gone = (present && present[i * n + j] == 0) || (corrupt && corrupt[i] == (int32_t)j);
+        if (!gone) continue;
+        const uint64_t w0 = seed * 0x9E3779B97F4A7C15ull + ((i * (uint64_t)n + j) << 24) + 2 * q;
+        const uint64_t a = splitmix64(w0), b = splitmix64(w0 + 1);
+        *reinterpret_cast<uint4 *>(shards + i * inst_pitch + j * row_pitch + 16 * q) =
+            make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+    }
+}
+
 // Host batch API, receiver side: move only the PRESENT shard rows of a pinned
 // caller batch into the device rows, reading the host memory directly over
 // PCIe (zero-copy; measured at the DMA engine's rate, tools/probes/
@@ -1515,6 +1561,16 @@ hipError_t rbc_launch_count_mismatch_rows(const uint8_t *shards, uint64_t inst_p
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(count_mismatch_rows_kernel, dim3(8192), dim3(256), 0, st, shards, inst_pitch, row_pitch, k, S,
                        values, value_pitch, B, count, counter);
+    return hipGetLastError();
+}
+hipError_t rbc_launch_poison_rows(uint8_t *shards, uint64_t inst_pitch, uint32_t row_pitch, int n,
+                                  const uint8_t *present, const int32_t *corrupt, uint64_t count, uint64_t seed,
+                                  hipStream_t st) {
+    if (count == 0 || n <= 0 || row_pitch == 0) return hipSuccess;
+    if (row_pitch % 16 || inst_pitch % 16 || ((uintptr_t)shards % 16) || (uint64_t)n * row_pitch > inst_pitch)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(poison_rows_kernel, dim3(8192), dim3(256), 0, st, shards, inst_pitch, row_pitch, n, present,
+                       corrupt, count, seed);
     return hipGetLastError();
 }
 

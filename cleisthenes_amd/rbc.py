@@ -69,6 +69,22 @@ def count_mismatch_rows(device: int, stream, shards, inst_pitch: int, row_pitch:
           "rbc_dev_count_mismatch_rows")
 
 
+def poison_rows(device: int, stream, shards, inst_pitch: int, row_pitch: int, n: int, present, corrupt, count: int,
+                seed: int) -> None:
+    """Overwrite every absent row (present == 0) and the corrupt[i] row of
+    each instance with seeded garbage over the whole row pitch: the receive
+    guard's input, so that only a real regeneration restores them."""
+    check(lib.rbc_dev_poison_rows(device, _dv(stream), _dv(shards), inst_pitch, row_pitch, n, _dv(present),
+                                  _dv(corrupt), count, seed), "rbc_dev_poison_rows")
+
+
+def library_path() -> str:
+    """The file librbc_gpu.so was actually mapped from (dladdr inside the library)."""
+    buf = ctypes.create_string_buffer(4096)
+    check(lib.rbc_library_path(buf, 4096), "rbc_library_path")
+    return buf.value.decode()
+
+
 def _bytes_array(x) -> np.ndarray:
     if x is None:
         return np.zeros(0, dtype=np.uint8)

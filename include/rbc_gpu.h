@@ -64,6 +64,9 @@ extern "C" {
 
 const char *rbc_strerror(int status);
 int rbc_abi_version(void);
+/* The file this library was mapped from (dladdr + realpath), so a caller can
+ * record which build it measured. */
+int rbc_library_path(char *out, size_t cap);
 int rbc_device_count(int *count);
 
 /* ---- context: one (N, f) RBC geometry on one GPU ------------------------
@@ -189,7 +192,7 @@ int rbc_dev_interpolate(rbc_ctx *ctx, void *stream, int count, uint8_t *shards, 
  * values_out / digests are final and equal rbc_dev_verify followed by
  * rbc_dev_interpolate(leaves_verified = 1) on the same inputs (interpolate,
  * rbc/rbc.go:86-90); cur's buffers must stay untouched until the next call's
- * work is done.  While a batch is pending, rbc_dev_interpolate(_phases) on
+ * work is done.  While a batch is pending, rbc_dev_interpolate on
  * the same context returns RBC_ERR_INVALID_ARG (they share its decode
  * workspace).  All pointers are device memory; present may be NULL (all
  * received).  cur and prev may share no output buffer (shards, valid, leaves,
@@ -377,6 +380,13 @@ int rbc_dev_count_mismatch(int device, void *stream, const uint8_t *a, uint64_t 
 int rbc_dev_count_mismatch_rows(int device, void *stream, const uint8_t *shards, uint64_t inst_pitch,
                                 uint32_t row_pitch, int k, uint32_t shard_len, const uint8_t *values,
                                 uint64_t value_pitch, uint32_t value_len, uint64_t count, uint32_t *mismatch_dev);
+/* The receive guard's input: every row a receiver has to regenerate -- absent
+ * (present[i][j] == 0; present nullable = none) or the Byzantine row
+ * corrupt[i] >= 0 (corrupt nullable) -- is overwritten over its whole
+ * row_pitch with seeded splitmix64 garbage, so that a decode which skipped a
+ * row cannot pass on the proposer's intact bytes.  row_pitch % 16 == 0. */
+int rbc_dev_poison_rows(int device, void *stream, uint8_t *shards, uint64_t inst_pitch, uint32_t row_pitch, int n,
+                        const uint8_t *present, const int32_t *corrupt, uint64_t count, uint64_t seed);
 
 #ifdef __cplusplus
 }

@@ -309,6 +309,11 @@ hipError_t rbc_launch_count_mismatch_rows(const uint8_t *, uint64_t, uint32_t, i
     touch(counter, 4);
     return hipSuccess;
 }
+hipError_t rbc_launch_poison_rows(uint8_t *shards, uint64_t inst_pitch, uint32_t, int, const uint8_t *,
+                                  const int32_t *, uint64_t count, uint64_t, hipStream_t) {
+    touch(shards, count * inst_pitch);
+    return hipSuccess;
+}
 hipError_t rbc_launch_marshal_val(const WireArgs &a, hipStream_t) {
     const size_t msgs = (size_t)a.count * a.n;
     if (msgs) touch(a.out, msgs * a.out_pitch);

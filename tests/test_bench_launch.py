@@ -166,3 +166,29 @@ def test_hbm_plan_divides_free_memory_by_the_ranks_sharing_the_device():
     # the row view needs no value buffer: the joined form costs k*S more per instance
     _, need3 = bench.hbm_plan(8192, n, 7, sp, vp, op, True, 0, free, 1, 0)
     assert need3["serial"] - need["serial"] == 8192 * op
+
+
+def test_rank_timing_keys_for_a_three_rank_rehearsal(tmp_path):
+    """bench.rank_timing over 3 ranks: every rank's record carries its own
+    elapsed time, ms per step and stage spans, and the line's skew names the
+    slowest and the fastest rank (what a multi-GPU SCALE run is diagnosed by)."""
+    script = _script(tmp_path, """
+        import bench
+        me = {"rank": rank, "device": rank, "pci_bus_id": f"0000:{rank:02x}:00.0"}
+        stage = {"enc": 1.0 + rank, "leaf": 2.0}
+        ranks, skew = bench.rank_timing(rdz, me, 0.5 + 0.25 * rank, 10, stage)
+        with open(os.path.join(out, f"r{rank}.json"), "w") as f:
+            json.dump({"ranks": ranks, "skew": skew}, f)
+        rdz.close()
+    """)
+    assert launch.spawn_ranks(3, [str(tmp_path)], script) == 0
+    res = [json.load(open(tmp_path / f"r{r}.json")) for r in range(3)]
+    for x in res:
+        assert x == res[0]
+        for r, rec in enumerate(x["ranks"]):
+            assert rec["rank"] == r and rec["device"] == r
+            assert rec["elapsed_s"] == 0.5 + 0.25 * r
+            assert rec["ms_per_step"] == round((0.5 + 0.25 * r) * 100.0, 4)
+            assert rec["stage_ms"] == {"enc": 1.0 + r, "leaf": 2.0}
+        assert x["skew"] == {"elapsed_min_s": 0.5, "elapsed_max_s": 1.0, "slowest_rank": 2, "fastest_rank": 0,
+                             "max_over_min": 2.0}

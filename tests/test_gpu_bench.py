@@ -19,9 +19,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 QUICK = ["--no-cpu-baseline", "--no-pcie", "--oracle-samples", "4"]
 
 
-def _run(args, timeout=300):
+def _run(args, timeout=300, env=None):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
-                       timeout=timeout)
+                       timeout=timeout, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, r.stdout
@@ -37,6 +37,11 @@ def test_bench_schedules_pass_their_guard(pipeline, join):
         assert key in d, key
     assert d["n_gpus"] == 1 and d["steps"] == 3 and d["value"] > 0
     assert d["decoded_ok"] == 96 and d["values_ok"] and d["oracle_sample_ok"] and d["oracle_samples_checked"] == 4
+    g = d["guard"]  # the last timed batch AND a poisoned receive both decode every instance to its input
+    assert g["timed_batch"] == {"decoded": 96, "value_mismatch_chunks": 0}
+    assert g["poisoned_batch"]["decoded"] == 96 and g["poisoned_batch"]["value_mismatch_chunks"] == 0
+    assert d["library"] == os.path.realpath(os.path.join(ROOT, "cleisthenes_amd", "librbc_gpu.so"))
+    assert d["rank_skew"]["slowest_rank"] == 0 and d["ranks"][0]["ms_per_step"] > 0
     assert 0 < d["roofline"]["frac"] < 1 and d["roofline"]["avg_ms"] > 0
     assert d["config"]["hbm_plan"]["schedule"] == ("pipelined" if pipeline else "serial")
     assert d["config"]["value_form"].startswith("joined" if join else "row view")
@@ -106,3 +111,26 @@ def test_bench_falls_back_to_serial_when_the_shard_sets_do_not_fit():
     d = _run(["--instances", "64", "--steps", "3", "--warmup", "2", "--hbm-budget", "1.5e9"] + QUICK)
     assert d["config"]["pipeline"] == "serial" and d["config"]["hbm_plan"]["schedule"] == "serial"
     assert d["decoded_ok"] == 64 and d["values_ok"] and d["oracle_sample_ok"]
+
+
+MUTANT = os.path.join(ROOT, "tests", "mutants", "librbc_gpu_skip_regen.so")
+
+
+@pytest.mark.parametrize("config,join", [("c2", False), ("c4", False), ("c2", True)])
+def test_bench_guard_fails_a_build_that_never_regenerates(config, join):
+    """The guard must not pass a no-op regeneration.  tests/mutants'
+    librbc_gpu_skip_regen.so is the product with gf_regen_kernel never
+    launched: the timed batches still hold the proposer's intact rows in the
+    absent slots and pass, but the poisoned receive cannot, so bench.py exits
+    3 with values_ok and decoded_ok false -- and names the mutant it mapped."""
+    assert os.path.exists(MUTANT), "build() makes tests/mutants"
+    args = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", config, "--instances", "64", "--steps", "3",
+            "--warmup", "3", "--no-isolated"] + QUICK + (["--join"] if join else [])
+    r = subprocess.run(args, capture_output=True, text=True, timeout=300, env=dict(os.environ, RBC_GPU_LIB=MUTANT))
+    assert r.returncode == 3, (r.returncode, r.stderr[-3000:])
+    err = [ln for ln in r.stderr.splitlines() if ln.startswith('{"error"')]
+    assert len(err) == 1, r.stderr[-3000:]
+    e = json.loads(err[0])
+    assert e["guard"]["timed_batch"] == {"decoded": 64, "value_mismatch_chunks": 0}
+    assert e["guard"]["poisoned_batch"]["decoded"] < 64 and e["guard"]["poisoned_batch"]["value_mismatch_chunks"] > 0
+    assert not e["values_ok"] and e["decoded_ok"] < 64 and e["library"] == os.path.realpath(MUTANT)

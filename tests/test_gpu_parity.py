@@ -224,16 +224,55 @@ class Pipeline:
         c.dev_leaves(None, self.I, b["shards"], self.spitch, None, self.S, b["leaves"])
         c.dev_merkle_build(None, self.I, b["leaves"], b["roots"], b["branches"])
 
-    def receive(self):
+    def poison(self, seed=99, present=True):
+        """Overwrite every row the receiver must regenerate -- absent, or the
+        instance's corrupted ECHO -- with seeded garbage over the whole pitch
+        (rbc_dev_poison_rows), so only interpolate's regeneration can restore
+        it (with the proposer's intact rows left in those slots a
+        regeneration that wrote nothing would pass)."""
+        b = self.b
+        self.ca.rbc.poison_rows(0, None, b["shards"], self.n * self.spitch, self.spitch, self.n,
+                                b["present"] if present else None, b["corrupt"], self.I, seed)
+
+    def receive(self, poison=True):
+        """Fault injection, ECHO verify, interpolate (one-shot calls); every row
+        the receiver must regenerate is poisoned first unless the caller did."""
         b, c = self.b, self.ctx
+        if poison:
+            self.poison()
         c.dev_inject_faults(None, self.I, b["shards"], self.spitch, b["corrupt"])
         c.dev_verify(None, self.I, b["shards"], self.spitch, None, self.S, b["branches"], b["roots"],
                      b["present"], b["valid"], b["leaves_r"])
         c.dev_interpolate(None, self.I, b["shards"], self.spitch, None, self.S, b["valid"], b["leaves_r"], 1,
                           b["roots"], b["out"], self.opitch, b["digests"], b["status"])
 
+    def receive_step(self, poison=True):
+        """The timed receiver: rbc_dev_receive_step(cur) then the flush that
+        completes it (verify + decode, then rehash + recheck + digest)."""
+        b, c = self.b, self.ctx
+        if poison:
+            self.poison()
+        c.dev_inject_faults(None, self.I, b["shards"], self.spitch, b["corrupt"])
+        cur = c.rx_batch(self.I, b["shards"], self.spitch, None, self.S, b["branches"], b["roots"], b["present"],
+                         b["valid"], b["leaves_r"], b["out"], self.opitch, b["digests"], b["status"])
+        c.dev_receive_step(None, cur, None)
+        c.dev_receive_step(None, None, cur)
+        self.ca.rbc.lib.rbc_device_sync(0)
+
     def shards(self):
         return self.b["shards"].download().reshape(self.I, self.n, self.spitch)
+
+    def assert_poisoned(self, before, sample=4):
+        """The poison reached the absent / corrupted rows of a few instances
+        and left the received ones alone."""
+        now = self.shards()
+        for i in np.linspace(0, self.I - 1, min(sample, self.I)).astype(int):
+            gone = ~self.present[i].astype(bool)
+            if self.corrupt[i] >= 0:
+                gone[self.corrupt[i]] = True
+            assert np.array_equal(now[i][~gone], before[i][~gone])
+            for j in np.flatnonzero(gone):
+                assert (now[i, j] != before[i, j]).mean() > 0.9, (i, j)
 
     def arr(self, name, dtype=np.uint8, shape=None):
         a = np.frombuffer(self.b[name].download().tobytes(), dtype=dtype)
@@ -264,7 +303,9 @@ def test_device_pipeline_full_size_vs_c_oracle(gpu, ref, name, n, f, B, I):
         assert bytes(roots[i]) == want_root
         assert np.array_equal(brs[i], want_br)
         assert np.array_equal(leaves[i], want_leaves)
-    pl.receive()
+    pl.poison()
+    pl.assert_poisoned(sh)
+    pl.receive(poison=False)
     valid = pl.arr("valid", shape=(I, n))
     status = pl.arr("status", np.int32)
     out = pl.arr("out", shape=(I, pl.opitch))
@@ -299,9 +340,11 @@ BATCH = [
 def test_device_pipeline_every_instance_of_a_bench_batch_vs_c_oracle(gpu, ref, name, n, f, B, I):
     """Every instance of a bench-sized batch against the C restatement: root,
     leaves and the branch of a rotating leaf after commit; valid mask, status,
-    value (k*S bytes) and digest after receive (one corrupted ECHO shard in
-    10% of instances).  The oracle runs on a thread pool (ctypes releases the
-    GIL)."""
+    value (k*S bytes) and digest after the timed receive path
+    (rbc_dev_receive_step; one corrupted ECHO shard in 10% of instances), with
+    every absent and corrupted row poisoned first, and the whole shard set
+    regenerated back to the commit.  The oracle runs on a thread pool (ctypes
+    releases the GIL)."""
     from concurrent.futures import ThreadPoolExecutor
     pl = Pipeline(gpu, n, f, B, I, seed=zlib.crc32(name.encode()))
     pl.commit()
@@ -309,12 +352,16 @@ def test_device_pipeline_every_instance_of_a_bench_batch_vs_c_oracle(gpu, ref, n
     roots = pl.arr("roots", shape=(I, 32))
     leaves = pl.arr("leaves", shape=(I, n, 32))
     brs = pl.arr("branches", shape=(I, n, max(pl.d, 1), 32))
-    pl.receive()
+    pl.poison()
+    pl.assert_poisoned(sh)
+    pl.receive_step(poison=False)
     valid = pl.arr("valid", shape=(I, n))
     status = pl.arr("status", np.int32)
     out = pl.arr("out", shape=(I, pl.opitch))
     digests = pl.arr("digests", shape=(I, 32))
     S, k = pl.S, pl.k
+    after = pl.shards()  # interpolate regenerated every poisoned row in place: the committed shard set again
+    assert np.array_equal(after, sh), name
 
     def check(i):
         _, want_root, want_br, want_leaves = ref.encode_commit(n, f, pl.values[i, :B])
@@ -1073,48 +1120,60 @@ def test_host_interpolate_zero_copy_reads_present_rows_only(gpu, ref, n, f, B, p
 
 
 REGEN_COUNTS = [
-    # (n, f, S, missing data rows per instance): gf_regen_kernel splits an
-    # instance's m rows over the waves of a block in groups of 4 (12 B per lane
-    # for short rows: 3 waves x 16 rows per pass; 16 B per lane: 2 x 12), so
-    # the counts straddle every group, wave and pass boundary of both forms
-    (256, 85, 763, [1, 3, 4, 5, 12, 13, 16, 17, 29, 32, 33, 47, 48, 49, 64, 86]),
-    (128, 42, 23832, [1, 4, 5, 11, 12, 13, 23, 24, 25, 44]),
-    (128, 42, 700, [1, 4, 16, 17, 32, 33, 44]),
+    # (n, f, S, missing data rows per instance, parity rows absent too):
+    # gf_regen_kernel splits an instance's m rows evenly over the fewest
+    # waves of a block that hold them (12 B per lane for short rows: 3 waves
+    # x 16 rows per pass; 16 B per lane: 2 waves x 12), and runs the pass body
+    # for exactly each wave's count, so the counts straddle every wave and
+    # pass boundary of both forms.  With parity rows absent as well, the
+    # first-k set takes the first m present parity rows, not parity 0..m-1
+    (256, 85, 763, [1, 3, 4, 5, 12, 13, 16, 17, 29, 32, 33, 47, 48, 49, 64, 86], False),
+    (128, 42, 23832, [1, 4, 5, 11, 12, 13, 23, 24, 25, 44], False),
+    (128, 42, 700, [1, 4, 16, 17, 32, 33, 44], False),
+    (256, 85, 763, [1, 12, 13, 29, 48, 49, 86], True),
+    (128, 42, 23832, [1, 12, 13, 24, 25, 44], True),
+    (128, 42, 95326, [1, 12, 13, 24, 25, 44], True),  # C3's shard (4 MiB values)
+    (64, 21, 47663, [1, 11, 12, 13, 22], True),       # C1's geometry and shard (1 MiB values)
 ]
 
 
-@pytest.mark.parametrize("n,f,S,ms", REGEN_COUNTS, ids=["n256-short", "n128-long", "n128-short"])
-def test_device_regen_missing_data_row_counts(gpu, n, f, S, ms):
-    """Interpolate with exactly m missing data rows per instance (every parity
-    row present, so the first-k set is the k - m data rows plus the first m
-    parity rows): each regenerated row equals the committed one, zero past S,
-    and the value is the input."""
+@pytest.mark.parametrize("n,f,S,ms,parity_gone", REGEN_COUNTS,
+                         ids=["n256-short", "n128-long", "n128-short", "n256-short-pgone", "c2-pgone", "c3-pgone",
+                              "c1-pgone"])
+def test_device_regen_missing_data_row_counts(gpu, n, f, S, ms, parity_gone):
+    """Interpolate with exactly m missing data rows per instance (and, with
+    parity_gone, a random set of absent parity rows that still leaves >= m):
+    every absent row holds garbage (poisoned), so only the regeneration can
+    restore it; each regenerated row -- data and parity -- equals the committed
+    one, zero past S, and the value is the input.  One-shot interpolate and
+    the receive step, on the same inputs."""
     k = n - 2 * f
+    p = n - k
     I = len(ms)
-    pl = Pipeline(gpu, n, f, k * S, I, seed=n + S, corrupt_frac=0.0)
-    rng = np.random.default_rng(S)
-    pl.present[:] = 1
-    for i, m in enumerate(ms):
-        pl.present[i, rng.permutation(k)[:m]] = 0
-    pl.b["present"].upload(pl.present)
-    pl.commit()
-    committed = pl.shards().copy()
-    # the absent rows hold garbage, so only the regeneration can restore them
-    garbled = committed.copy()
-    for i in range(I):
-        gone = np.flatnonzero(pl.present[i] == 0)
-        garbled[i][gone] = rng.integers(0, 256, size=(len(gone), pl.spitch), dtype=np.uint8)
-    pl.b["shards"].upload(garbled)
-    pl.receive()
-    assert (pl.arr("status", np.int32) == 0).all()
-    out = pl.arr("out", shape=(I, pl.opitch))
-    assert np.array_equal(out[:, : pl.B], pl.values[:, : pl.B])
-    after = pl.shards()
-    for i, m in enumerate(ms):
-        miss = np.flatnonzero(pl.present[i, :k] == 0)
-        assert len(miss) == m
-        assert np.array_equal(after[i][miss], committed[i][miss]), (i, m)
-        assert not after[i][miss, S:].any(), (i, m)
+    for mode in ("oneshot", "step"):
+        pl = Pipeline(gpu, n, f, k * S, I, seed=n + S, corrupt_frac=0.0)
+        rng = np.random.default_rng(S + parity_gone)
+        pl.present[:] = 1
+        for i, m in enumerate(ms):
+            pl.present[i, rng.permutation(k)[:m]] = 0
+            if parity_gone:
+                gone = int(rng.integers(1, p - m + 1))
+                pl.present[i, k + rng.permutation(p)[:gone]] = 0
+        pl.b["present"].upload(pl.present)
+        pl.commit()
+        committed = pl.shards().copy()
+        pl.poison(seed=S)
+        pl.assert_poisoned(committed, sample=I)
+        pl.receive(poison=False) if mode == "oneshot" else pl.receive_step(poison=False)
+        assert (pl.arr("status", np.int32) == 0).all(), mode
+        out = pl.arr("out", shape=(I, pl.opitch))
+        assert np.array_equal(out[:, : pl.B], pl.values[:, : pl.B]), mode
+        after = pl.shards()
+        for i, m in enumerate(ms):
+            miss = np.flatnonzero(pl.present[i, :k] == 0)
+            assert len(miss) == m
+            assert np.array_equal(after[i], committed[i]), (mode, i, m)  # every row, data and parity
+            assert not after[i][:, S:].any(), (mode, i, m)
 
 
 @pytest.mark.parametrize("S", [763, 100, 1400, 1500, 2000])
@@ -1231,6 +1290,7 @@ def test_receive_step_pipeline_equals_verify_then_interpolate(gpu, ref, n, f, B,
             c.dev_inject_faults(None, I, b["shards"], pl.spitch, d_byz)
             c.dev_leaves(None, I, b["shards"], pl.spitch, None, pl.S, b["leaves"])
             c.dev_merkle_build(None, I, b["leaves"], b["roots"], b["branches"])
+            pl.poison(seed=bi, present=not all_present)  # absent + corrupted rows: garbage
             c.dev_inject_faults(None, I, b["shards"], pl.spitch, b["corrupt"])
             pls.append(pl)
         present = (lambda pl: None) if all_present else (lambda pl: pl.b["present"])
@@ -1291,6 +1351,7 @@ def test_row_view_interpolate_equals_joined_value(gpu, ref, n, f, B, I):
     for mode in ("joined", "view", "step_view"):
         pl = Pipeline(gpu, n, f, B, I, seed=n + B, corrupt_frac=0.3)
         pl.commit()
+        pl.poison()
         b, c = pl.b, pl.ctx
         c.dev_inject_faults(None, I, b["shards"], pl.spitch, b["corrupt"])
         roots = pl.arr("roots", shape=(I, 32)).copy()
@@ -1367,6 +1428,7 @@ def test_receive_step_rejects_aliased_batches(gpu, ref):
     for bi in range(2):
         pl = Pipeline(gpu, n, f, B, I, seed=77 + bi, corrupt_frac=0.3)
         pl.commit()
+        pl.poison()
         pl.ctx.dev_inject_faults(None, I, pl.b["shards"], pl.spitch, pl.b["corrupt"])
         pls.append(pl)
     rx = gpu.Context(n, f)
@@ -1453,6 +1515,9 @@ def test_receive_step_ragged_lengths_and_too_few_shards(gpu, ref, n, f):
             present[i, pres] = 1
             if i % 3 == 0:
                 sh[i, pres[0], rng.integers(int(out["shard_lens"][i]))] ^= 0x21
+            # every absent row holds garbage across the whole pitch: only the decode can restore it
+            gone = np.flatnonzero(present[i] == 0)
+            sh[i, gone] = rng.integers(0, 256, (len(gone), pitch), dtype=np.uint8)
         batches.append(dict(values=values, out=out, sh=sh, present=present, pitch=pitch, opitch=opitch))
     res = {}
     for mode in ("oneshot", "step"):
@@ -1510,6 +1575,7 @@ def test_receive_step_batches_of_different_sizes(gpu, ref):
         for bi, I in enumerate(sizes):
             pl = Pipeline(gpu, n, f, B, I, seed=555 + bi, corrupt_frac=0.3)
             pl.commit()
+            pl.poison(seed=bi)
             pl.ctx.dev_inject_faults(None, I, pl.b["shards"], pl.spitch, pl.b["corrupt"])
             pls.append(pl)
         if mode == "oneshot":

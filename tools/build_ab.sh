@@ -2,7 +2,7 @@
 # Build A/B variants of librbc_gpu.so that differ in the kernel sources'
 # compile flags (kernels.hip and rs_fft.hip):
 #   tools/build_ab.sh <name> "<-D flags>" ... -> ab/librbc_gpu_<name>.so
-# (select one with RBC_GPU_LIB_AB=ab/librbc_gpu_<name>.so).
+# (select one with RBC_GPU_LIB=ab/librbc_gpu_<name>.so).
 set -euo pipefail
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 C=$ROOT/cleisthenes_amd/csrc
