@@ -82,6 +82,12 @@ struct DevBuf {
 // work: the context's device API has one, every host-API slot has its own.
 struct Ws {
     DevBuf used, regen, dmat, nmiss, flags, list, counter, rcount, cls, vleaves, vlist;
+    // receive step's node-reuse recheck: the roots each in-flight batch's
+    // branches were verified against (two slots: cur and prev), and the
+    // instances handed to the full recheck
+    DevBuf vroot[2], need_full;
+    int rx_vslot = 0;           // slot of the pending batch's verified roots
+    bool rx_vreuse = false;     // ... kept (the recheck mode when it was verified was REUSE)
     // fork the join onto an aux stream (device API); host-API slots keep one
     // stream each (their concurrency comes from the slots themselves, and
     // the box has GPU_MAX_HW_QUEUES = 4 hardware queues per process)
@@ -96,7 +102,8 @@ struct Ws {
                hipEventCreateWithFlags(&ev_hashed, hipEventDisableTiming) == hipSuccess;
     }
     void release() {
-        for (DevBuf *b : {&used, &regen, &dmat, &nmiss, &flags, &list, &counter, &rcount, &cls, &vleaves, &vlist})
+        for (DevBuf *b : {&used, &regen, &dmat, &nmiss, &flags, &list, &counter, &rcount, &cls, &vleaves, &vlist,
+                          &vroot[0], &vroot[1], &need_full})
             b->release();
         if (aux) (void)hipStreamDestroy(aux);
         if (ev_fork) (void)hipEventDestroy(ev_fork);
@@ -157,6 +164,9 @@ struct rbc_ctx {
     // rbc_ctx_set_decode_priority, default -1 = the commit side's level, like
     // the commit side's own transform
     int gemv_prio_ = -1, reencode_prio_ = -1;
+    // the receive step's root recheck: RBC_RECHECK_REUSE (default: over the
+    // nodes ECHO verify established) or RBC_RECHECK_FULL (the whole tree)
+    int recheck = RBC_RECHECK_REUSE;
     int gemv_prio() const { return gemv_prio_ < 0 ? tx_prio : gemv_prio_; }
     int reencode_prio() const { return reencode_prio_ < 0 ? tx_prio : reencode_prio_; }
     std::vector<uint8_t> h_M;      // n x k encode matrix
@@ -764,6 +774,14 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
         r.list = w.list.as<uint32_t>();
         r.list_count = w.counter.as<uint32_t>();
     }
+    // node-reuse recheck (merkle_recheck_kernel): keep the roots cur's branches
+    // are verified against now, for cur's recheck in the next call
+    const bool reuse = c->recheck == RBC_RECHECK_REUSE && c->depth >= 1 && c->width <= 256;
+    const int cur_vslot = w.rx_vslot ^ (hp ? 1 : 0);
+    if (hc && reuse) {
+        RBC_HIP(w.vroot[cur_vslot].ensure((size_t)cur->count * 32));
+        RBC_HIP(hipMemcpyAsync(w.vroot[cur_vslot].p, cur->roots, (size_t)cur->count * 32, hipMemcpyDeviceToDevice, st));
+    }
     RBC_HIP(rbc_launch_sha_rx(v, r, v_walk, st));
     if (hc && v_path) {
         PathArgs p{};
@@ -813,6 +831,29 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
         m.expect_roots = prev->roots;
         m.status = prev->status;
         m.prio = c->rx_prio;
+        if (reuse && w.rx_vreuse) {
+            // the nodes inside the valid-free subtrees only; an instance whose
+            // decode changed a valid row goes on to the full recheck (m.only)
+            RBC_HIP(w.need_full.ensure((size_t)prev->count));
+            RecheckArgs ra{};
+            ra.count = prev->count;
+            ra.n = c->n;
+            ra.width = c->width;
+            ra.depth = c->depth;
+            ra.leaves = prev->leaves;
+            ra.leaves_inst_pitch = (uint64_t)c->n * 32;
+            ra.branches = prev->branches;
+            ra.br_inst_pitch = (uint64_t)c->n * c->depth * 32;
+            ra.valid = prev->valid;
+            ra.flags = w.flags.as<uint32_t>();
+            ra.vroots = w.vroot[w.rx_vslot].as<uint8_t>();
+            ra.expect_roots = prev->roots;
+            ra.status = prev->status;
+            ra.need_full = w.need_full.as<uint8_t>();
+            ra.prio = c->rx_prio;
+            RBC_HIP(rbc_launch_recheck(ra, st));
+            m.only = ra.need_full;
+        }
         RBC_HIP(rbc_launch_merkle(m, true, st));
     }
     w.rx_count = 0;  // prev is complete once this call's work on `st` is; cur is pending only on success
@@ -831,6 +872,8 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
         }
         w.rx_count = cur->count;
         w.rx_shards = cur->shards;
+        w.rx_vslot = cur_vslot;
+        w.rx_vreuse = reuse;  // its verified roots were kept
     }
     return RBC_OK;  // pj: `st` waits for prev's join + digest
 }
@@ -926,6 +969,13 @@ const char *rbc_strerror(int s) {
 }
 
 int rbc_abi_version(void) { return RBC_ABI_VERSION; }
+
+int rbc_ctx_set_recheck(rbc_ctx *c, int mode) {
+    if (!c || (mode != RBC_RECHECK_REUSE && mode != RBC_RECHECK_FULL)) return RBC_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->recheck = mode;
+    return RBC_OK;
+}
 
 int rbc_library_path(char *out, size_t cap) {
     if (!out || cap == 0) return RBC_ERR_INVALID_ARG;

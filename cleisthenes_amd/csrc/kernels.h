@@ -84,7 +84,27 @@ struct MerkleArgs {
     uint8_t *digests;          // check: [I][32] (nullable)
     int trees_per_block;       // set by rbc_launch_merkle
     int prio;                  // wave issue priority 0..3 (set_wave_prio)
+    const uint8_t *only;       // check: [I] nonzero = recheck this instance, others untouched (nullable = all)
 };
+
+// merkle_recheck_kernel: the receive step's root recheck over the nodes ECHO
+// verify established
+struct RecheckArgs {
+    int count, n, width, depth;
+    const uint8_t *leaves;     // [I][N][32]: verified leaves + the regenerated rows' hashes
+    uint64_t leaves_inst_pitch;
+    const uint8_t *branches;   // [I][N][d][32]: the received ECHO branches
+    uint64_t br_inst_pitch;
+    const uint8_t *valid;      // [I][N]
+    const uint32_t *flags;     // [I][N]: valid rows the re-encoding changed (decode compare)
+    const uint8_t *vroots;     // [I][32]: the roots the branches were verified against
+    const uint8_t *expect_roots;  // [I][32]
+    int32_t *status;           // in/out
+    uint8_t *need_full;        // [I] out: 1 = leave the instance to the full recheck (merkle_kernel<true>, only)
+    int inst_per_block;        // set by rbc_launch_recheck
+    int prio;
+};
+hipError_t rbc_launch_recheck(const RecheckArgs &a, hipStream_t st);
 
 // merkle_path_kernel: shared-path branch verification over precomputed leaves
 struct PathArgs {

@@ -682,7 +682,7 @@ __global__ __launch_bounds__(64) void merkle_kernel(MerkleArgs a) {
         for (int t = tid; t < G * m; t += 64) {
             const int g = t >> lgm, i = m + (t & (m - 1));
             const int inst = inst0 + g;
-            if (inst >= a.count) continue;
+            if (inst >= a.count || (CHECK && a.only && !a.only[inst])) continue;
             const int lc = 2 * i, rc = lc + 1;
             // one compression body for every node form (fewer live registers):
             // H(L || R) = [L | R] + a constant pad block; H(L) (right child an
@@ -737,7 +737,7 @@ __global__ __launch_bounds__(64) void merkle_kernel(MerkleArgs a) {
     // roots: one thread per tree (W == 1: the root is leaf 0)
     for (int g = tid; g < G; g += 64) {
         const int inst = inst0 + g;
-        if (inst >= a.count) continue;
+        if (inst >= a.count || (CHECK && a.only && !a.only[inst])) continue;
         uint32_t root[8];
         if (W == 1) {
             load_digest(a.leaves + (size_t)inst * a.leaves_inst_pitch, root);
@@ -787,6 +787,163 @@ __global__ __launch_bounds__(64) void merkle_kernel(MerkleArgs a) {
                 *reinterpret_cast<uint4 *>(a.branches + (size_t)inst * a.br_inst_pitch + (size_t)jl * 32u + 16u * half) = v;
             }
         }
+    }
+}
+
+// ============================================================================
+// merkle_recheck: interpolate's root recheck inside rbc_dev_receive_step,
+// over the nodes ECHO verify already established (interpolate,
+// rbc/rbc.go:86-90; validateMessage, rbc/rbc.go:92-95).
+// Every valid ECHO leaf j was verified against the committed root R, so its
+// leaf hash and every sibling in its branch are nodes of the committed tree C
+// (collision resistance).  The re-encoding E equals C at every valid leaf the
+// decode left unchanged (used rows are never rewritten; a valid unused row
+// the re-encoding differs from is flagged).  Hence E's root equals R iff
+// E(v) == C(v) at the root v of every MAXIMAL subtree that holds no valid
+// leaf, and C(v) is the level-l entry of the branch of any valid leaf under
+// v's sibling.  So only the nodes inside those subtrees are hashed (C4:
+// ~15 of 255 per instance, C2 ~25 of 127) plus one 32-byte compare per
+// subtree, instead of the whole tree; and R (copied when the branches were
+// verified) must equal expect_roots[i] now.  An instance with a flagged row
+// is left to the full recheck (need_full -> merkle_kernel<true>, `only`).
+// The status equals the full recheck's on every input, up to SHA-256
+// collisions (tests/test_gpu_parity.py: node-reuse vs full recheck).
+// One-wave blocks of G instances: the node hashes of one level of all G
+// instances are packed onto consecutive lanes (like merkle_kernel); LDS
+// holds E of the hashed nodes ([G][W][8] words, heap index 1..W-1) and a
+// has-valid byte per heap node ([G][2W], leaves at W..2W-1).
+// ============================================================================
+__global__ __launch_bounds__(64) void merkle_recheck_kernel(RecheckArgs a) {
+    set_wave_prio(a.prio);
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int G = a.inst_per_block, W = a.width, lgW = a.depth, n = a.n;
+    uint32_t *E = reinterpret_cast<uint32_t *>(smem);
+    uint8_t *hv = smem + (size_t)G * W * 32;
+    uint16_t *task = reinterpret_cast<uint16_t *>(hv + (size_t)G * 2 * W);  // G * W / 2 entries at most
+    __shared__ uint32_t s_state[64];  // per instance: bit 0 live, bit 1 a compare failed, bit 2 flagged row
+    const int lane = threadIdx.x;
+    const int inst0 = (int)blockIdx.x * G;
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int g = lane; g < G; g += 64) {
+        const int inst = inst0 + g;
+        s_state[g] = (inst < a.count && a.status[inst] == 0) ? 1u : 0u;
+    }
+    __syncthreads();
+    // 1. leaves: has-valid = valid; a flagged (changed) valid row sends the instance to the full recheck
+    for (int t = lane; t < G * W; t += 64) {
+        const int g = t >> lgW, j = t & (W - 1), inst = inst0 + g;
+        uint8_t v = 0;
+        if ((s_state[g] & 1u) && j < n) {
+            v = a.valid[(size_t)inst * n + j] != 0;
+            if (v && a.flags[(size_t)inst * n + j]) atomicOr(&s_state[g], 4u);
+        }
+        hv[g * 2 * W + W + j] = v;
+    }
+    __syncthreads();
+    // 2. has-valid up the tree (heap order: node i's children are 2i, 2i+1)
+    for (int l = 1; l <= lgW; ++l) {
+        const int m = W >> l;
+        for (int t = lane; t < G * m; t += 64) {
+            const int g = t >> (lgW - l), i = m + (t & (m - 1));
+            uint8_t *h = hv + g * 2 * W;
+            h[i] = h[2 * i] | h[2 * i + 1];
+        }
+        __syncthreads();
+    }
+    auto active = [&](int g) { return (s_state[g] & 5u) == 1u; };  // live, no flagged row
+    // 3. E of every node that holds no valid leaf, level by level, the
+    //    level's nodes of all G instances on consecutive lanes
+    for (int l = 1; l < lgW; ++l) {
+        const int m = W >> l;
+        int total = 0;
+        for (int t0 = 0; t0 < G * m; t0 += 64) {  // wave-uniform trip count
+            const int t = t0 + lane;
+            const int g = t >> (lgW - l), i = m + (t & (m - 1));
+            const bool need = t < G * m && active(g) && !hv[g * 2 * W + i];
+            const uint64_t bm = __ballot(need);
+            if (need) task[total + __popcll(bm & below)] = (uint16_t)(g * 2 * W + i);
+            total += __popcll(bm);
+        }
+        __syncthreads();
+        if (total == 0) continue;  // wave-uniform: no hashing at this level
+        for (int q = lane; q < total; q += 64) {
+            const int gi = task[q], g = gi / (2 * W), i = gi - g * 2 * W;
+            uint32_t o[8];
+            if (l == 1) {  // children are leaves 2i - W, 2i + 1 - W (empty past n)
+                const int jl = 2 * i - W, jr = jl + 1;
+                const uint8_t *lv = a.leaves + (size_t)(inst0 + g) * a.leaves_inst_pitch;
+                if (jl >= n) {
+                    sha256_empty(o);
+                } else {
+                    uint32_t L[8];
+                    load_digest(lv + 32u * jl, L);
+                    if (jr < n) {
+                        uint32_t R[8];
+                        load_digest(lv + 32u * jr, R);
+                        sha256_node64(L, R, o);
+                    } else {
+                        sha256_node32(L, o);
+                    }
+                }
+            } else {
+                uint32_t L[8], R[8];
+                const uint32_t *nl = E + ((size_t)g * W + 2 * i) * 8, *nr = E + ((size_t)g * W + 2 * i + 1) * 8;
+#pragma unroll
+                for (int q2 = 0; q2 < 8; ++q2) { L[q2] = nl[q2]; R[q2] = nr[q2]; }
+                sha256_node64(L, R, o);
+            }
+            uint32_t *dst = E + ((size_t)g * W + i) * 8;
+#pragma unroll
+            for (int q2 = 0; q2 < 8; ++q2) dst[q2] = o[q2];
+        }
+        __syncthreads();
+    }
+    // 4. compare the root v of every maximal valid-free subtree (level l < d)
+    //    holding a real leaf with the level-l branch entry of the first valid
+    //    leaf under its sibling (an all-padding subtree is the same constant
+    //    in both trees)
+    for (int l = 0; l < lgW; ++l) {
+        const int m = W >> l;
+        for (int t = lane; t < G * m; t += 64) {
+            const int g = t >> (lgW - l), i = m + (t & (m - 1));
+            const uint8_t *h = hv + g * 2 * W;
+            if (!active(g) || h[i] || !h[i >> 1] || ((i - m) << l) >= n) continue;
+            int s = i ^ 1;
+            while (s < W) s = h[2 * s] ? 2 * s : 2 * s + 1;  // first valid leaf under the sibling
+            const int inst = inst0 + g, j = s - W;
+            const uint4 *br = reinterpret_cast<const uint4 *>(a.branches + (size_t)inst * a.br_inst_pitch +
+                                                              ((size_t)j * lgW + l) * 32u);
+            const uint4 c0 = br[0], c1 = br[1];
+            uint4 e0, e1;
+            if (l == 0) {  // E = the regenerated row's leaf hash, raw bytes
+                const uint4 *lf = reinterpret_cast<const uint4 *>(a.leaves + (size_t)inst * a.leaves_inst_pitch +
+                                                                  32u * (i - W));
+                e0 = lf[0];
+                e1 = lf[1];
+            } else {  // LDS holds the digest words; the branch holds their bytes
+                const uint32_t *e = E + ((size_t)g * W + i) * 8;
+                e0 = make_uint4(bswap32(e[0]), bswap32(e[1]), bswap32(e[2]), bswap32(e[3]));
+                e1 = make_uint4(bswap32(e[4]), bswap32(e[5]), bswap32(e[6]), bswap32(e[7]));
+            }
+            const bool same = e0.x == c0.x && e0.y == c0.y && e0.z == c0.z && e0.w == c0.w && e1.x == c1.x &&
+                              e1.y == c1.y && e1.z == c1.z && e1.w == c1.w;
+            if (!same) atomicOr(&s_state[g], 2u);
+        }
+    }
+    __syncthreads();
+    // 5. status, or the hand-off to the full recheck
+    for (int g = lane; g < G; g += 64) {
+        const int inst = inst0 + g;
+        if (inst >= a.count) continue;
+        const uint32_t st = s_state[g];
+        a.need_full[inst] = (st & 5u) == 5u ? 1 : 0;
+        if ((st & 5u) != 1u) continue;
+        const uint4 *x = reinterpret_cast<const uint4 *>(a.vroots + (size_t)inst * 32u);
+        const uint4 *y = reinterpret_cast<const uint4 *>(a.expect_roots + (size_t)inst * 32u);
+        const uint4 x0 = x[0], x1 = x[1], y0 = y[0], y1 = y[1];
+        const bool root_same = x0.x == y0.x && x0.y == y0.y && x0.z == y0.z && x0.w == y0.w && x1.x == y1.x &&
+                               x1.y == y1.y && x1.z == y1.z && x1.w == y1.w;
+        a.status[inst] = (!(st & 2u) && root_same) ? 0 : RBC_ERR_ROOT_MISMATCH;
     }
 }
 
@@ -1701,7 +1858,10 @@ hipError_t rbc_launch_merkle_path(const PathArgs &a, hipStream_t st) {
     const int L = a.width > 64 ? a.width / 64 : 1;
     b.inst_per_block = a.width >= 64 ? 1 : 64 / a.width;
     const dim3 grid((unsigned)((a.count + b.inst_per_block - 1) / b.inst_per_block));
-    if (L == 4) hipLaunchKernelGGL(merkle_path_kernel<4>, grid, dim3(64), 0, st, b);
+#ifndef RBC_AB_PATH_PAD
+#define RBC_AB_PATH_PAD 0  // A/B only (tools/build_ab.sh): dynamic LDS that caps the blocks resident per CU
+#endif
+    if (L == 4) hipLaunchKernelGGL(merkle_path_kernel<4>, grid, dim3(64), RBC_AB_PATH_PAD, st, b);
     else if (L == 2) hipLaunchKernelGGL(merkle_path_kernel<2>, grid, dim3(64), 0, st, b);
     else hipLaunchKernelGGL(merkle_path_kernel<1>, grid, dim3(64), 0, st, b);
     return hipGetLastError();
@@ -1722,6 +1882,22 @@ hipError_t rbc_launch_merkle(const MerkleArgs &a, bool check, hipStream_t st) {
     const unsigned blocks = (unsigned)((a.count + b.trees_per_block - 1) / b.trees_per_block);
     if (check) hipLaunchKernelGGL(merkle_kernel<true>, dim3(blocks), dim3(64), lds, st, b);
     else hipLaunchKernelGGL(merkle_kernel<false>, dim3(blocks), dim3(64), lds, st, b);
+    return hipGetLastError();
+}
+
+hipError_t rbc_launch_recheck(const RecheckArgs &a, hipStream_t st) {
+    if (a.count <= 0) return hipSuccess;
+    if (a.width < 2 || a.width > 256 || (a.width & (a.width - 1)) || (1 << a.depth) != a.width)
+        return hipErrorInvalidValue;
+    RecheckArgs b = a;
+    // G instances per one-wave block: 512 / W leaves' worth (16 KiB of node
+    // LDS), but >= 512 blocks so that a small batch still spreads over the CUs
+    int g = std::min(512 / a.width, 64);
+    while (g > 1 && (a.count + g - 1) / g < 512) g >>= 1;
+    b.inst_per_block = g;
+    const size_t lds = (size_t)g * a.width * 32 + (size_t)g * 2 * a.width + (size_t)g * a.width;
+    const unsigned blocks = (unsigned)((a.count + g - 1) / g);
+    hipLaunchKernelGGL(merkle_recheck_kernel, dim3(blocks), dim3(64), lds, st, b);
     return hipGetLastError();
 }
 

@@ -269,6 +269,11 @@ class Context:
         """s_setprio level (0..3, -1 = the commit level) of interpolate's GF transforms."""
         check(lib.rbc_ctx_set_decode_priority(self._p, gemv, reencode), "rbc_ctx_set_decode_priority")
 
+    def set_recheck(self, mode: str) -> None:
+        """The receive step's root recheck: "reuse" (default; only the subtrees
+        with no valid ECHO leaf are hashed) or "full" (the whole tree)."""
+        check(lib.rbc_ctx_set_recheck(self._p, {"reuse": 0, "full": 1}[mode]), "rbc_ctx_set_recheck")
+
     def set_codec(self, codec: str) -> None:
         check(lib.rbc_ctx_set_codec(self._p, {"auto": 0, "matrix": 1, "fft": 2}[codec]), "rbc_ctx_set_codec")
 

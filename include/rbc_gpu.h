@@ -98,6 +98,17 @@ int rbc_ctx_set_wave_priority(rbc_ctx *ctx, int commit_prio, int receive_prio);
  * transform.  Which side they should side with depends on which stream
  * limits the pipelined step. */
 int rbc_ctx_set_decode_priority(rbc_ctx *ctx, int gemv_prio, int reencode_prio);
+/* Root recheck of rbc_dev_receive_step (interpolate's Merkle recheck,
+ * rbc/rbc.go:86-90).  RBC_RECHECK_REUSE (default): hash only the subtrees
+ * that hold no valid ECHO leaf and compare their roots with the received
+ * branches (verified against the committed root), falling back to the whole
+ * tree for an instance whose decode changed a valid row; RBC_RECHECK_FULL:
+ * rehash the whole tree.  The statuses are the same either way (up to
+ * SHA-256 collisions); rbc_dev_interpolate always rehashes the whole tree
+ * (it has no branches). */
+#define RBC_RECHECK_REUSE 0
+#define RBC_RECHECK_FULL 1
+int rbc_ctx_set_recheck(rbc_ctx *ctx, int mode);
 
 /* ---- device memory / streams / events (so a host runtime needs no other
  *      GPU library to drive the rbc_dev_* path) ---------------------------- */

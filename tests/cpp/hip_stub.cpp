@@ -226,6 +226,12 @@ hipError_t rbc_launch_sha_rx(const ShaArgs &v, const ShaArgs &r, bool v_walk, hi
     if (r.count > 0) touch(r.leaves, (size_t)r.count * r.leaves_inst_pitch);
     return hipSuccess;
 }
+hipError_t rbc_launch_recheck(const RecheckArgs &a, hipStream_t) {
+    if (a.count <= 0) return hipSuccess;
+    touch(a.status, (size_t)a.count * 4);
+    touch(a.need_full, (size_t)a.count);
+    return hipSuccess;
+}
 hipError_t rbc_launch_merkle(const MerkleArgs &a, bool check, hipStream_t) {
     if (a.count <= 0) return hipSuccess;
     if (!check) {

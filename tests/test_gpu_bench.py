@@ -131,6 +131,9 @@ def test_bench_guard_fails_a_build_that_never_regenerates(config, join):
     err = [ln for ln in r.stderr.splitlines() if ln.startswith('{"error"')]
     assert len(err) == 1, r.stderr[-3000:]
     e = json.loads(err[0])
-    assert e["guard"]["timed_batch"] == {"decoded": 64, "value_mismatch_chunks": 0}
-    assert e["guard"]["poisoned_batch"]["decoded"] < 64 and e["guard"]["poisoned_batch"]["value_mismatch_chunks"] > 0
-    assert not e["values_ok"] and e["decoded_ok"] < 64 and e["library"] == os.path.realpath(MUTANT)
+    timed, poisoned = e["guard"]["timed_batch"], e["guard"]["poisoned_batch"]
+    # the timed batches' absent rows still hold the proposer's bytes: only the ~10 % of instances whose
+    # corrupted ECHO is a data row can fail there; with every such row poisoned, (nearly) every one does
+    assert timed["decoded"] >= 64 * 0.7, timed
+    assert poisoned["decoded"] <= 64 * 0.1 and poisoned["value_mismatch_chunks"] > 10 * max(1, timed["value_mismatch_chunks"])
+    assert not e["values_ok"] and e["decoded_ok"] <= poisoned["decoded"] and e["library"] == os.path.realpath(MUTANT)

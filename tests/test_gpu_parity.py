@@ -1601,3 +1601,131 @@ def test_receive_step_batches_of_different_sizes(gpu, ref):
         assert (s0 == 0).all() and np.array_equal(s0, s1)
         assert np.array_equal(o0[:, : pl.k * pl.S], o1[:, : pl.k * pl.S]) and np.array_equal(d0, d1)
         assert all(bytes(pl.values[i, :B]) == bytes(o1[i, :B]) for i in range(pl.I))
+
+
+RECHECK_GEOMS = [(7, 2, 1000, 40), (16, 5, 3001, 48), (33, 10, 13 * 50 + 3, 40), (64, 21, 22 * 300, 40),
+                 (128, 42, 44 * 200, 48), (256, 85, 86 * 40, 48)]
+
+
+@pytest.mark.parametrize("n,f,B,I", RECHECK_GEOMS, ids=[f"n{g[0]}" for g in RECHECK_GEOMS])
+def test_receive_step_node_reuse_recheck_equals_full_recheck(gpu, ref, n, f, B, I):
+    """rbc_dev_receive_step's root recheck over the nodes ECHO verify
+    established (RBC_RECHECK_REUSE: hash only the subtrees that hold no valid
+    leaf, compare their roots with a valid leaf's branch) against the whole-
+    tree recheck (RBC_RECHECK_FULL) and one-shot verify + interpolate, on the
+    same three batches: statuses, valid masks, digests, leaves, values and the
+    regenerated shard sets are identical.  Inputs per instance: honest with
+    random, data-only, parity-heavy and all-present ECHO sets; corrupted
+    shards; a corrupted branch slot at every level (the leaf is invalid, its
+    siblings' anchors are not); a Byzantine non-codeword commitment (a valid
+    unused row the re-encoding changes: the full-recheck fallback, or a
+    regenerated row that misses its anchor); wrong roots written after the
+    verify (the copy of the verified roots must disagree)."""
+    k = n - 2 * f
+    d = max(1, (n - 1).bit_length())
+    nb = 3
+
+    def make_batches():
+        pls, plan = [], []
+        for bi in range(nb):
+            rng = np.random.default_rng(7000 + 31 * n + bi)
+            pl = Pipeline(gpu, n, f, B, I, seed=900 * n + bi, corrupt_frac=0.0)
+            kind = [rng.integers(0, 7) for _ in range(I)]
+            byz = np.full(I, -1, np.int32)
+            for i, kd in enumerate(kind):
+                if kd == 3:
+                    pl.present[i] = 0
+                    pl.present[i, :k] = 1                    # data rows only
+                elif kd == 4:
+                    pl.present[i] = 0
+                    pl.present[i, rng.permutation(n)[:k]] = 1  # exactly k
+                elif kd == 5:
+                    pl.present[i] = 1                        # everything received
+                if kd == 6 and n > k:
+                    byz[i] = int(rng.integers(k, n))          # non-codeword: a parity row altered before the tree
+            pl.b["present"].upload(pl.present)
+            b, c = pl.b, pl.ctx
+            c.dev_encode(None, I, b["values"], pl.vpitch, None, B, b["shards"], pl.spitch)
+            d_byz = gpu.DeviceBuffer(I * 4)
+            d_byz.upload(byz)
+            c.dev_inject_faults(None, I, b["shards"], pl.spitch, d_byz)
+            c.dev_leaves(None, I, b["shards"], pl.spitch, None, pl.S, b["leaves"])
+            c.dev_merkle_build(None, I, b["leaves"], b["roots"], b["branches"])
+            gpu.rbc.lib.rbc_device_sync(0)
+            sh = pl.shards().copy()
+            brs = pl.arr("branches", shape=(I, n, d, 32)).copy()
+            for i, kd in enumerate(kind):
+                pres = np.flatnonzero(pl.present[i])
+                if kd == 1:   # a corrupted received shard
+                    sh[i, pres[rng.integers(len(pres))], rng.integers(pl.S)] ^= 0x10
+                elif kd == 2:  # a corrupted branch slot of a received leaf, at every level in turn
+                    j = pres[rng.integers(len(pres))]
+                    lvl = i % d
+                    if not (lvl == 0 and (j ^ 1) >= n):
+                        brs[i, j, lvl, rng.integers(32)] ^= 0x04
+            # absent rows hold garbage
+            for i in range(I):
+                gone = np.flatnonzero(pl.present[i] == 0)
+                sh[i, gone] = rng.integers(0, 256, (len(gone), pl.spitch), dtype=np.uint8)
+            b["shards"].upload(sh)
+            b["branches"].upload(brs)
+            pls.append(pl)
+            plan.append(kind)
+        return pls, plan
+
+    def run(mode):
+        pls, plan = make_batches()
+        if mode == "oneshot":
+            for pl in pls:
+                b, c = pl.b, pl.ctx
+                c.dev_verify(None, I, b["shards"], pl.spitch, None, pl.S, b["branches"], b["roots"], b["present"],
+                             b["valid"], b["leaves_r"])
+                gpu.rbc.lib.rbc_device_sync(0)
+                wrong = pl.arr("roots", shape=(I, 32)).copy()
+                wrong[5::11, 3] ^= 0x01
+                b["roots"].upload(wrong)
+                c.dev_interpolate(None, I, b["shards"], pl.spitch, None, pl.S, b["valid"], b["leaves_r"], 1,
+                                  b["roots"], b["out"], pl.opitch, b["digests"], b["status"])
+        else:
+            rx = gpu.Context(n, f)
+            rx.set_recheck(mode)
+            bs = [rx.rx_batch(I, pl.b["shards"], pl.spitch, None, pl.S, pl.b["branches"], pl.b["roots"],
+                              pl.b["present"], pl.b["valid"], pl.b["leaves_r"], pl.b["out"], pl.opitch,
+                              pl.b["digests"], pl.b["status"]) for pl in pls]
+            prev = None
+            for bi, cur in enumerate(bs + [None]):
+                rx.dev_receive_step(None, cur, prev)
+                gpu.rbc.lib.rbc_device_sync(0)
+                if cur is not None:  # after cur's verify, before its recheck in the next call
+                    pl = pls[bi]
+                    wrong = pl.arr("roots", shape=(I, 32)).copy()
+                    wrong[5::11, 3] ^= 0x01
+                    pl.b["roots"].upload(wrong)
+                prev = cur
+        gpu.rbc.lib.rbc_device_sync(0)
+        out = []
+        for pl in pls:
+            st = pl.arr("status", np.int32).copy()
+            ok = st == 0
+            out.append(dict(status=st, valid=pl.arr("valid", shape=(I, n)).copy(),
+                            digests=pl.arr("digests", shape=(I, 32))[ok].copy(),
+                            leaves=pl.arr("leaves_r", shape=(I, n, 32))[ok].copy(),
+                            out=pl.arr("out", shape=(I, pl.opitch))[ok, : pl.k * pl.S].copy(),
+                            shards=pl.shards()[ok].copy(), present=pl.present.copy(), values=pl.values))
+        return out, plan
+
+    res = {m: run(m) for m in ("oneshot", "full", "reuse")}
+    plan = res["reuse"][1]
+    for bi in range(nb):
+        a, b_, c_ = res["oneshot"][0][bi], res["full"][0][bi], res["reuse"][0][bi]
+        pr = c_["present"].astype(bool)
+        for key in ("status", "digests", "leaves", "out", "shards"):
+            assert np.array_equal(a[key], c_[key]) and np.array_equal(b_[key], c_[key]), (bi, key)
+        assert np.array_equal(a["valid"][pr], c_["valid"][pr]) and np.array_equal(b_["valid"], c_["valid"]), bi
+        st, kind = c_["status"], np.array(plan[bi])
+        assert (st[5::11] == -8).all(), bi  # the roots changed after the verify
+        assert (st[kind == 6][(np.arange(I)[kind == 6] % 11) != 5] == -8).all() or n == k, bi  # non-codeword
+        honest = (kind != 6) & (np.arange(I) % 11 != 5)
+        assert (st[honest] == 0).all(), (bi, st[honest])
+        for t, i in enumerate(np.flatnonzero(st == 0)):
+            assert bytes(c_["out"][t][:B]) == bytes(c_["values"][i, :B])
