@@ -87,6 +87,8 @@ def parse_args(argv):
                          "0: one stream, stages in order")
     ap.add_argument("--join", action="store_true",
                     help="assemble interpolate's value (k*S bytes per instance) instead of the row view")
+    ap.add_argument("--no-joined-leg", action="store_true",
+                    help="skip the secondary timed run in the joined value form (key value_joined)")
     ap.add_argument("--faults-on", default="receiver", choices=("receiver", "proposer"),
                     help="stream that injects the corrupted ECHO shards (synthetic input)")
     ap.add_argument("--wave-prio", default="",
@@ -246,7 +248,8 @@ def run(args, world, rank, local_rank, wd, out):
     rstream = ca.Stream(dev) if pipe else stream
     names = ("t0", "enc", "leaf", "tree", "pf", "r0", "rf", "hashed", "dbeg", "ddone", "rend", "gather")
     ev_sets = [{nm: ca.Event() for nm in names} for _ in range(max(args.steps, 3))]
-    vpo = (lambda rb: (rb["out"], opitch)) if args.join else (lambda rb: (None, 0))  # noqa: E731
+    form = {"join": args.join, "start": 0}  # value form of the receive steps; the first step of a run
+    vpo = lambda rb: (rb["out"], opitch) if form["join"] else (None, 0)  # noqa: E731
 
     def rec(ev, name, st):
         if ev is not None:
@@ -296,7 +299,7 @@ def run(args, world, rank, local_rank, wd, out):
             ctx.dev_inject_faults(P.ptr, I, sp["shards"], spitch, d_corrupt)
         rec(ev, "pf", P)
         evP[t % nsets].record(P)
-        if t == 0:
+        if t == form["start"]:
             return
         x = t - 1
         sr, rb = sets[x % nsets], rxb[x % 2]
@@ -398,6 +401,45 @@ def run(args, world, rank, local_rank, wd, out):
     poisoned = check_batch(args, ca, dev, stream, I, n, k, B, S, spitch, vpitch, opitch, d_values, pset, prb, d_count)
     checks = fold_guard(args, synth, rdz, first, I, total, n, f, k, B, vpitch, checks, timed, poisoned)
 
+    def joined_leg():
+        """The same pipelined step with interpolate's value assembled (k*S
+        contiguous bytes per instance, as rbc/rbc.go:88 returns it) instead of
+        the row view: a shorter second timed run, reported beside `value`."""
+        extra = 2 * I * opitch
+        if need["pipelined"] + extra > plan["budget_bytes"]:
+            return {"skipped": "the joined values do not fit the HBM plan"}
+        for rb in rxb:
+            rb["out"] = mb(I * opitch)
+        form.update(join=True, start=100000)
+        stream.sync()
+        rstream.sync()
+        steps_j = max(20, args.steps // 3)
+        for t in range(3):
+            pstep(form["start"] + t)
+        barrier()
+        t1 = time.perf_counter()
+        for t in range(steps_j):
+            pstep(form["start"] + 3 + t, ev_sets[t])
+        barrier()
+        el = time.perf_counter() - t1
+        x_j, cur_j = pending.popitem()
+        ctx.dev_receive_step(rstream.ptr, None, cur_j)
+        rstream.sync()
+        res = check_batch(args, ca, dev, stream, I, n, k, B, S, spitch, vpitch, opitch, d_values, sets[x_j % nsets],
+                          rxb[x_j % 2], d_count, join=True)
+        sm = spans(ev_sets[:steps_j], args.faults_on)
+        return {"value": round(total * n * S * steps_j / el / 1e9, 3), "unit": "GB/s", "steps": steps_j,
+                "ms_per_step": round(el * 1000.0 / steps_j, 4),
+                "decoded_ok": int((res["status"] == 0).sum()), "values_ok": res["mism"] == 0,
+                "stage_ms": {kk: round(v, 4) for kk, v in sm.items()},
+                "value_form": "joined (k*S contiguous bytes per instance, join_kernel on the aux stream)",
+                "note": "secondary run after the guard, same pipelined schedule; `value` is the row view"}
+
+    joined = None
+    if pipe and world == 1 and not args.join and not args.no_joined_leg:
+        wd.enter("joined-value leg", 300)
+        joined = joined_leg()
+
     ms_per_step = elapsed_max * 1000.0 / args.steps
     value = total * n * S * args.steps / elapsed_max / 1e9
     wd.enter("report", 1200)
@@ -444,10 +486,12 @@ def run(args, world, rank, local_rank, wd, out):
                                 f"recheck(t-2), decode(t-1) (rbc_dev_receive_step), two streams, {nsets} shard "
                                 "sets") if pipe else "serial"},
         **rep, **checks, "cpu_baseline": cpu, "pcie_inclusive": pcie, "rccl": rccl, "ranks": ranks,
-        "rank_skew": skew, "library": ca.rbc.library_path(),
+        "rank_skew": skew, "library": ca.rbc.library_path(), "value_joined": joined,
         "host": {kk: host[kk] for kk in ("cpu_model", "nproc", "cgroup_cpu_quota", "affinity_cpus")},
     }
     ok = all(checks[c] for c in ("values_ok", "oracle_sample_ok", "gather_ok")) and checks["decoded_ok"] == total
+    if joined and "value" in joined:  # the joined leg's last batch passes the same value check
+        ok = ok and joined["values_ok"] and joined["decoded_ok"] == I
     wd.leave()
     if not ok:
         print(json.dumps({"error": "correctness check failed", **checks, "library": line["library"]}),
@@ -598,12 +642,12 @@ def report(args, ctx, I, n, k, d, S, present_h, corrupt_h, stage_ms, iso, elapse
     return out
 
 
-def check_batch(args, ca, dev, stream, I, n, k, B, S, spitch, vpitch, opitch, d_values, sp, rb, d_count):
+def check_batch(args, ca, dev, stream, I, n, k, B, S, spitch, vpitch, opitch, d_values, sp, rb, d_count, join=None):
     """One received batch on the device: statuses, and every decoded value
     against its input (the joined value, or the row view's k data rows)."""
     stream.sync()
     status = rb["status"].download(I * 4).view(np.int32).copy()
-    if args.join:
+    if args.join if join is None else join:
         ca.rbc.count_mismatch(dev, stream.ptr, rb["out"], opitch, d_values, vpitch, I, B, d_count)
     else:  # the row view: the k data rows of the shard set are the value
         ca.rbc.count_mismatch_rows(dev, stream.ptr, sp["shards"], n * spitch, spitch, k, S, d_values, vpitch, B, I,

@@ -323,6 +323,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) vo
     // inside it costs the compiler ~2x the registers (spills).
     auto pass = [&](auto rgc, int r0, int rows) {
         constexpr int RG = decltype(rgc)::value;
+        // the lane id through an opaque copy: otherwise LLVM hoists every row
+        // count's lane-derived table addresses (e / RG, my_off, ...) out of
+        // the pass to the kernel entry, where 12 sets of them stay live and
+        // spilled (116 B of scratch per lane: the dirty scratch lines were
+        // ~1x the missing rows' bytes of extra HBM writes and reads, PMC r04b)
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
         uint32_t acc[RG][W];
 #pragma unroll
         for (int r = 0; r < RG; ++r)
@@ -335,7 +342,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) vo
             // consecutive lanes take consecutive rows of one input: their
             // 16-byte table stores are adjacent in LDS (input-major lanes
             // stored RC * 16 bytes apart, a 16-way bank conflict)
-            for (int e = lane; e < RG * JC; e += 64) {
+            for (int e = ln; e < RG * JC; e += 64) {
                 const int jl = e / RG, r = e - jl * RG, j = j0 + jl;
                 const uint32_t cf = (j < K && r < rows) ? coef[(size_t)(r0 + r) * K + j] : 0u;
                 uint4 t01;
@@ -1858,10 +1865,17 @@ hipError_t rbc_launch_merkle_path(const PathArgs &a, hipStream_t st) {
     const int L = a.width > 64 ? a.width / 64 : 1;
     b.inst_per_block = a.width >= 64 ? 1 : 64 / a.width;
     const dim3 grid((unsigned)((a.count + b.inst_per_block - 1) / b.inst_per_block));
-#ifndef RBC_AB_PATH_PAD
-#define RBC_AB_PATH_PAD 0  // A/B only (tools/build_ab.sh): dynamic LDS that caps the blocks resident per CU
-#endif
-    if (L == 4) hipLaunchKernelGGL(merkle_path_kernel<4>, grid, dim3(64), RBC_AB_PATH_PAD, st, b);
+    // W = 256 (C4): dynamic LDS caps the kernel at 3 resident blocks per CU
+    // (46 KiB each of the 160).  Each block walks 8 levels over its instance's
+    // branches, touching every 128-B branch line once per level; with the 8
+    // blocks per CU the VGPRs allow, the lines of the blocks in flight on an
+    // XCD do not stay in its 4 MiB L2 between levels.  Measured at C4
+    // (tools/gpu_runs/gpu_r04c.sh, profiles/r04c*): 8 blocks per CU read 2.74
+    // GB per launch, 4 (38 KiB) 1.64, 3 1.34; the step 350.7-351.4 (8),
+    // 349.3-349.8 (5), 355.3-355.5 (4 and 3) GB/s.
+    constexpr size_t kPathStaticLds = sizeof(uint32_t) * 256 * 17 + 256 + 2 * 256;
+    constexpr size_t kPathBlockLds = 46 * 1024;
+    if (L == 4) hipLaunchKernelGGL(merkle_path_kernel<4>, grid, dim3(64), kPathBlockLds - kPathStaticLds, st, b);
     else if (L == 2) hipLaunchKernelGGL(merkle_path_kernel<2>, grid, dim3(64), 0, st, b);
     else hipLaunchKernelGGL(merkle_path_kernel<1>, grid, dim3(64), 0, st, b);
     return hipGetLastError();

@@ -18,8 +18,10 @@ pass() {  # pass <name> <counters...>
     timeout -s KILL 180 rocprofv3 --pmc "$@" -d "$OUT/$name" -o run --output-format csv -- \
         python3 "$ROOT/bench.py" $ARGS > "$OUT/$name.json" 2> "$OUT/$name.log"
 }
-pass sq1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT
-pass sq2 SQ_WAIT_INST_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE
-pass fetch FETCH_SIZE
-pass write WRITE_SIZE
+# PASSES (default all): a subset, e.g. PASSES="fetch write" for the traffic alone
+want() { [ -z "${PASSES:-}" ] || [[ " $PASSES " == *" $1 "* ]]; }
+want sq1 && pass sq1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT
+want sq2 && pass sq2 SQ_WAIT_INST_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE
+want fetch && pass fetch FETCH_SIZE
+want write && pass write WRITE_SIZE
 echo "pmc $TAG done"
