@@ -247,7 +247,7 @@ def run(args, world, rank, local_rank, wd, out):
 
     rstream = ca.Stream(dev) if pipe else stream
     names = ("t0", "enc", "leaf", "tree", "pf", "r0", "rf", "hashed", "dbeg", "ddone", "rend", "gather")
-    ev_sets = [{nm: ca.Event() for nm in names} for _ in range(max(args.steps, 3))]
+    ev_sets = [{nm: ca.Event() for nm in names} for _ in range(max(args.steps, 20))]  # >= the joined leg's steps
     form = {"join": args.join, "start": 0}  # value form of the receive steps; the first step of a run
     vpo = lambda rb: (rb["out"], opitch) if form["join"] else (None, 0)  # noqa: E731
 
@@ -583,6 +583,18 @@ def report(args, ctx, I, n, k, d, S, present_h, corrupt_h, stage_ms, iso, elapse
             pmc_path = os.path.join("profiles", cand)
             break
         pm = {}
+    # the loaded clock per kernel, each kernel alone (serial schedule; tools/clock_summary.py)
+    clk, clk_path = {}, None
+    for cand in sorted((x for x in os.listdir(os.path.join(ROOT, "profiles")) if x.startswith("valu_clock_r")),
+                       reverse=True):
+        try:
+            c = json.load(open(os.path.join(ROOT, "profiles", cand)))
+        except (OSError, ValueError):
+            continue
+        if c.get("config") == args.config and c.get("instances", 1024) == I:
+            clk, clk_path = c, os.path.join("profiles", cand)
+            break
+    clock_ghz = clk.get("clock_ghz_weighted")
 
     def roofline(name, span=None):
         stage, nbytes, ncomp = kern[name]
@@ -604,6 +616,15 @@ def report(args, ctx, I, n, k, d, S, present_h, corrupt_h, stage_ms, iso, elapse
                          "frac_of_attainable": round(cps / SHA_PROBE_CPS, 4),
                          "model": "4 clk alignbit/add3/perm, 2 clk bitop3/add/shift per wave64 instr; 4484 SIMD "
                                   "clk per wave-compression @2.4 GHz nominal (the chip runs ~2.1 GHz under load)"}
+        if pk and pk.get("SQ_INSTS_VALU") and clock_ghz:
+            # measured, not modelled: the launch's wave64 VALU instructions (PMC) over the SIMD
+            # cycles of its live span at the loaded clock, each instruction at the VALU's 4 clocks
+            # (SQ_ACTIVE_INST_VALU only counts instructions on gfx950: tools/clock_summary.py)
+            r.setdefault("valu", {})["measured"] = {
+                "valu_instr_per_launch": pk["SQ_INSTS_VALU"], "clock_ghz": clock_ghz,
+                "busy_4clk": round(4 * pk["SQ_INSTS_VALU"] / (1024 * clock_ghz * 1e9 * ms / 1e3), 4),
+                "sources": [pmc_path, clk_path],
+                "note": "under the pipeline the span also issues the other stream's instructions"}
         if iso and iso.get(stage) and not name.startswith("sha_rx"):  # sha_rx runs only under the pipeline
             ms_i = iso[stage]
             r["isolated"] = {"avg_ms": round(ms_i, 4), "achieved": round(nbytes / ms_i / 1e6, 1),
@@ -619,6 +640,24 @@ def report(args, ctx, I, n, k, d, S, present_h, corrupt_h, stage_ms, iso, elapse
     out["roofline_decode"] = roofline(
         "decode: prepare + gf_regen_kernel + rs_fft_kernel<decode>",
         "receive step's decode_begin -> decoded marks (rbc_rx_marks) on the receiver stream") if pipe else None
+    # the whole step's VALU issue, measured: every data-path kernel's wave64 VALU instructions per
+    # launch (PMC, one launch each per step) at the loaded clock, against the chip's SIMD cycles
+    util = ("fill_random", "count_mismatch", "poison_rows", "inject_faults", "__amd", "[grid")
+    if pm.get("kernels") and clock_ghz:
+        vk = {kk: v["SQ_INSTS_VALU"] for kk, v in pm["kernels"].items()
+              if v.get("SQ_INSTS_VALU") and not any(u in kk for u in util) and not kk.startswith("decode:")}
+        if vk:
+            tot = sum(vk.values())
+            step_s = elapsed_max / args.steps
+            out_valu = {"valu_instr_per_step": int(tot), "clock_ghz": clock_ghz,
+                        "busy_4clk": round(4 * tot / (1024 * clock_ghz * 1e9 * step_s), 4),
+                        "kernels": len(vk), "sources": [pmc_path, clk_path],
+                        "note": "wave64 VALU instructions of the step's kernels (PMC, per launch) x 4 clocks / "
+                                "(1024 SIMDs x loaded clock x ms_per_step); above 1.0 some issue in 2 clocks"}
+        else:
+            out_valu = None
+    else:
+        out_valu = None
     step_comp = I * n * bps + R * (bps + 2 * d) + regen * bps
     step_cps = step_comp / (elapsed_max / args.steps)
     out["sha256_chip"] = {"compressions_per_step": int(step_comp), "achieved": round(step_cps / 1e9, 2),
@@ -626,6 +665,7 @@ def report(args, ctx, I, n, k, d, S, present_h, corrupt_h, stage_ms, iso, elapse
                           "frac_of_attainable": round(step_cps / SHA_PROBE_CPS, 3),
                           "note": "leaves (all N rows) + ECHO verify (received rows + branch walk) + interpolate's "
                                   "regenerated rows, per ms_per_step"}
+    out["valu_step"] = out_valu
     src = iso if iso is not None else (stage_ms if not pipe else None)
     for key, stages, note in (("commit_only", ("enc", "leaf", "tree"), "RS encode + Merkle build alone "
                                "(BASELINE configs[1]'s stages): encode + leaf hashing + tree spans of serial steps"),

@@ -479,13 +479,11 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
         g.count = count;
         g.R = rmax;
         g.K = c->k;
-        // gf_regen_kernel: 1 KiB column tiles (16 B per lane), or 768 B (12 B
-        // per lane) where that keeps more lanes busy (C4: S = 763 -> 64 of 64
-        // lanes instead of 48)
+        // gf_regen_kernel: one wave per column tile owns every missing row;
+        // 512-B tiles (8 B per lane), or 256 B (4 B per lane) for short rows,
+        // where they keep the lanes busy (C4: S = 763 -> 3 tiles, 99 %)
         const uint32_t S = shard_lens ? (uint32_t)shard_pitch : uniform_shard_len;
-        const double u16 = (double)S / (1024.0 * ((S + 1023) / 1024));
-        const double u12 = (double)S / (768.0 * ((S + 767) / 768));
-        g.wpt = u12 > u16 + 0.05 ? 3 : 4;
+        g.wpt = S <= 2048 ? 1 : 2;
         g.tiles = (int)((shard_pitch + 256 * g.wpt - 1) / (256 * g.wpt));
         g.mode = GF_MODE_DECODE;
         g.in = shards;

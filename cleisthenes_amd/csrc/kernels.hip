@@ -22,46 +22,7 @@
 
 using namespace rbcdev;
 
-namespace {
-
-using rsrc_t = __amdgpu_buffer_rsrc_t;
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
-constexpr int RBC_RSRC_DW3 = 0x00020000;  // gfx9 raw buffer, bounds-checked
-
-RBC_DEV rsrc_t make_rsrc(const void *p, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, RBC_RSRC_DW3);
-}
-RBC_DEV uint4 bload16(rsrc_t r, uint32_t off) {
-    auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
-    return make_uint4(v[0], v[1], v[2], v[3]);
-}
-// per-lane offset + a wave-uniform one (a row start), which the buffer
-// instruction takes as its scalar soffset: no per-lane address arithmetic
-RBC_DEV uint4 bload16s(rsrc_t r, uint32_t voff, uint32_t soff) {
-    auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0);
-    return make_uint4(v[0], v[1], v[2], v[3]);
-}
-RBC_DEV uint32_t uniform(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
-RBC_DEV uint32_t inst_len(const uint32_t *lens, uint32_t uniform, int i) { return lens ? lens[i] : uniform; }
-
-// byte mask keeping the first `nv` bytes (little-endian) of a word
-RBC_DEV uint32_t keep_bytes(int nv) {
-    return nv >= 4 ? 0xffffffffu : (nv <= 0 ? 0u : ((1u << (8 * nv)) - 1u));
-}
-RBC_DEV uint4 mask16(uint4 v, int nvalid) {
-    v.x &= keep_bytes(nvalid);
-    v.y &= keep_bytes(nvalid - 4);
-    v.z &= keep_bytes(nvalid - 8);
-    v.w &= keep_bytes(nvalid - 12);
-    return v;
-}
-// gfx950 runs with unaligned global/buffer access enabled (hipcc itself
-// emits dwordx4 for byte-aligned pointers), so a 16-byte row read at any
-// byte offset is a single buffer_load_dwordx4; bounds are still checked by
-// the buffer descriptor (out of range -> 0).
-
-}  // namespace
+#include "buffer_io.h"
 
 // ============================================================================
 // gf_rows: out[r] = XOR_j coef[r][j] * in[j]   (klauspost codeSomeShards)
@@ -227,214 +188,6 @@ __global__ __launch_bounds__(TPB, (RC <= 21 ? 3 : 2)) void gf_rows_kernel(GfArgs
                 }
             }
         }
-    }
-}
-
-// ============================================================================
-// gf_regen: interpolate's missing data rows with the FFT codec (decode mode,
-// no compare / copy): out[r] = XOR_j D[r][j] * in[j] for the rcount[i] <= R
-// missing rows of each instance.
-//
-// One block per (instance, column tile); a tile is 64 lanes x W words.  The
-// block's NW waves split the instance's m missing rows evenly between them
-// (at most RC rows a wave; a pass holds NW * RC rows, i.e. all but a few
-// C1-C4 instances in one), and each reads the k input rows of the tile.
-// They share them through the CU's L1 / the XCD's L2 only as far as they stay
-// in step: PMC reads are 1.29x (C2) / 1.68x (C4) of the algorithmic k*S.  A block
-// barrier every trip keeps them in step (1.08x / 1.12x) and costs 0.5-2 % of
-// the pipelined step (tools/gpu_runs/gpu_r03q.sh), so there is none.  The five perm
-// tables of each coefficient sit in a per-wave LDS region, built for JC
-// inputs at a time by the wave itself (no barrier for them: one wave's LDS
-// operations complete in order), and read by wave-uniform broadcast at a
-// VGPR base with immediate offsets.  Byte selectors of an input word are
-// computed once per wave and shared by up to RC rows.
-// ============================================================================
-template <int W>
-struct GfVec {
-    uint32_t v[W];
-};
-template <int V>
-struct IntC {
-    static constexpr int value = V;
-};
-// f(IntC<rows>{}) for a runtime rows in [I, MAX]
-template <int I, int MAX, class F>
-__device__ __forceinline__ void dispatch_rows(int rows, F &&f) {
-    if constexpr (I <= MAX) {
-        if (rows == I) f(IntC<I>{});
-        else dispatch_rows<I + 1, MAX>(rows, f);
-    }
-}
-
-// <= 128 VGPRs (4 waves per SIMD); a cap of 2 waves measured the same
-// under the pipeline (tools/gpu_runs/gpu_r03j.sh)
-template <int W, int RC, int JC, int NW>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) void gf_regen_kernel(GfArgs a) {
-    static_assert(JC % 4 == 0, "two input pairs per trip");
-    set_wave_prio(a.prio);
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    // the wave index is uniform per wave: readfirstlane tells the compiler,
-    // so the per-wave row split below stays in SGPRs and scalar branches
-    const int wave = (int)uniform(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
-    const int inst = (int)blockIdx.x / a.tiles;
-    const int tile = (int)blockIdx.x - inst * a.tiles;
-    if (inst >= a.count) return;
-    if (a.status && a.status[inst] != 0) return;
-    const int m = min(a.rcount[inst], a.R);
-    if (m <= 0) return;
-    const uint32_t tile0 = (uint32_t)tile * (256u * W);
-    if (tile0 >= a.out_row_pitch) return;
-    const uint32_t my_off = tile0 + 4u * W * (uint32_t)lane;
-    const uint32_t S = inst_len(a.lens, a.uniform_len, inst);
-    const int K = a.K;
-    const int KP = (K + 3) & ~3;
-    constexpr uint32_t T01_B = 16u * RC * JC, T2_B = 8u * RC * (JC / 2);
-    const uint32_t wave_b = T01_B + T2_B + 4u * (uint32_t)(KP + 8);  // % 16 == 0 (KP % 4 == 0)
-    unsigned char *wbase = smem + (size_t)wave * wave_b;
-    uint4 *s_t01 = reinterpret_cast<uint4 *>(wbase);
-    uint2 *s_t2 = reinterpret_cast<uint2 *>(wbase + T01_B);
-    uint32_t *s_off = reinterpret_cast<uint32_t *>(wbase + T01_B + T2_B);
-    const uint8_t *in_inst = a.in + (size_t)inst * a.in_inst_pitch;
-    uint8_t *out_inst = a.out + (size_t)inst * a.out_inst_pitch;
-    const rsrc_t rin = make_rsrc(in_inst, a.in_inst_bytes);
-    const rsrc_t rout = make_rsrc(out_inst, (uint32_t)a.out_inst_pitch);
-    const uint8_t *idx = a.in_idx + (size_t)inst * a.idx_stride;
-    // input row starts; the prefetch past K reads row 0 (never accumulated)
-    for (int t = lane; t < KP + 8; t += 64) s_off[t] = (t < K ? (uint32_t)idx[t] : 0u) * a.in_row_pitch;
-    const uint8_t *coef = a.coef + (size_t)inst * a.coef_inst_stride;
-
-    auto load_row = [&](int j) -> GfVec<W> {
-        const uint32_t so = uniform(s_off[j]);
-        GfVec<W> x;
-        if constexpr (W == 4) {
-            auto v = __builtin_amdgcn_raw_buffer_load_b128(rin, (int)my_off, (int)so, 0);
-            x.v[0] = v[0]; x.v[1] = v[1]; x.v[2] = v[2]; x.v[3] = v[3];
-        } else {
-            static_assert(W == 3, "W = 3 or 4");
-            auto v = __builtin_amdgcn_raw_buffer_load_b96(rin, (int)my_off, (int)so, 0);
-            x.v[0] = v[0]; x.v[1] = v[1]; x.v[2] = v[2];
-        }
-        return x;
-    };
-
-    // one pass = up to NW * RC rows, split between the waves (wave-uniform;
-    // see the loop below).  The pass body is instantiated per row count RG,
-    // so the unrolled multiply-accumulate is straight-line: a per-row exit
-    // inside it costs the compiler ~2x the registers (spills).
-    auto pass = [&](auto rgc, int r0, int rows) {
-        constexpr int RG = decltype(rgc)::value;
-        // the lane id through an opaque copy: otherwise LLVM hoists every row
-        // count's lane-derived table addresses (e / RG, my_off, ...) out of
-        // the pass to the kernel entry, where 12 sets of them stay live and
-        // spilled (116 B of scratch per lane: the dirty scratch lines were
-        // ~1x the missing rows' bytes of extra HBM writes and reads, PMC r04b)
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
-        uint32_t acc[RG][W];
-#pragma unroll
-        for (int r = 0; r < RG; ++r)
-#pragma unroll
-            for (int w = 0; w < W; ++w) acc[r][w] = 0;
-        // tables of inputs [j0, j0 + JC) for the RG rows, layout [j][r] (t2
-        // as {j even, j odd} pairs), zero past `rows`: one VGPR base plus
-        // immediates per input pair in the loop
-        auto build = [&](int j0) {
-            // consecutive lanes take consecutive rows of one input: their
-            // 16-byte table stores are adjacent in LDS (input-major lanes
-            // stored RC * 16 bytes apart, a 16-way bank conflict)
-            for (int e = ln; e < RG * JC; e += 64) {
-                const int jl = e / RG, r = e - jl * RG, j = j0 + jl;
-                const uint32_t cf = (j < K && r < rows) ? coef[(size_t)(r0 + r) * K + j] : 0u;
-                uint4 t01;
-                uint32_t t2;
-                gf_tables(cf, t01, t2);
-                s_t01[jl * RC + r] = t01;
-                reinterpret_cast<uint32_t *>(s_t2)[((jl >> 1) * RC + r) * 2 + (jl & 1)] = t2;
-            }
-        };
-        auto mac_pair = [&](int jl, const GfVec<W> &xa, const GfVec<W> &xb) {
-            GfSel sa[W], sb[W];
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                sa[w] = gf_sel(xa.v[w]);
-                sb[w] = gf_sel(xb.v[w]);
-            }
-            uint32_t o01 = (uint32_t)jl * (16u * RC), o2 = (uint32_t)(jl >> 1) * (8u * RC);
-            asm volatile("" : "+v"(o01), "+v"(o2));  // VGPR base: no per-read v_mov of an SGPR address
-            const unsigned char *p01 = reinterpret_cast<const unsigned char *>(s_t01) + o01;
-            const unsigned char *p2 = reinterpret_cast<const unsigned char *>(s_t2) + o2;
-#pragma unroll
-            for (int r = 0; r < RG; ++r) {
-                const uint4 ta = *reinterpret_cast<const uint4 *>(p01 + 16 * r);
-                const uint4 tb = *reinterpret_cast<const uint4 *>(p01 + 16 * (RC + r));
-                const uint2 t2 = *reinterpret_cast<const uint2 *>(p2 + 8 * r);
-#pragma unroll
-                for (int w = 0; w < W; ++w)
-                    acc[r][w] = xor3(acc[r][w], gf_mul4(ta, t2.x, sa[w]), gf_mul4(tb, t2.y, sb[w]));
-            }
-        };
-        // two buffers of an input pair each, every load issued one pair of
-        // multiplies ahead of its use (see gf_rows_kernel)
-        GfVec<W> a0 = load_row(0), a1 = load_row(1), b0, b1;
-        for (int j = 0; j < KP; j += 4) {
-            b0 = load_row(j + 2);
-            b1 = load_row(j + 3);
-            const int jl = j % JC;  // JC % 4 == 0: a chunk starts at a trip
-            if (jl == 0) build(j);
-            mac_pair(jl, a0, a1);
-            a0 = load_row(j + 4);
-            a1 = load_row(j + 5);
-            mac_pair(jl + 2, b0, b1);
-        }
-        // zero the bytes past S; never write past the row pitch.  Each lane
-        // stores its W words as ONE dwordx4 / dwordx3 (a wave's store then
-        // fills whole 128-B lines; per-word stores wrote a quarter of every
-        // line they touched and PMC showed 1.9x the missing rows' bytes
-        // written).  The pitch is a multiple of 64 B, so only a W = 3 lane of
-        // the row's last tile can straddle it, and only that lane takes the
-        // word-guarded path.
-        const int nvalid = (int)S - (int)my_off;
-        const uint8_t *oidx = a.out_idx + (size_t)inst * a.idx_stride2 + r0;
-        const bool whole = my_off + 4u * W <= a.out_row_pitch;
-        const bool part = !whole && my_off < a.out_row_pitch;
-#pragma unroll
-        for (int r = 0; r < RG; ++r) {
-            if (r < rows) {
-                const uint32_t so = uniform((uint32_t)oidx[r] * a.out_row_pitch);
-                uint32_t v[W];
-#pragma unroll
-                for (int w = 0; w < W; ++w) v[w] = acc[r][w] & keep_bytes(nvalid - 4 * w);
-                if (whole) {
-                    if constexpr (W == 4) {
-                        __builtin_amdgcn_raw_buffer_store_b128(u32x4{v[0], v[1], v[2], v[3]}, rout, (int)my_off,
-                                                               (int)so, 0);
-                    } else {
-                        __builtin_amdgcn_raw_buffer_store_b96(u32x3{v[0], v[1], v[2]}, rout, (int)my_off, (int)so,
-                                                              0);
-                    }
-                } else if (part) {
-#pragma unroll
-                    for (int w = 0; w < W; ++w)
-                        if (my_off + 4u * w < a.out_row_pitch)
-                            __builtin_amdgcn_raw_buffer_store_b32(v[w], rout, (int)(my_off + 4u * w), (int)so, 0);
-                }
-            }
-        }
-    };
-    // a pass covers up to NW * RC rows; they go evenly to the fewest waves
-    // that hold them, each wave running the body for exactly its row count
-    // (round 3's 4-row groups padded ~1.5 zero-table rows a pass: ~10 % of
-    // the multiplies at C1-C4); a wave left idle ends at once (every pass
-    // but the last is full)
-    for (int base = 0; base < m; base += NW * RC) {
-        const int mp = min(NW * RC, m - base);
-        const int nw = (mp + RC - 1) / RC;  // active waves (block-uniform)
-        const int q = mp / nw, rem = mp - q * nw;
-        const int rows = wave < nw ? q + (wave < rem) : 0;
-        if (rows == 0) return;  // idle: only in the last pass
-        const int r0 = base + wave * q + min(wave, rem);
-        static_assert(RC <= 16, "up to 16 rows per wave");
-        dispatch_rows<1, RC>(rows, [&](auto rgc) { pass(rgc, r0, rows); });
     }
 }
 
@@ -973,7 +726,7 @@ __global__ __launch_bounds__(64) void merkle_recheck_kernel(RecheckArgs a) {
 // Leaves come from sha_rows_kernel<false>; this kernel writes valid[].
 // ============================================================================
 template <int L>
-__global__ __launch_bounds__(64) void merkle_path_kernel(PathArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void merkle_path_kernel(PathArgs a) {
     set_wave_prio(a.prio);
     // one wave per block; lane owns leaf positions p = s*64 + lane (s < L)
     __shared__ uint32_t s_pair[64 * L][17];  // +1 word: conflict-free rows; an owner's task
@@ -998,13 +751,37 @@ __global__ __launch_bounds__(64) void merkle_path_kernel(PathArgs a) {
         pm[s] = __ballot(part[s]);
         if (part[s]) load_digest(a.leaves + (size_t)inst_s[s] * a.leaves_inst_pitch + 32u * jj[s], x[s]);
     }
-    auto pmask = [&](int w) -> uint64_t {
-        uint64_t m = pm[0];
+    // participation masks by leaf word, read at a runtime word index: from
+    // LDS (a select chain over pm[] became a scratch array in the 4-level form)
+    __shared__ uint64_t s_pm[L];
+    if (lane == 0) {
 #pragma unroll
-        for (int s = 1; s < L; ++s) m = (w == s) ? pm[s] : m;
-        return m;
-    };
-    for (int l = 0; l < a.depth; ++l) {
+        for (int s = 0; s < L; ++s) s_pm[s] = pm[s];
+    }
+    __syncthreads();
+    auto pmask = [&](int w) -> uint64_t { return s_pm[w]; };
+    // QL levels of every participating leaf's branch are read at once: at W =
+    // 256 (C4, d = 8) a leaf's levels 4q..4q+3 are one 128-B line, so each
+    // line crosses HBM once instead of once per level (the levels of a block
+    // are far apart in time, and the lines of the blocks in flight on an XCD
+    // outgrow its L2: round 3 read 3.4x the branch bytes).  128 more VGPRs
+    // per lane: one wave per SIMD, 4 blocks per CU.
+    constexpr int QL = L == 4 ? 4 : 1;
+    uint32_t sq[L][QL][8];
+    for (int lq = 0; lq < a.depth; lq += QL) {
+#pragma unroll
+        for (int s = 0; s < L; ++s) {
+            if (!part[s]) continue;
+            const uint8_t *br = a.branches + (size_t)inst_s[s] * a.br_inst_pitch + ((size_t)jj[s] * a.depth + lq) * 32u;
+#pragma unroll
+            for (int t = 0; t < QL; ++t)
+                if (lq + t < a.depth) load_digest(br + 32u * t, sq[s][t]);
+        }
+    // one level, t a compile-time index into sq (a loop index kept sq in scratch)
+    auto level = [&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        const int l = lq + t;
+        if (l < a.depth) {  // wave-uniform
         // 1. each leaf's ordered input (left || right) for level l
 #pragma unroll
         for (int s = 0; s < L; ++s) {
@@ -1012,12 +789,8 @@ __global__ __launch_bounds__(64) void merkle_path_kernel(PathArgs a) {
             const int p = s * 64 + lane, j = jj[s];
             const bool empty = (l == 0) && ((j ^ 1) >= a.n);
             uint32_t sib[8];
-            if (empty) {
 #pragma unroll
-                for (int q = 0; q < 8; ++q) sib[q] = 0;
-            } else {
-                load_digest(a.branches + (size_t)inst_s[s] * a.br_inst_pitch + ((size_t)j * a.depth + l) * 32u, sib);
-            }
+            for (int q = 0; q < 8; ++q) sib[q] = empty ? 0u : sq[s][t][q];
             const bool right = (j >> l) & 1;
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
@@ -1105,6 +878,14 @@ __global__ __launch_bounds__(64) void merkle_path_kernel(PathArgs a) {
             for (int q = 0; q < 8; ++q) x[s][q] = s_pair[o][q];
         }
         __syncthreads();
+        }
+    };
+    level(IntC<0>{});
+    if constexpr (QL == 4) {
+        level(IntC<1>{});
+        level(IntC<2>{});
+        level(IntC<3>{});
+    }
     }
 #pragma unroll
     for (int s = 0; s < L; ++s) {
@@ -1780,31 +1561,6 @@ hipError_t rbc_launch_gf_rows(const GfArgs &a, hipStream_t st) {
     }
 }
 
-hipError_t rbc_launch_gf_regen(const GfArgs &a, hipStream_t st) {
-    if (a.count <= 0 || a.R <= 0) return hipSuccess;
-    if (a.mode != GF_MODE_DECODE || !a.rcount || a.nmiss || a.copy || a.K < 1 || a.K > 248 || a.tiles < 1)
-        return hipErrorInvalidValue;
-    const int W = a.wpt == 3 ? 3 : 4;
-    if ((uint64_t)a.tiles * 256u * W < a.out_row_pitch) return hipErrorInvalidValue;
-    const uint64_t blocks = (uint64_t)a.count * a.tiles;
-    if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    constexpr int JC = 16;
-    const int KP = (a.K + 3) & ~3;
-    const dim3 grid((unsigned)blocks);
-    if (W == 3) {
-        // C4 (m ~ 29 +- 4.4 of k = 86): up to 48 rows in one pass, so every
-        // input row is read once per tile; two waves hold m <= 32
-        constexpr int RC = 16, NW = 3;
-        const size_t lds = NW * ((size_t)20 * RC * JC + 4 * (KP + 8));
-        hipLaunchKernelGGL((gf_regen_kernel<3, RC, JC, NW>), grid, dim3(64 * NW), lds, st, a);
-    } else {
-        constexpr int RC = 12, NW = 2;  // C1-C3 (m ~ 7-15 of k = 22-44): one pass for m <= 24
-        const size_t lds = NW * ((size_t)20 * RC * JC + 4 * (KP + 8));
-        hipLaunchKernelGGL((gf_regen_kernel<4, RC, JC, NW>), grid, dim3(64 * NW), lds, st, a);
-    }
-    return hipGetLastError();
-}
-
 hipError_t rbc_launch_sha_rows(const ShaArgs &a, bool verify, hipStream_t st) {
     const long total = (long)a.count * a.rows_per_inst;
     if (total <= 0) return hipSuccess;
@@ -1865,17 +1621,16 @@ hipError_t rbc_launch_merkle_path(const PathArgs &a, hipStream_t st) {
     const int L = a.width > 64 ? a.width / 64 : 1;
     b.inst_per_block = a.width >= 64 ? 1 : 64 / a.width;
     const dim3 grid((unsigned)((a.count + b.inst_per_block - 1) / b.inst_per_block));
-    // W = 256 (C4): dynamic LDS caps the kernel at 3 resident blocks per CU
-    // (46 KiB each of the 160).  Each block walks 8 levels over its instance's
-    // branches, touching every 128-B branch line once per level; with the 8
-    // blocks per CU the VGPRs allow, the lines of the blocks in flight on an
-    // XCD do not stay in its 4 MiB L2 between levels.  Measured at C4
-    // (tools/gpu_runs/gpu_r04c.sh, profiles/r04c*): 8 blocks per CU read 2.74
-    // GB per launch, 4 (38 KiB) 1.64, 3 1.34; the step 350.7-351.4 (8),
-    // 349.3-349.8 (5), 355.3-355.5 (4 and 3) GB/s.
-    constexpr size_t kPathStaticLds = sizeof(uint32_t) * 256 * 17 + 256 + 2 * 256;
-    constexpr size_t kPathBlockLds = 46 * 1024;
-    if (L == 4) hipLaunchKernelGGL(merkle_path_kernel<4>, grid, dim3(64), kPathBlockLds - kPathStaticLds, st, b);
+    // W = 256 (C4): the kernel holds 4 branch levels of its 4 leaves per lane
+    // (>256 VGPRs, one wave per SIMD, 4 blocks per CU).  Fewer blocks in
+    // flight also pays by itself (tools/gpu_runs/gpu_r04c.sh, profiles/r04c*,
+    // branch loads per level, resident blocks capped with dynamic LDS): 8
+    // blocks per CU read 2.74 GB per launch, 4 1.64, 3 1.34; the step
+    // 350.7-351.4 (8), 349.3-349.8 (5), 355.3-355.5 (4 and 3) GB/s.
+#ifndef RBC_AB_PATH_PAD
+#define RBC_AB_PATH_PAD 0  // A/B only (tools/build_ab.sh): dynamic LDS that caps the blocks resident per CU
+#endif
+    if (L == 4) hipLaunchKernelGGL(merkle_path_kernel<4>, grid, dim3(64), RBC_AB_PATH_PAD, st, b);
     else if (L == 2) hipLaunchKernelGGL(merkle_path_kernel<2>, grid, dim3(64), 0, st, b);
     else hipLaunchKernelGGL(merkle_path_kernel<1>, grid, dim3(64), 0, st, b);
     return hipGetLastError();

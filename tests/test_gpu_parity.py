@@ -1121,16 +1121,16 @@ def test_host_interpolate_zero_copy_reads_present_rows_only(gpu, ref, n, f, B, p
 
 REGEN_COUNTS = [
     # (n, f, S, missing data rows per instance, parity rows absent too):
-    # gf_regen_kernel splits an instance's m rows evenly over the fewest
-    # waves of a block that hold them (12 B per lane for short rows: 3 waves
-    # x 16 rows per pass; 16 B per lane: 2 waves x 12), and runs the pass body
-    # for exactly each wave's count, so the counts straddle every wave and
-    # pass boundary of both forms.  With parity rows absent as well, the
+    # gf_regen_kernel gives each 256-B (S <= 2048) or 512-B column tile to one
+    # wave, which accumulates every missing row in passes of at most 40 / 24
+    # rows (one body per exact row count), its block's 3 / 4 waves sharing the
+    # LDS tables; the counts straddle every pass boundary of both forms, and a
+    # last tile group with idle waves.  With parity rows absent as well, the
     # first-k set takes the first m present parity rows, not parity 0..m-1
-    (256, 85, 763, [1, 3, 4, 5, 12, 13, 16, 17, 29, 32, 33, 47, 48, 49, 64, 86], False),
+    (256, 85, 763, [1, 3, 4, 5, 16, 17, 29, 39, 40, 41, 48, 64, 79, 80, 81, 86], False),
     (128, 42, 23832, [1, 4, 5, 11, 12, 13, 23, 24, 25, 44], False),
-    (128, 42, 700, [1, 4, 16, 17, 32, 33, 44], False),
-    (256, 85, 763, [1, 12, 13, 29, 48, 49, 86], True),
+    (128, 42, 700, [1, 4, 16, 17, 32, 39, 40, 41, 44], False),
+    (256, 85, 763, [1, 12, 13, 29, 40, 41, 86], True),
     (128, 42, 23832, [1, 12, 13, 24, 25, 44], True),
     (128, 42, 95326, [1, 12, 13, 24, 25, 44], True),  # C3's shard (4 MiB values)
     (64, 21, 47663, [1, 11, 12, 13, 22], True),       # C1's geometry and shard (1 MiB values)
@@ -1176,12 +1176,13 @@ def test_device_regen_missing_data_row_counts(gpu, n, f, S, ms, parity_gone):
             assert not after[i][:, S:].any(), (mode, i, m)
 
 
-@pytest.mark.parametrize("S", [763, 100, 1400, 1500, 2000])
+@pytest.mark.parametrize("S", [763, 100, 1400, 1500, 2000, 2049, 3000])
 def test_device_interpolate_short_rows(gpu, S):
-    """Missing-data GF rows for short shards (one-wave tiles: 12 bytes per
-    lane where that keeps more lanes busy -- C4's S = 763 -- including a last
-    tile that straddles the row pitch, S = 1400): interpolate returns the
-    value and rewrites every regenerated row exactly as committed, zero past S."""
+    """Missing-data GF rows for short shards (256-B column tiles up to S =
+    2048, C4's S = 763 in 3; 512-B above), including last tile groups whose
+    waves have no tile (S = 2000: 8 tiles in blocks of 3; S = 2049: 5 in
+    blocks of 4) and lanes past the row pitch: interpolate returns the value
+    and rewrites every regenerated row exactly as committed, zero past S."""
     n, f, I = 256, 85, 6
     k = n - 2 * f
     pl = Pipeline(gpu, n, f, k * S, I, seed=S, corrupt_frac=0.3)
