@@ -94,8 +94,10 @@ __global__ __launch_bounds__(TPB, (RC <= 21 ? 3 : 2)) void gf_rows_kernel(GfArgs
             }
             return v;
         } else {
-            // the row position is wave-uniform: row start in SGPRs (s_mul), not a per-lane v_mul_lo
-            return bload16s(rin, my_off, uniform(s_in[j]) * a.in_row_pitch);
+            // the row position is wave-uniform: row start in SGPRs (s_mul), not a per-lane v_mul_lo;
+            // a lane past the pitch (never stored) loads a clamped column: the buffer range check
+            // does not cover the scalar row offset, so the last row's overhang could leave the buffer
+            return bload16s(rin, min(my_off, a.in_row_pitch - 16u), uniform(s_in[j]) * a.in_row_pitch);
         }
     };
 
@@ -766,7 +768,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void me
     // are far apart in time, and the lines of the blocks in flight on an XCD
     // outgrow its L2: round 3 read 3.4x the branch bytes).  128 more VGPRs
     // per lane: one wave per SIMD, 4 blocks per CU.
-    constexpr int QL = L == 4 ? 4 : 1;
+#ifndef RBC_AB_PATH_Q8
+#define RBC_AB_PATH_Q8 2  // A/B: branch levels held per leaf when a wave owns two W = 256 instances
+#endif
+    constexpr int QL = L == 4 ? 4 : L == 8 ? RBC_AB_PATH_Q8 : 1;
     uint32_t sq[L][QL][8];
     for (int lq = 0; lq < a.depth; lq += QL) {
 #pragma unroll
@@ -881,8 +886,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void me
         }
     };
     level(IntC<0>{});
+    if constexpr (QL >= 2) level(IntC<1>{});
     if constexpr (QL == 4) {
-        level(IntC<1>{});
         level(IntC<2>{});
         level(IntC<3>{});
     }
@@ -1619,7 +1624,11 @@ hipError_t rbc_launch_merkle_path(const PathArgs &a, hipStream_t st) {
     // were slower still (70 KB of LDS per block).
     PathArgs b = a;
     const int L = a.width > 64 ? a.width / 64 : 1;
-    b.inst_per_block = a.width >= 64 ? 1 : 64 / a.width;
+#ifndef RBC_AB_PATH_PAIR
+#define RBC_AB_PATH_PAIR 0  // A/B: 1 = one wave owns two W = 256 instances (L = 8)
+#endif
+    const bool pair = RBC_AB_PATH_PAIR && a.width == 256;
+    b.inst_per_block = pair ? 2 : a.width >= 64 ? 1 : 64 / a.width;
     const dim3 grid((unsigned)((a.count + b.inst_per_block - 1) / b.inst_per_block));
     // W = 256 (C4): the kernel holds 4 branch levels of its 4 leaves per lane
     // (>256 VGPRs, one wave per SIMD, 4 blocks per CU).  Fewer blocks in
@@ -1630,7 +1639,8 @@ hipError_t rbc_launch_merkle_path(const PathArgs &a, hipStream_t st) {
 #ifndef RBC_AB_PATH_PAD
 #define RBC_AB_PATH_PAD 0  // A/B only (tools/build_ab.sh): dynamic LDS that caps the blocks resident per CU
 #endif
-    if (L == 4) hipLaunchKernelGGL(merkle_path_kernel<4>, grid, dim3(64), RBC_AB_PATH_PAD, st, b);
+    if (pair) hipLaunchKernelGGL(merkle_path_kernel<8>, grid, dim3(64), RBC_AB_PATH_PAD, st, b);
+    else if (L == 4) hipLaunchKernelGGL(merkle_path_kernel<4>, grid, dim3(64), RBC_AB_PATH_PAD, st, b);
     else if (L == 2) hipLaunchKernelGGL(merkle_path_kernel<2>, grid, dim3(64), 0, st, b);
     else hipLaunchKernelGGL(merkle_path_kernel<1>, grid, dim3(64), 0, st, b);
     return hipGetLastError();
