@@ -479,12 +479,7 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
         g.count = count;
         g.R = rmax;
         g.K = c->k;
-        // gf_regen_kernel: one wave per column tile owns every missing row;
-        // 512-B tiles (8 B per lane), or 256 B (4 B per lane) for short rows,
-        // where they keep the lanes busy (C4: S = 763 -> 3 tiles, 99 %)
-        const uint32_t S = shard_lens ? (uint32_t)shard_pitch : uniform_shard_len;
-        g.wpt = S <= 2048 ? 1 : 2;
-        g.tiles = (int)((shard_pitch + 256 * g.wpt - 1) / (256 * g.wpt));
+        // gf_regen_kernel's column tiles and block shape: rbc_launch_gf_regen (gf_regen.hip)
         g.mode = GF_MODE_DECODE;
         g.in = shards;
         g.in_inst_pitch = (uint64_t)c->n * shard_pitch;

@@ -44,10 +44,10 @@ __device__ __forceinline__ void dispatch_rows(int rows, F &&f) {
     }
 }
 
-template <int W, int RC, int JC, int NT>
-__global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(4))) void gf_regen_kernel(GfArgs a) {
+template <int W, int RC, int JC, int NT, int WPE>
+__global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(WPE))) void gf_regen_kernel(GfArgs a) {
     static_assert(JC % 4 == 0, "two input pairs per trip");
-    static_assert(W == 1 || W == 2 || W == 4, "1, 2 or 4 words per lane");
+    static_assert(W >= 1 && W <= 4, "1 to 4 words per lane");
     set_wave_prio(a.prio);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wave = (int)uniform(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
@@ -88,6 +88,9 @@ __global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(4))) vo
         if constexpr (W == 4) {
             auto v = __builtin_amdgcn_raw_buffer_load_b128(rin, (int)ld_off, (int)so, 0);
             x.v[0] = v[0]; x.v[1] = v[1]; x.v[2] = v[2]; x.v[3] = v[3];
+        } else if constexpr (W == 3) {
+            auto v = __builtin_amdgcn_raw_buffer_load_b96(rin, (int)ld_off, (int)so, 0);
+            x.v[0] = v[0]; x.v[1] = v[1]; x.v[2] = v[2];
         } else if constexpr (W == 2) {
             auto v = __builtin_amdgcn_raw_buffer_load_b64(rin, (int)ld_off, (int)so, 0);
             x.v[0] = v[0]; x.v[1] = v[1];
@@ -185,6 +188,15 @@ __global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(4))) vo
                 for (int w = 0; w < W; ++w) v[w] = acc[r][w] & keep_bytes(nvalid - 4 * w);
                 if constexpr (W == 4) {
                     __builtin_amdgcn_raw_buffer_store_b128(u32x4{v[0], v[1], v[2], v[3]}, rout, (int)my_off, (int)so, 0);
+                } else if constexpr (W == 3) {
+                    if (my_off + 12u <= pitch) {
+                        __builtin_amdgcn_raw_buffer_store_b96(u32x3{v[0], v[1], v[2]}, rout, (int)my_off, (int)so, 0);
+                    } else {  // the last tile's lane that straddles the pitch (pitch % 12 != 0)
+#pragma unroll
+                        for (int w = 0; w < 3; ++w)
+                            if (my_off + 4u * w < pitch)
+                                __builtin_amdgcn_raw_buffer_store_b32(v[w], rout, (int)(my_off + 4u * w), (int)so, 0);
+                    }
                 } else if constexpr (W == 2) {
                     __builtin_amdgcn_raw_buffer_store_b64(u32x2{v[0], v[1]}, rout, (int)my_off, (int)so, 0);
                 } else {
@@ -203,22 +215,33 @@ __global__ __launch_bounds__(64 * NT) __attribute__((amdgpu_waves_per_eu(4))) vo
 
 hipError_t rbc_launch_gf_regen(const GfArgs &a, hipStream_t st) {
     if (a.count <= 0 || a.R <= 0) return hipSuccess;
-    if (a.mode != GF_MODE_DECODE || !a.rcount || a.nmiss || a.copy || a.K < 1 || a.K > 248 || a.tiles < 1)
+    if (a.mode != GF_MODE_DECODE || !a.rcount || a.nmiss || a.copy || a.K < 1 || a.K > 248 || a.out_row_pitch % 4u)
         return hipErrorInvalidValue;
-    const int W = a.wpt == 1 ? 1 : 2;
-    if ((uint64_t)a.tiles * 256u * W < a.out_row_pitch || a.out_row_pitch % (4u * W)) return hipErrorInvalidValue;
+    // one wave per column tile owns every missing row: 512-B tiles (8 B per
+    // lane), or 256 B (4 B per lane) for rows of at most 2 KiB, where they keep
+    // the lanes busy (C4: S = 763 -> 3 tiles, 99 %)
+    const uint32_t S = a.lens ? a.out_row_pitch : a.uniform_len;
+#ifndef RBC_AB_REGEN_W3
+#define RBC_AB_REGEN_W3 0  // A/B: rows of 513..768 B as one 768-B tile per wave (12 B per lane)
+#endif
+    const int W = (RBC_AB_REGEN_W3 && S > 512 && S <= 768) ? 3 : S <= 2048 ? 1 : 2;
+    GfArgs b = a;
+    b.wpt = W;
+    b.tiles = (int)((a.out_row_pitch + 256u * W - 1) / (256u * W));
     constexpr int JC = 16;
     const int KP = (a.K + 3) & ~3;
     auto go = [&](auto kern, int RC, int NT) {
-        const uint64_t blocks = (uint64_t)a.count * ((a.tiles + NT - 1) / NT);
+        const uint64_t blocks = (uint64_t)b.count * ((b.tiles + NT - 1) / NT);
         if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
         const size_t lds = 2 * (size_t)24 * RC * JC + 4 * (size_t)(KP + 8);
-        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(64 * NT), lds, st, a);
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(64 * NT), lds, st, b);
         return hipGetLastError();
     };
+    if (W == 3)  // A/B (RBC_AB_REGEN_W3): C4's 768-B row in one wave's tile, every row of the instance
+        return go(gf_regen_kernel<3, 32, JC, 1, 3>, 32, 1);
     if (W == 1)  // short rows (C4: S = 763, 3 tiles of 256 B; m ~ 29 +- 4 of k = 86 in one pass)
-        return go(gf_regen_kernel<1, 40, JC, 3>, 40, 3);
+        return go(gf_regen_kernel<1, 40, JC, 3, 4>, 40, 3);
     // long rows (C1-C3: m ~ 7-15 of k = 22-44): 512-B tiles, four to a block
-    return go(gf_regen_kernel<2, 24, JC, 4>, 24, 4);
+    return go(gf_regen_kernel<2, 24, JC, 4, 4>, 24, 4);
 }
 

@@ -11,10 +11,10 @@ enum { GF_MODE_ENCODE = 0, GF_MODE_DECODE = 1 };
 
 struct GfArgs {
     int count;                 // instances
-    int tiles;                 // column tiles per instance (gf_rows: 16 * tpb bytes; gf_regen: 256 * wpt)
+    int tiles;                 // column tiles per instance (gf_rows: 16 * tpb bytes; gf_regen: set by its launcher)
     int rc;                    // rows per chunk (template)
     int tpb;                   // gf_rows: threads per block, 256 (4 KiB tiles); 0 = 256
-    int wpt;                   // gf_regen: words per lane, 1 (256 B tiles) or 2 (512 B tiles)
+    int wpt;                   // gf_regen: words per lane (set by rbc_launch_gf_regen)
     int R, K;                  // output rows, input rows per instance
     int mode;                  // GF_MODE_*
     const uint8_t *in;         // encode: values [I][value_pitch]; decode: shards [I][N][pitch]
@@ -211,8 +211,8 @@ hipError_t rbc_launch_rs_fft(const FftArgs &a, hipStream_t st);
 
 int rbc_gf_pick_rc(int R, int rcmax);
 hipError_t rbc_launch_gf_rows(const GfArgs &a, hipStream_t st);
-// interpolate's missing data rows (FFT codec, gf_regen.hip): tiles of 256 * W bytes, W = 1
-// when a.wpt == 1 else 2 (one wave per tile, every row); needs rcount (per-instance row count <= R)
+// interpolate's missing data rows (FFT codec, gf_regen.hip): one wave per column tile of 256 * W
+// bytes owns every row (W and the tiles chosen from the row length); needs rcount (row count <= R)
 hipError_t rbc_launch_gf_regen(const GfArgs &a, hipStream_t st);
 hipError_t rbc_launch_sha_rows(const ShaArgs &a, bool verify, hipStream_t st);
 // receive step: v's rows (list or all; branch walk + verdict when v_walk) and
