@@ -20,4 +20,5 @@ PASSES="sq1 fetch write" bash tools/pmc_passes.sh r04d_c4 --config c4 --steps 5 
 PASSES="sq1 sq2" bash tools/pmc_passes.sh r04d_c2s --pipeline 0 --steps 5 --warmup 3 --no-isolated --no-joined-leg $Q || { echo PMCFAIL c2s; exit 1; }
 mkdir -p $O/calib && cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $R/$O/calib -o run --output-format csv -- $R/tools/probes/fetch_calib > $R/$O/calib.txt 2>&1 || { echo CALIBFAIL; tail -20 $R/$O/calib.txt; exit 1; }
 grep useful $R/$O/calib.txt
+cd $R && bash tools/gpu_runs/gpu_r04e.sh || { echo R04EFAIL; exit 1; }
 echo ok
