@@ -221,10 +221,9 @@ hipError_t rbc_launch_gf_regen(const GfArgs &a, hipStream_t st) {
     // lane), or 256 B (4 B per lane) for rows of at most 2 KiB, where they keep
     // the lanes busy (C4: S = 763 -> 3 tiles, 99 %)
     const uint32_t S = a.lens ? a.out_row_pitch : a.uniform_len;
-#ifndef RBC_AB_REGEN_W3
-#define RBC_AB_REGEN_W3 0  // A/B: rows of 513..768 B as one 768-B tile per wave (12 B per lane)
-#endif
-    const int W = (RBC_AB_REGEN_W3 && S > 512 && S <= 768) ? 3 : S <= 2048 ? 1 : 2;
+    // (C4's 768-B row as ONE tile of 12 B per lane, a wave owning the whole
+    // instance at 167 VGPRs: 308-312 against 320 GB/s, tools/gpu_runs/gpu_r04e.sh)
+    const int W = S <= 2048 ? 1 : 2;
     GfArgs b = a;
     b.wpt = W;
     b.tiles = (int)((a.out_row_pitch + 256u * W - 1) / (256u * W));
@@ -237,8 +236,6 @@ hipError_t rbc_launch_gf_regen(const GfArgs &a, hipStream_t st) {
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(64 * NT), lds, st, b);
         return hipGetLastError();
     };
-    if (W == 3)  // A/B (RBC_AB_REGEN_W3): C4's 768-B row in one wave's tile, every row of the instance
-        return go(gf_regen_kernel<3, 32, JC, 1, 3>, 32, 1);
     if (W == 1)  // short rows (C4: S = 763, 3 tiles of 256 B; m ~ 29 +- 4 of k = 86 in one pass)
         return go(gf_regen_kernel<1, 40, JC, 3, 4>, 40, 3);
     // long rows (C1-C3: m ~ 7-15 of k = 22-44): 512-B tiles, four to a block

@@ -728,7 +728,7 @@ __global__ __launch_bounds__(64) void merkle_recheck_kernel(RecheckArgs a) {
 // Leaves come from sha_rows_kernel<false>; this kernel writes valid[].
 // ============================================================================
 template <int L>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void merkle_path_kernel(PathArgs a) {
+__global__ __launch_bounds__(64) void merkle_path_kernel(PathArgs a) {
     set_wave_prio(a.prio);
     // one wave per block; lane owns leaf positions p = s*64 + lane (s < L)
     __shared__ uint32_t s_pair[64 * L][17];  // +1 word: conflict-free rows; an owner's task
@@ -762,27 +762,34 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void me
     }
     __syncthreads();
     auto pmask = [&](int w) -> uint64_t { return s_pm[w]; };
-    // QL levels of every participating leaf's branch are read at once: at W =
-    // 256 (C4, d = 8) a leaf's levels 4q..4q+3 are one 128-B line, so each
-    // line crosses HBM once instead of once per level (the levels of a block
-    // are far apart in time, and the lines of the blocks in flight on an XCD
-    // outgrow its L2: round 3 read 3.4x the branch bytes).  128 more VGPRs
-    // per lane: one wave per SIMD, 4 blocks per CU.
-#ifndef RBC_AB_PATH_Q8
-#define RBC_AB_PATH_Q8 2  // A/B: branch levels held per leaf when a wave owns two W = 256 instances
-#endif
-    constexpr int QL = L == 4 ? 4 : L == 8 ? RBC_AB_PATH_Q8 : 1;
-    uint32_t sq[L][QL][8];
+    // At W = 256 (C4, d = 8) a leaf's branch levels 4q..4q+3 are one 128-B
+    // line.  They are staged in LDS four levels at a time, every line of the
+    // instance's participating leaves read once, whole, by 8 consecutive lanes:
+    // the levels of a block are far apart in time and the lines of the blocks
+    // in flight on an XCD outgrow its L2, so loading one 32-B sibling per level
+    // read 3.4x the branch bytes (round 3).  The 32 KiB stage also holds the
+    // kernel at 3 blocks per CU, the residency that measured fastest
+    // (tools/gpu_runs/gpu_r04c.sh); holding the levels in VGPRs instead (332
+    // per lane) read them once too but crowded the other stream off the SIMDs
+    // (C4 320 against 351 GB/s, gpu_r04d.sh).
+    constexpr int QL = L == 4 ? 4 : 1;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint4 *s_stage = reinterpret_cast<uint4 *>(smem);  // [64 * L][8] x 16 B when QL == 4
     for (int lq = 0; lq < a.depth; lq += QL) {
-#pragma unroll
-        for (int s = 0; s < L; ++s) {
-            if (!part[s]) continue;
-            const uint8_t *br = a.branches + (size_t)inst_s[s] * a.br_inst_pitch + ((size_t)jj[s] * a.depth + lq) * 32u;
-#pragma unroll
-            for (int t = 0; t < QL; ++t)
-                if (lq + t < a.depth) load_digest(br + 32u * t, sq[s][t]);
+        if constexpr (QL == 4) {
+            const int nl = min(4, a.depth - lq);  // levels in this stage
+            __syncthreads();                        // the previous stage's reads are done
+            for (int c = lane; c < 64 * L * 8; c += 64) {
+                const int p = c >> 3, piece = c & 7;
+                if (piece >= 2 * nl || !((pmask(p >> 6) >> (p & 63)) & 1ull)) continue;
+                const int g = p >> lgW, j = p & (W - 1);
+                s_stage[c] = *reinterpret_cast<const uint4 *>(
+                    a.branches + (size_t)((int)blockIdx.x * a.inst_per_block + g) * a.br_inst_pitch +
+                    ((size_t)j * a.depth + lq) * 32u + 16u * piece);
+            }
+            __syncthreads();
         }
-    // one level, t a compile-time index into sq (a loop index kept sq in scratch)
+    // one level of the stage (t a compile-time index)
     auto level = [&](auto tc) {
         constexpr int t = decltype(tc)::value;
         const int l = lq + t;
@@ -794,8 +801,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void me
             const int p = s * 64 + lane, j = jj[s];
             const bool empty = (l == 0) && ((j ^ 1) >= a.n);
             uint32_t sib[8];
+            if (empty) {
 #pragma unroll
-            for (int q = 0; q < 8; ++q) sib[q] = empty ? 0u : sq[s][t][q];
+                for (int q = 0; q < 8; ++q) sib[q] = 0u;
+            } else if constexpr (QL == 4) {
+                load_digest(reinterpret_cast<const uint8_t *>(s_stage + p * 8 + 2 * t), sib);
+            } else {
+                load_digest(a.branches + (size_t)inst_s[s] * a.br_inst_pitch + ((size_t)j * a.depth + l) * 32u, sib);
+            }
             const bool right = (j >> l) & 1;
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
@@ -886,8 +899,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void me
         }
     };
     level(IntC<0>{});
-    if constexpr (QL >= 2) level(IntC<1>{});
     if constexpr (QL == 4) {
+        level(IntC<1>{});
         level(IntC<2>{});
         level(IntC<3>{});
     }
@@ -1624,23 +1637,15 @@ hipError_t rbc_launch_merkle_path(const PathArgs &a, hipStream_t st) {
     // were slower still (70 KB of LDS per block).
     PathArgs b = a;
     const int L = a.width > 64 ? a.width / 64 : 1;
-#ifndef RBC_AB_PATH_PAIR
-#define RBC_AB_PATH_PAIR 0  // A/B: 1 = one wave owns two W = 256 instances (L = 8)
-#endif
-    const bool pair = RBC_AB_PATH_PAIR && a.width == 256;
-    b.inst_per_block = pair ? 2 : a.width >= 64 ? 1 : 64 / a.width;
+    b.inst_per_block = a.width >= 64 ? 1 : 64 / a.width;
     const dim3 grid((unsigned)((a.count + b.inst_per_block - 1) / b.inst_per_block));
-    // W = 256 (C4): the kernel holds 4 branch levels of its 4 leaves per lane
-    // (>256 VGPRs, one wave per SIMD, 4 blocks per CU).  Fewer blocks in
-    // flight also pays by itself (tools/gpu_runs/gpu_r04c.sh, profiles/r04c*,
-    // branch loads per level, resident blocks capped with dynamic LDS): 8
-    // blocks per CU read 2.74 GB per launch, 4 1.64, 3 1.34; the step
-    // 350.7-351.4 (8), 349.3-349.8 (5), 355.3-355.5 (4 and 3) GB/s.
-#ifndef RBC_AB_PATH_PAD
-#define RBC_AB_PATH_PAD 0  // A/B only (tools/build_ab.sh): dynamic LDS that caps the blocks resident per CU
-#endif
-    if (pair) hipLaunchKernelGGL(merkle_path_kernel<8>, grid, dim3(64), RBC_AB_PATH_PAD, st, b);
-    else if (L == 4) hipLaunchKernelGGL(merkle_path_kernel<4>, grid, dim3(64), RBC_AB_PATH_PAD, st, b);
+    // W = 256 (C4): 32 KiB of dynamic LDS stage four branch levels of every
+    // leaf (see the kernel); with the 18 KiB of its static LDS, 3 blocks per CU.
+    // Measured residency alone (tools/gpu_runs/gpu_r04c.sh, one sibling load per
+    // level, blocks capped with dynamic LDS): 8 blocks per CU read 2.74 GB per
+    // launch, 4 1.64, 3 1.34; the step 350.7-351.4 (8), 349.3-349.8 (5),
+    // 355.3-355.5 (4 and 3) GB/s.
+    if (L == 4) hipLaunchKernelGGL(merkle_path_kernel<4>, grid, dim3(64), (size_t)64 * 4 * 128, st, b);
     else if (L == 2) hipLaunchKernelGGL(merkle_path_kernel<2>, grid, dim3(64), 0, st, b);
     else hipLaunchKernelGGL(merkle_path_kernel<1>, grid, dim3(64), 0, st, b);
     return hipGetLastError();
