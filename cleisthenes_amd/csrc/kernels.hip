@@ -772,15 +772,18 @@ __global__ __launch_bounds__(64) void merkle_path_kernel(PathArgs a) {
     // (tools/gpu_runs/gpu_r04c.sh); holding the levels in VGPRs instead (332
     // per lane) read them once too but crowded the other stream off the SIMDs
     // (C4 320 against 351 GB/s, gpu_r04d.sh).
-    constexpr int QL = L == 4 ? 4 : 1;
+    // (A/B, RBC_AB_PATH_PAIR: two W = 256 instances per wave, L = 8, their
+    // level's hash tasks on one wave's lanes; 2 levels staged, 32 KiB)
+    constexpr int QL = L == 4 ? 4 : L == 8 ? 2 : 1;
+    constexpr int PPL = 2 * QL;  // 16-B pieces per leaf and stage
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint4 *s_stage = reinterpret_cast<uint4 *>(smem);  // [64 * L][8] x 16 B when QL == 4
+    uint4 *s_stage = reinterpret_cast<uint4 *>(smem);  // [64 * L][PPL] x 16 B when QL > 1
     for (int lq = 0; lq < a.depth; lq += QL) {
-        if constexpr (QL == 4) {
-            const int nl = min(4, a.depth - lq);  // levels in this stage
-            __syncthreads();                        // the previous stage's reads are done
-            for (int c = lane; c < 64 * L * 8; c += 64) {
-                const int p = c >> 3, piece = c & 7;
+        if constexpr (QL > 1) {
+            const int nl = min(QL, a.depth - lq);  // levels in this stage
+            __syncthreads();                         // the previous stage's reads are done
+            for (int c = lane; c < 64 * L * PPL; c += 64) {
+                const int p = c / PPL, piece = c % PPL;
                 if (piece >= 2 * nl || !((pmask(p >> 6) >> (p & 63)) & 1ull)) continue;
                 const int g = p >> lgW, j = p & (W - 1);
                 s_stage[c] = *reinterpret_cast<const uint4 *>(
@@ -804,8 +807,8 @@ __global__ __launch_bounds__(64) void merkle_path_kernel(PathArgs a) {
             if (empty) {
 #pragma unroll
                 for (int q = 0; q < 8; ++q) sib[q] = 0u;
-            } else if constexpr (QL == 4) {
-                load_digest(reinterpret_cast<const uint8_t *>(s_stage + p * 8 + 2 * t), sib);
+            } else if constexpr (QL > 1) {
+                load_digest(reinterpret_cast<const uint8_t *>(s_stage + p * PPL + 2 * t), sib);
             } else {
                 load_digest(a.branches + (size_t)inst_s[s] * a.br_inst_pitch + ((size_t)j * a.depth + l) * 32u, sib);
             }
@@ -899,8 +902,8 @@ __global__ __launch_bounds__(64) void merkle_path_kernel(PathArgs a) {
         }
     };
     level(IntC<0>{});
+    if constexpr (QL >= 2) level(IntC<1>{});
     if constexpr (QL == 4) {
-        level(IntC<1>{});
         level(IntC<2>{});
         level(IntC<3>{});
     }
@@ -1637,7 +1640,11 @@ hipError_t rbc_launch_merkle_path(const PathArgs &a, hipStream_t st) {
     // were slower still (70 KB of LDS per block).
     PathArgs b = a;
     const int L = a.width > 64 ? a.width / 64 : 1;
-    b.inst_per_block = a.width >= 64 ? 1 : 64 / a.width;
+#ifndef RBC_AB_PATH_PAIR
+#define RBC_AB_PATH_PAIR 0  // A/B only: two W = 256 instances per wave (L = 8)
+#endif
+    const bool pair = RBC_AB_PATH_PAIR && a.width == 256;
+    b.inst_per_block = pair ? 2 : a.width >= 64 ? 1 : 64 / a.width;
     const dim3 grid((unsigned)((a.count + b.inst_per_block - 1) / b.inst_per_block));
     // W = 256 (C4): 32 KiB of dynamic LDS stage four branch levels of every
     // leaf (see the kernel); with the 18 KiB of its static LDS, 3 blocks per CU.
@@ -1645,7 +1652,8 @@ hipError_t rbc_launch_merkle_path(const PathArgs &a, hipStream_t st) {
     // level, blocks capped with dynamic LDS): 8 blocks per CU read 2.74 GB per
     // launch, 4 1.64, 3 1.34; the step 350.7-351.4 (8), 349.3-349.8 (5),
     // 355.3-355.5 (4 and 3) GB/s.
-    if (L == 4) hipLaunchKernelGGL(merkle_path_kernel<4>, grid, dim3(64), (size_t)64 * 4 * 128, st, b);
+    if (pair) hipLaunchKernelGGL(merkle_path_kernel<8>, grid, dim3(64), (size_t)64 * 8 * 64, st, b);
+    else if (L == 4) hipLaunchKernelGGL(merkle_path_kernel<4>, grid, dim3(64), (size_t)64 * 4 * 128, st, b);
     else if (L == 2) hipLaunchKernelGGL(merkle_path_kernel<2>, grid, dim3(64), 0, st, b);
     else hipLaunchKernelGGL(merkle_path_kernel<1>, grid, dim3(64), 0, st, b);
     return hipGetLastError();
