@@ -18,4 +18,5 @@ for run in c4_1 c1 c4_2 c3 c4_3; do
 done
 PASSES="sq1 fetch write" bash tools/pmc_passes.sh r04f_c4 --config c4 --steps 5 --warmup 3 --no-isolated --no-joined-leg $Q || { echo PMCFAIL c4; exit 1; }
 PASSES="sq1 sq2" bash tools/pmc_passes.sh r04f_c4s --config c4 --pipeline 0 --steps 5 --warmup 3 --no-isolated --no-joined-leg $Q || { echo PMCFAIL c4s; exit 1; }
+bash tools/gpu_runs/gpu_r04g.sh || { echo R04GFAIL; exit 1; }
 echo ok
