@@ -764,31 +764,51 @@ __global__ __launch_bounds__(64) void merkle_path_kernel(PathArgs a) {
     auto pmask = [&](int w) -> uint64_t { return s_pm[w]; };
     // At W = 256 (C4, d = 8) a leaf's branch levels 4q..4q+3 are one 128-B
     // line.  They are staged in LDS four levels at a time, every line of the
-    // instance's participating leaves read once, whole, by 8 consecutive lanes:
-    // the levels of a block are far apart in time and the lines of the blocks
-    // in flight on an XCD outgrow its L2, so loading one 32-B sibling per level
-    // read 3.4x the branch bytes (round 3).  The 32 KiB stage also holds the
-    // kernel at 3 blocks per CU, the residency that measured fastest
-    // (tools/gpu_runs/gpu_r04c.sh); holding the levels in VGPRs instead (332
-    // per lane) read them once too but crowded the other stream off the SIMDs
-    // (C4 320 against 351 GB/s, gpu_r04d.sh).
-    // (A/B, RBC_AB_PATH_PAIR: two W = 256 instances per wave, L = 8, their
-    // level's hash tasks on one wave's lanes; 2 levels staged, 32 KiB)
-    constexpr int QL = L == 4 ? 4 : L == 8 ? 2 : 1;
+    // instance's participating leaves read once, whole, by 8 consecutive lanes
+    // with 8 loads per lane in flight: the levels of a block are far apart in
+    // time and the lines of the blocks in flight on an XCD outgrow its L2, so
+    // loading one 32-B sibling per level read 1.34-2.74 GB per launch against
+    // 0.80 GB of branches (round 3 and tools/gpu_runs/gpu_r04c.sh).  The
+    // 32 KiB stage also holds the kernel at 3 blocks per CU, a residency that
+    // measured fastest (gpu_r04c.sh).  Measured at C4 (GB/s): this form
+    // 355.6 (gpu_r04j.sh); per-level loads at 3 / 4 / 8 blocks per CU 355-356,
+    // 355-361, 355 (gpu_r04i.sh, gpu_r04j.sh); the stage waiting on every load
+    // 336 (gpu_r04f.sh); the levels in VGPRs (332 per lane) 320 (gpu_r04d.sh);
+    // two instances per wave 263 (gpu_r04g.sh).
+#ifndef RBC_AB_PATH_QL
+#define RBC_AB_PATH_QL 4  // A/B: 1 = one 32-B sibling load per level, 2 = two levels staged
+#endif
+    constexpr int QL = L == 4 ? RBC_AB_PATH_QL : 1;
     constexpr int PPL = 2 * QL;  // 16-B pieces per leaf and stage
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint4 *s_stage = reinterpret_cast<uint4 *>(smem);  // [64 * L][PPL] x 16 B when QL > 1
+    // the block's branches (the launcher keeps inst_per_block * pitch < 4 GiB)
+    const rsrc_t rb = make_rsrc(a.branches + (size_t)blockIdx.x * a.inst_per_block * a.br_inst_pitch,
+                                (uint32_t)((uint64_t)a.inst_per_block * a.br_inst_pitch));
     for (int lq = 0; lq < a.depth; lq += QL) {
         if constexpr (QL > 1) {
             const int nl = min(QL, a.depth - lq);  // levels in this stage
             __syncthreads();                         // the previous stage's reads are done
-            for (int c = lane; c < 64 * L * PPL; c += 64) {
-                const int p = c / PPL, piece = c % PPL;
-                if (piece >= 2 * nl || !((pmask(p >> 6) >> (p & 63)) & 1ull)) continue;
-                const int g = p >> lgW, j = p & (W - 1);
-                s_stage[c] = *reinterpret_cast<const uint4 *>(
-                    a.branches + (size_t)((int)blockIdx.x * a.inst_per_block + g) * a.br_inst_pitch +
-                    ((size_t)j * a.depth + lq) * 32u + 16u * piece);
+            // batches of SB pieces per lane: every load of a batch in flight
+            // before the first LDS write (one wait per batch, not per piece)
+#ifndef RBC_AB_PATH_SB
+#define RBC_AB_PATH_SB 8  // A/B: stage loads in flight per lane
+#endif
+            constexpr int SB = RBC_AB_PATH_SB;
+#pragma unroll 1
+            for (int c0 = 0; c0 < L * PPL; c0 += SB) {
+                uint4 v[SB];
+#pragma unroll
+                for (int u = 0; u < SB; ++u) {  // no branch: an idle piece reads past the buffer (0)
+                    const int c = (c0 + u) * 64 + lane;
+                    const int p = c / PPL, piece = c % PPL;
+                    const bool on = piece < 2 * nl && ((pmask(p >> 6) >> (p & 63)) & 1ull);
+                    const uint32_t off = (uint32_t)(p >> lgW) * (uint32_t)a.br_inst_pitch +
+                                         ((uint32_t)(p & (W - 1)) * a.depth + lq) * 32u + 16u * piece;
+                    v[u] = bload16(rb, on ? off : 0xfffffff0u);
+                }
+#pragma unroll
+                for (int u = 0; u < SB; ++u) s_stage[(c0 + u) * 64 + lane] = v[u];
             }
             __syncthreads();
         }
@@ -1640,20 +1660,16 @@ hipError_t rbc_launch_merkle_path(const PathArgs &a, hipStream_t st) {
     // were slower still (70 KB of LDS per block).
     PathArgs b = a;
     const int L = a.width > 64 ? a.width / 64 : 1;
-#ifndef RBC_AB_PATH_PAIR
-#define RBC_AB_PATH_PAIR 0  // A/B only: two W = 256 instances per wave (L = 8)
-#endif
-    const bool pair = RBC_AB_PATH_PAIR && a.width == 256;
-    b.inst_per_block = pair ? 2 : a.width >= 64 ? 1 : 64 / a.width;
+    b.inst_per_block = a.width >= 64 ? 1 : 64 / a.width;
+    if (L == 4 && a.br_inst_pitch > 0xffffffffull)
+        return hipErrorInvalidValue;  // the stage's buffer descriptor spans an instance's branches
     const dim3 grid((unsigned)((a.count + b.inst_per_block - 1) / b.inst_per_block));
     // W = 256 (C4): 32 KiB of dynamic LDS stage four branch levels of every
     // leaf (see the kernel); with the 18 KiB of its static LDS, 3 blocks per CU.
-    // Measured residency alone (tools/gpu_runs/gpu_r04c.sh, one sibling load per
-    // level, blocks capped with dynamic LDS): 8 blocks per CU read 2.74 GB per
-    // launch, 4 1.64, 3 1.34; the step 350.7-351.4 (8), 349.3-349.8 (5),
-    // 355.3-355.5 (4 and 3) GB/s.
-    if (pair) hipLaunchKernelGGL(merkle_path_kernel<8>, grid, dim3(64), (size_t)64 * 8 * 64, st, b);
-    else if (L == 4) hipLaunchKernelGGL(merkle_path_kernel<4>, grid, dim3(64), (size_t)64 * 4 * 128, st, b);
+#ifndef RBC_AB_PATH_LDS
+#define RBC_AB_PATH_LDS (64 * 4 * 32 * RBC_AB_PATH_QL)  // A/B: the stage (or a residency pad when QL = 1)
+#endif
+    if (L == 4) hipLaunchKernelGGL(merkle_path_kernel<4>, grid, dim3(64), (size_t)RBC_AB_PATH_LDS, st, b);
     else if (L == 2) hipLaunchKernelGGL(merkle_path_kernel<2>, grid, dim3(64), 0, st, b);
     else hipLaunchKernelGGL(merkle_path_kernel<1>, grid, dim3(64), 0, st, b);
     return hipGetLastError();
