@@ -785,6 +785,167 @@ __global__ __launch_bounds__(64) void merkle_path_kernel(PathArgs a) {
     // the block's branches (the launcher keeps inst_per_block * pitch < 4 GiB)
     const rsrc_t rb = make_rsrc(a.branches + (size_t)blockIdx.x * a.inst_per_block * a.br_inst_pitch,
                                 (uint32_t)((uint64_t)a.inst_per_block * a.br_inst_pitch));
+    // ---- Speculative top levels (W = 256).  Levels 0 and 1 run exactly as
+    // above (128 + 64 tasks fill the lanes); levels 2..7 would take one pass
+    // each for 32, 16, .. 1 tasks.  Instead every node above level 2 is hashed
+    // at once from the values the branches CLAIM for its children: claim(v)
+    // at level l is the level-l branch entry of the first participating leaf
+    // under v's sibling.  The instance is proven -- every participating leaf
+    // valid -- when (i) all participating leaves under each level-l node v
+    // (l >= 2) hold the same level-l entry, (ii) all of them reached the same
+    // exact level-2 value X(v), equal to claim(v) where that exists, and (iii)
+    // each node's hash equals its claim (the root at the top).  Then, by
+    // induction over the levels, each leaf's own walk computes exactly these
+    // hashes and ends at the root.  A child with no claim (no participant
+    // under its sibling) takes its own task's hash instead: a later pass.
+    // Anything else re-runs levels 2..7 exactly (the per-level form above),
+    // so valid[] is bit-identical to the per-leaf walk for every input.
+#ifndef RBC_PATH_SPEC
+#define RBC_PATH_SPEC 1  // A/B: 0 = every level exact
+#endif
+    constexpr bool SPEC = RBC_PATH_SPEC && L == 4 && QL == 4;
+    constexpr int L0 = 2;                 // first speculative level
+    int lo = 0, hi = SPEC ? L0 : a.depth;  // exact levels of this pass: [lo, hi)
+    bool spec = SPEC, proven = false, sfail = false;
+    // spec scratch in s_pair (no exact level runs meanwhile), in words:
+    // claims [126][8] (raw bytes; level l at node v: row 128 - (256 >> (l-1)) + v),
+    // X2 [64][8] at 1008, task hashes [63][8] at 1520, task done flags [63] at 2024
+    uint32_t *s_raw = &s_pair[0][0];
+    auto claim_row = [](int l, int v) { return 128 - (256 >> (l - 1)) + v; };
+    auto task_of = [](int m, int v) { return 64 - (256 >> (m - 1)) + v; };  // node v at level m >= 3
+    auto sub_mask = [&](int l, int v) -> uint64_t {  // participants under node (l, v), l <= 6
+        const int p0 = v << l;
+        const uint64_t m = pmask(p0 >> 6);
+        return l >= 6 ? m : (m >> (p0 & 63)) & ((1ull << (1 << l)) - 1ull);
+    };
+    auto has = [&](int l, int v) -> bool {
+        if (l <= 6) return sub_mask(l, v) != 0;
+        uint64_t m = 0;
+        for (int w = (v << l) >> 6; w < ((v + 1) << l) >> 6; ++w) m |= pmask(w);
+        return m != 0;
+    };
+    auto rep_of = [&](int l, int v, int self) -> int {  // first participant under (l, v)
+        if (l <= 6) return (v << l) + __builtin_ctzll(sub_mask(l, v));
+        for (int w = (v << l) >> 6; w < ((v + 1) << l) >> 6; ++w) {
+            const uint64_t m = pmask(w);
+            if (m) return w * 64 + __builtin_ctzll(m);
+        }
+        return self;
+    };
+    auto eq8 = [](const uint4 &a0, const uint4 &a1, const uint4 &b0, const uint4 &b1) {
+        return a0.x == b0.x && a0.y == b0.y && a0.z == b0.z && a0.w == b0.w && a1.x == b1.x && a1.y == b1.y &&
+               a1.z == b1.z && a1.w == b1.w;
+    };
+    // the staged levels lq..lq+3: check (i) and publish the claims
+    auto spec_collect = [&](int lq) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int l = lq + t;
+            if (l < L0) continue;
+#pragma unroll
+            for (int s = 0; s < L; ++s) {
+                if (!part[s]) continue;
+                const int p = s * 64 + lane, v = p >> l, r = rep_of(l, v, p);
+                const uint4 m0 = s_stage[p * PPL + 2 * t], m1 = s_stage[p * PPL + 2 * t + 1];
+                if (r == p) {
+                    uint4 *c = reinterpret_cast<uint4 *>(s_raw + 8 * claim_row(l, v ^ 1));
+                    c[0] = m0;
+                    c[1] = m1;
+                } else {
+                    sfail |= !eq8(m0, m1, s_stage[r * PPL + 2 * t], s_stage[r * PPL + 2 * t + 1]);
+                }
+            }
+        }
+        if (lq == 0) {  // each level-2 node's first participant publishes its exact value
+#pragma unroll
+            for (int s = 0; s < L; ++s) {
+                const int p = s * 64 + lane;
+                if (part[s] && rep_of(L0, p >> L0, p) == p)
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) s_raw[1008 + 8 * (p >> L0) + q] = x[s][q];
+            }
+        }
+    };
+    auto claim_words = [&](int l, int v, uint32_t (&o)[8]) {
+        load_digest(reinterpret_cast<const uint8_t *>(s_raw + 8 * claim_row(l, v)), o);
+    };
+    // checks (ii) and (iii), the node hashes of levels 3..8; true = not proven
+    auto spec_finish = [&]() -> bool {
+        uint32_t *s_done = s_raw + 2024;
+        if (lane < 63) s_done[lane] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < L; ++s) {
+            if (!part[s]) continue;
+            const uint32_t *X = s_raw + 1008 + 8 * ((s * 64 + lane) >> L0);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) sfail |= x[s][q] != X[q];
+        }
+        // lane t: node P at level m (3..8), children 2P, 2P + 1 at level l
+        const int t = lane;
+        const int m = t < 32 ? 3 : t < 48 ? 4 : t < 56 ? 5 : t < 60 ? 6 : t < 62 ? 7 : 8;
+        const int P = t - task_of(m, 0), l = m - 1;
+        const bool h0 = t < 63 && has(l, 2 * P), h1 = t < 63 && has(l, 2 * P + 1);
+        const bool active = h0 || h1;
+        uint32_t in[2][8];
+        int dep[2] = {-1, -1};
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int c = 2 * P + k;
+            const bool hc = k ? h1 : h0, hs = k ? h0 : h1;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) in[k][q] = 0;
+            if (!active) continue;
+            if (l == L0 && hc) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) in[k][q] = s_raw[1008 + 8 * c + q];
+                if (hs) {
+                    uint32_t cl[8];
+                    claim_words(l, c, cl);
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) sfail |= cl[q] != in[k][q];
+                }
+            } else if (hs) {
+                claim_words(l, c, in[k]);
+            } else {
+                dep[k] = task_of(l, c);
+            }
+        }
+        bool done = false;
+        uint32_t h[8];
+        for (int it = 0; it < 8 - L0; ++it) {
+            const bool ready = active && !done && dep[0] < 0 && dep[1] < 0;
+            if (__ballot(ready) == 0) break;
+            if (ready) {
+                sha256_node64(in[0], in[1], h);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) s_raw[1520 + 8 * t + q] = h[q];
+                s_done[t] = 1;
+                done = true;
+            }
+            __syncthreads();
+            if (active && !done) {
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    if (dep[k] >= 0 && s_done[dep[k]]) {
+#pragma unroll
+                        for (int q = 0; q < 8; ++q) in[k][q] = s_raw[1520 + 8 * dep[k] + q];
+                        dep[k] = -1;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        if (active && !done) sfail = true;
+        if (done && (m == 8 || has(m, P ^ 1))) {
+            uint32_t ref[8];
+            if (m == 8) load_digest(a.roots + (size_t)inst_s[0] * 32u, ref);
+            else claim_words(m, P, ref);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) sfail |= h[q] != ref[q];
+        }
+        return __ballot(sfail) != 0;
+    };
     for (int lq = 0; lq < a.depth; lq += QL) {
         if constexpr (QL > 1) {
             const int nl = min(QL, a.depth - lq);  // levels in this stage
@@ -816,7 +977,7 @@ __global__ __launch_bounds__(64) void merkle_path_kernel(PathArgs a) {
     auto level = [&](auto tc) {
         constexpr int t = decltype(tc)::value;
         const int l = lq + t;
-        if (l < a.depth) {  // wave-uniform
+        if (l >= lo && l < hi) {  // wave-uniform
         // 1. each leaf's ordered input (left || right) for level l
 #pragma unroll
         for (int s = 0; s < L; ++s) {
@@ -927,12 +1088,27 @@ __global__ __launch_bounds__(64) void merkle_path_kernel(PathArgs a) {
         level(IntC<2>{});
         level(IntC<3>{});
     }
+    if constexpr (SPEC) {
+        if (spec) {  // wave-uniform
+            spec_collect(lq);
+            if (lq + QL >= a.depth) {
+                spec = false;
+                if (!spec_finish()) {
+                    proven = true;
+                    break;
+                }
+                lo = L0;  // not proven: levels 2..7 exactly, restaged from level 0
+                hi = a.depth;
+                lq = -QL;
+            }
+        }
+    }
     }
 #pragma unroll
     for (int s = 0; s < L; ++s) {
         if (!(ok_s[s] && jj[s] < a.n)) continue;
-        bool ok = false;
-        if (part[s]) {
+        bool ok = part[s] && proven;
+        if (part[s] && !proven) {
             uint32_t root[8];
             load_digest(a.roots + (size_t)inst_s[s] * 32u, root);
             ok = true;

@@ -873,6 +873,70 @@ def test_device_verify_shared_paths_adversarial(gpu, ref, n, f, B, I):
     assert got[0].all() and not got[4].any()
 
 
+@pytest.mark.parametrize("n,f", [(256, 85), (200, 66)])
+def test_device_verify_speculative_top_levels(gpu, ref, n, f):
+    """merkle_path_kernel's speculative top levels (W = 256: every node above
+    level 2 hashed at once from the children the branches claim, proven or
+    re-run exactly) against the per-leaf oracle walk, one instance per case:
+    honest; whole 8/16/32/128-leaf blocks absent (claims missing, a chain of
+    dependent node hashes up to six deep); a single participant; one leaf's
+    slot corrupted at each level 2..7; a level-3 subtree whose leaves agree on
+    a wrong level-3 sibling; two leaves of a level-2 node reaching different
+    level-2 values; a level-2 sibling claim that disagrees with the exact
+    value; a wrong root; nothing present; random sparse sets with random slot
+    corruption.  valid[i][j] must equal present && oracle verify."""
+    B, I = 9 * (n - 2 * f), 40
+    pl = Pipeline(gpu, n, f, B, I, seed=500 + n, corrupt_frac=0.0, present_n=n)
+    pl.commit()
+    c, b, d, S = pl.ctx, pl.b, pl.d, pl.S
+    assert d == 8
+    sh = pl.shards().copy()
+    roots = pl.arr("roots", shape=(I, 32)).copy()
+    brs = pl.arr("branches", shape=(I, n, d, 32)).copy()
+    rng = np.random.default_rng(3 + n)
+    present = np.ones((I, n), np.uint8)
+    i = 1
+    for blk in (8, 16, 32, 128):  # 1-4: whole blocks absent
+        present[i, blk:2 * blk] = 0
+        present[i, 0:min(n, 4)] = 0
+        i += 1
+    present[5] = 0  # 5: one participant
+    present[5, 37] = 1
+    for l in range(2, 8):  # 6-11: one leaf's level-l slot corrupted
+        brs[6 + l - 2, int(rng.integers(n)), l, int(rng.integers(32))] ^= 0x40
+    brs[12, 8:16, 3, 0] ^= 0x01  # 12: a level-3 subtree agrees on a wrong level-3 sibling
+    sh[13, 41, 0] ^= 0x01  # 13: leaf 41's level-2 value differs from leaves 40, 42, 43
+    brs[14, 4:8, 2, 7] ^= 0x80  # 14: leaves 4..7 claim a wrong value for node (2, 0)
+    roots[15, 31] ^= 0x01  # 15: wrong root
+    present[16] = 0  # 16: nothing present
+    brs[17, 0:64, 6, 3] ^= 0x02  # 17: the left quarter agrees on a wrong level-6 sibling
+    present[18] = 0  # 18: only the right half
+    present[18, 128:] = 1
+    for i in range(19, I):  # random sparse sets, some with a corrupted slot or shard
+        present[i] = (rng.random(n) < rng.uniform(0.05, 0.9)).astype(np.uint8)
+        if i % 3 == 0:
+            brs[i, int(rng.integers(n)), int(rng.integers(d)), int(rng.integers(32))] ^= 0x10
+        if i % 5 == 0:
+            sh[i, int(rng.integers(n)), int(rng.integers(S))] ^= 0x10
+    b["shards"].upload(sh)
+    b["branches"].upload(brs)
+    b["roots"].upload(roots)
+    b["present"].upload(present)
+    b["valid"].upload(np.full((I, n), 7, np.uint8))
+    c.dev_verify(None, I, b["shards"], pl.spitch, None, S, b["branches"], b["roots"], b["present"], b["valid"],
+                 b["leaves_r"])
+    got = pl.arr("valid", shape=(I, n))
+    for i in range(I):
+        for j in range(n):
+            slots = brs[i, j].copy()
+            if (j ^ 1) >= n:
+                slots[0] = 0
+            want = bool(present[i, j]) and ref.verify(n, sh[i, j, :S], j, slots, bytes(roots[i]))
+            assert got[i, j] == int(want), (n, i, j)
+    assert got[0].all() and got[1:5][present[1:5] == 1].all() and got[5, 37] and got[18, 128:].all()
+    assert not got[15].any() and not got[16].any() and not got[12, 8:16].any() and not got[17, 0:64].any()
+
+
 def test_device_verify_shared_paths_large_grid(gpu, ref):
     """The shared-path kernel over a large grid: 4096 instances at N = 256, 64 of them adversarial (corrupted shards and
     branch slots at random levels, a wrong root, a spliced subtree), checked
