@@ -2,7 +2,7 @@
 """Per-kernel-role durations from a rocprofv3 --kernel-trace CSV of bench.py.
 
 usage: tools/trace_summary.py <run_kernel_trace.csv> --config c2 [--instances 1024] [--last K]
-       [--json out.json]
+       [--before join_kernel] [--json out.json]
 
 Roles are told apart by kernel name plus grid size: sha_rows_kernel<false>
 is the commit-side leaf hashing when its grid covers every row (I*N threads)
@@ -12,7 +12,10 @@ Only the last `K` launches of each role are averaged (the bench's K timed
 steps; warmup launches come first, and launches on other batch sizes -- the
 PCIe host-path measurement -- have other grids, hence other roles), so the
 averages cover the same launches whose HIP-event spans bench.py reports as
-stage_ms / roofline.avg_ms.
+stage_ms / roofline.avg_ms.  `--before KERNEL` drops every launch from the first
+launch of KERNEL on: the default bench line's joined-value leg (join_kernel)
+runs after the timed region and the guard, so its launches would otherwise be
+the last ones.
 """
 import argparse
 import csv
@@ -43,11 +46,16 @@ def role(name, grid, n, k, inst):
     return b
 
 
-def summarize(path, config, inst, last):
+def summarize(path, config, inst, last, before=None):
     n, f = CONFIGS[config]
     k = n - 2 * f
     durs = []
-    for r in csv.DictReader(open(path)):
+    rows = list(csv.DictReader(open(path)))
+    if before:
+        cut = min((int(r["Start_Timestamp"]) for r in rows if base(r["Kernel_Name"]) == before), default=None)
+        if cut is not None:
+            rows = [r for r in rows if int(r["Start_Timestamp"]) < cut]
+    for r in rows:
         grid = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6  # ms
         durs.append((int(r["Dispatch_Id"]), role(r["Kernel_Name"], grid, n, k, inst), grid, d))
@@ -74,9 +82,10 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--instances", type=int, default=1024)
     ap.add_argument("--last", type=int, default=0, help="average only the last K launches per role (timed steps)")
+    ap.add_argument("--before", help="ignore launches from the first launch of this kernel on")
     ap.add_argument("--json")
     a = ap.parse_args()
-    res = summarize(a.trace, a.config, a.instances, a.last)
+    res = summarize(a.trace, a.config, a.instances, a.last, a.before)
     for rl, v in sorted(res.items(), key=lambda x: -x[1]["avg_ms"] * x[1]["timed_launches"]):
         print(f"{rl:46s} {v['timed_launches']:4d} x {v['avg_ms']:8.4f} ms  (min {v['min_ms']:.4f}, max {v['max_ms']:.4f})")
     if a.json:
