@@ -1858,7 +1858,8 @@ hipError_t rbc_launch_merkle(const MerkleArgs &a, bool check, hipStream_t st) {
     MerkleArgs b = a;
     // up to 512 / W trees per block (<= 64), but keep >= 512 blocks so that a
     // small batch still spreads over every CU (C2 and C4: 2 trees per block)
-    // (C4, W = 256, measured: 1 tree per block 0.68 ms, 2 trees 0.63, 4 trees 0.95)
+    // (C4, W = 256, measured: 1 tree per block 0.68 ms, 2 trees 0.63, 4 trees 0.95;
+    // in the pipelined step 4 trees per block equal to 2 at C2 and C4, gpu_r04l.sh)
     int g = a.width >= 512 ? 1 : (512 / a.width < 64 ? 512 / a.width : 64);
     while (g > 1 && (a.count + g - 1) / g < 512) g >>= 1;
     b.trees_per_block = g;
