@@ -775,10 +775,7 @@ __global__ __launch_bounds__(64) void merkle_path_kernel(PathArgs a) {
     // 355-361, 355 (gpu_r04i.sh, gpu_r04j.sh); the stage waiting on every load
     // 336 (gpu_r04f.sh); the levels in VGPRs (332 per lane) 320 (gpu_r04d.sh);
     // two instances per wave 263 (gpu_r04g.sh).
-#ifndef RBC_AB_PATH_QL
-#define RBC_AB_PATH_QL 4  // A/B: 1 = one 32-B sibling load per level, 2 = two levels staged
-#endif
-    constexpr int QL = L == 4 ? RBC_AB_PATH_QL : 1;
+    constexpr int QL = L == 4 ? 4 : 1;  // levels per stage (W = 256 only)
     constexpr int PPL = 2 * QL;  // 16-B pieces per leaf and stage
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint4 *s_stage = reinterpret_cast<uint4 *>(smem);  // [64 * L][PPL] x 16 B when QL > 1
@@ -800,10 +797,7 @@ __global__ __launch_bounds__(64) void merkle_path_kernel(PathArgs a) {
     // under its sibling) takes its own task's hash instead: a later pass.
     // Anything else re-runs levels 2..7 exactly (the per-level form above),
     // so valid[] is bit-identical to the per-leaf walk for every input.
-#ifndef RBC_PATH_SPEC
-#define RBC_PATH_SPEC 1  // A/B: 0 = every level exact
-#endif
-    constexpr bool SPEC = RBC_PATH_SPEC && L == 4 && QL == 4;
+    constexpr bool SPEC = L == 4;
     constexpr int L0 = 2;                 // first speculative level
     int lo = 0, hi = SPEC ? L0 : a.depth;  // exact levels of this pass: [lo, hi)
     bool spec = SPEC, proven = false, sfail = false;
@@ -952,10 +946,7 @@ __global__ __launch_bounds__(64) void merkle_path_kernel(PathArgs a) {
             __syncthreads();                         // the previous stage's reads are done
             // batches of SB pieces per lane: every load of a batch in flight
             // before the first LDS write (one wait per batch, not per piece)
-#ifndef RBC_AB_PATH_SB
-#define RBC_AB_PATH_SB 8  // A/B: stage loads in flight per lane
-#endif
-            constexpr int SB = RBC_AB_PATH_SB;
+            constexpr int SB = 8;  // 16 measured the same (gpu_r04j.sh)
 #pragma unroll 1
             for (int c0 = 0; c0 < L * PPL; c0 += SB) {
                 uint4 v[SB];
@@ -1842,10 +1833,7 @@ hipError_t rbc_launch_merkle_path(const PathArgs &a, hipStream_t st) {
     const dim3 grid((unsigned)((a.count + b.inst_per_block - 1) / b.inst_per_block));
     // W = 256 (C4): 32 KiB of dynamic LDS stage four branch levels of every
     // leaf (see the kernel); with the 18 KiB of its static LDS, 3 blocks per CU.
-#ifndef RBC_AB_PATH_LDS
-#define RBC_AB_PATH_LDS (64 * 4 * 32 * RBC_AB_PATH_QL)  // A/B: the stage (or a residency pad when QL = 1)
-#endif
-    if (L == 4) hipLaunchKernelGGL(merkle_path_kernel<4>, grid, dim3(64), (size_t)RBC_AB_PATH_LDS, st, b);
+    if (L == 4) hipLaunchKernelGGL(merkle_path_kernel<4>, grid, dim3(64), (size_t)64 * 4 * 128, st, b);
     else if (L == 2) hipLaunchKernelGGL(merkle_path_kernel<2>, grid, dim3(64), 0, st, b);
     else hipLaunchKernelGGL(merkle_path_kernel<1>, grid, dim3(64), 0, st, b);
     return hipGetLastError();
