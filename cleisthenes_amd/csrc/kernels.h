@@ -85,6 +85,7 @@ struct MerkleArgs {
     int trees_per_block;       // set by rbc_launch_merkle
     int prio;                  // wave issue priority 0..3 (set_wave_prio)
     const uint8_t *only;       // check: [I] nonzero = recheck this instance, others untouched (nullable = all)
+    int stop_m;                // build, set by rbc_launch_merkle: stop at the layer of stop_m nodes (0 = root)
 };
 
 // merkle_recheck_kernel: the receive step's root recheck over the nodes ECHO

@@ -440,7 +440,8 @@ __global__ __launch_bounds__(64) void merkle_kernel(MerkleArgs a) {
     const int G = a.trees_per_block, W = a.width, n = a.n;
     const int inst0 = (int)blockIdx.x * G;
     const int tid = threadIdx.x;
-    for (int m = W >> 1, lgm = a.depth - 1; m >= 1; m >>= 1, --lgm) {
+    const int m_last = (!CHECK && a.stop_m) ? a.stop_m : 1;
+    for (int m = W >> 1, lgm = a.depth - 1; m >= m_last; m >>= 1, --lgm) {
         for (int t = tid; t < G * m; t += 64) {
             const int g = t >> lgm, i = m + (t & (m - 1));
             const int inst = inst0 + g;
@@ -496,9 +497,25 @@ __global__ __launch_bounds__(64) void merkle_kernel(MerkleArgs a) {
         }
         __syncthreads();
     }
+    if (!CHECK && a.stop_m) {
+        // W = 256, stopped at the layer of 32 nodes (level 3): merkle_top_kernel
+        // finishes the tree.  Hand the layer over in the level-4..7 branch
+        // slots of leaves 0..7 (1 KiB, node 32 + q at leaf q / 4, slot 4 + q % 4,
+        // as words); merkle_top_kernel reads them before it writes those slots.
+        for (int e = tid; e < G * 32; e += 64) {
+            const int g = e >> 5, q = e & 31, inst = inst0 + g;
+            if (inst >= a.count) continue;
+            const uint32_t *nd = nodes + ((size_t)g * W + 32 + q) * 8;
+            uint4 *dst = reinterpret_cast<uint4 *>(a.branches + (size_t)inst * a.br_inst_pitch +
+                                                   ((size_t)(q >> 2) * a.depth + 4 + (q & 3)) * 32u);
+            dst[0] = make_uint4(nd[0], nd[1], nd[2], nd[3]);
+            dst[1] = make_uint4(nd[4], nd[5], nd[6], nd[7]);
+        }
+    }
     // roots: one thread per tree (W == 1: the root is leaf 0)
     for (int g = tid; g < G; g += 64) {
         const int inst = inst0 + g;
+        if (!CHECK && a.stop_m) break;  // merkle_top_kernel writes them
         if (inst >= a.count || (CHECK && a.only && !a.only[inst])) continue;
         uint32_t root[8];
         if (W == 1) {
@@ -522,20 +539,23 @@ __global__ __launch_bounds__(64) void merkle_kernel(MerkleArgs a) {
     }
     if (!CHECK && a.branches && a.depth > 0) {  // W == 1: no branch bytes
         // branch[j][l] = node ((W + j) >> l) ^ 1; one 16-byte half per item,
-        // item e of a tree = (jl = j*depth + l, half) at e = 2*jl + half, so a
-        // wave store covers 1 KiB of consecutive branch bytes.  jl advances by
-        // 32 per pass: (j, l) step by (32 / depth, 32 % depth) with a carry,
-        // no integer division inside the loop.
+        // item e of a tree = (jl = j*lw + l, half) at e = 2*jl + half, so a
+        // wave store covers 1 KiB of consecutive branch bytes (lw = depth) or
+        // eight leaves' first 128-B lines (lw = 4).  jl advances by 32 per
+        // pass: (j, l) step by (32 / lw, 32 % lw) with a carry, no integer
+        // division inside the loop.
         // Level 0 siblings are leaves (zero slot when past n).
-        const int depth = a.depth, items = n * depth * 2;
-        const int qd = 32 / depth, rd = 32 - qd * depth;
-        const int half = tid & 1, j_0 = (tid >> 1) / depth, l_0 = (tid >> 1) - j_0 * depth;
+        // With stop_m (W = 256) only levels 0..3 are written here (lw = 4, the
+        // first 128-B line of each leaf's branch); merkle_top_kernel writes 4..7.
+        const int depth = a.depth, lw = a.stop_m ? 4 : depth, items = n * lw * 2;
+        const int qd = 32 / lw, rd = 32 - qd * lw;
+        const int half = tid & 1, j_0 = (tid >> 1) / lw, l_0 = (tid >> 1) - j_0 * lw;
         for (int g = 0; g < G; ++g) {
             const int inst = inst0 + g;
             if (inst >= a.count) break;
-            int jl = tid >> 1, j = j_0, l = l_0;
-            for (int e = tid; e < items; e += 64, jl += 32, j += qd, l += rd) {
-                if (l >= depth) { l -= depth; ++j; }
+            int j = j_0, l = l_0;
+            for (int e = tid; e < items; e += 64, j += qd, l += rd) {
+                if (l >= lw) { l -= lw; ++j; }
                 const int node = ((W + j) >> l) ^ 1;
                 uint4 v = make_uint4(0, 0, 0, 0);
                 if (l == 0) {
@@ -546,8 +566,62 @@ __global__ __launch_bounds__(64) void merkle_kernel(MerkleArgs a) {
                     const uint32_t *nd = nodes + ((size_t)g * W + node) * 8 + 4 * half;
                     v = make_uint4(bswap32(nd[0]), bswap32(nd[1]), bswap32(nd[2]), bswap32(nd[3]));
                 }
-                *reinterpret_cast<uint4 *>(a.branches + (size_t)inst * a.br_inst_pitch + (size_t)jl * 32u + 16u * half) = v;
+                *reinterpret_cast<uint4 *>(a.branches + (size_t)inst * a.br_inst_pitch +
+                                           ((size_t)j * depth + l) * 32u + 16u * half) = v;
             }
+        }
+    }
+}
+
+// ============================================================================
+// merkle_top: the top five layers (16, 8, 4, 2, 1 nodes) of W = 256 trees
+// that merkle_kernel<false> stopped at the layer of 32 nodes, T trees per
+// one-wave block.  Beside two trees in a wave those layers fill 32, 16, .. 2
+// lanes of five passes; here T = 8 trees' layer fills 128, 64, .. 8 lanes of
+// six passes for four times the trees.  Writes the roots and the branch
+// levels 4..7 (the second 128-B line of each leaf's branch record), after
+// reading the 32-node layer merkle_kernel left in those slots.
+// ============================================================================
+__global__ __launch_bounds__(64) void merkle_top_kernel(MerkleArgs a) {
+    set_wave_prio(a.prio);
+    constexpr int T = 8, M0 = 32, W = 256;
+    __shared__ uint32_t nodes[T][2 * M0][8];  // heap index 1 .. 63 of each tree
+    const int tid = threadIdx.x, inst0 = (int)blockIdx.x * T, d = a.depth;
+    for (int e = tid; e < T * M0; e += 64) {
+        const int g = e >> 5, q = e & 31, inst = inst0 + g;
+        if (inst >= a.count) continue;
+        const uint4 *src = reinterpret_cast<const uint4 *>(a.branches + (size_t)inst * a.br_inst_pitch +
+                                                           ((size_t)(q >> 2) * d + 4 + (q & 3)) * 32u);
+        const uint4 v0 = src[0], v1 = src[1];
+        uint32_t *nd = nodes[g][M0 + q];
+        nd[0] = v0.x; nd[1] = v0.y; nd[2] = v0.z; nd[3] = v0.w;
+        nd[4] = v1.x; nd[5] = v1.y; nd[6] = v1.z; nd[7] = v1.w;
+    }
+    __syncthreads();
+    for (int m = M0 / 2, lgm = 4; m >= 1; m >>= 1, --lgm) {
+        for (int t = tid; t < T * m; t += 64) {
+            const int g = t >> lgm, i = m + (t & (m - 1));
+            if (inst0 + g >= a.count) continue;
+            uint32_t o[8];
+            sha256_node64(nodes[g][2 * i], nodes[g][2 * i + 1], o);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) nodes[g][i][q] = o[q];
+        }
+        __syncthreads();
+    }
+    for (int g = tid; g < T; g += 64)
+        if (inst0 + g < a.count) store_digest(a.roots + (size_t)(inst0 + g) * 32u, nodes[g][1]);
+    // branch[j][l] = node ((W + j) >> l) ^ 1 for l = 4..7: item e = (j, l - 4, half)
+    const int items = a.n * 4 * 2;
+    for (int g = 0; g < T; ++g) {
+        const int inst = inst0 + g;
+        if (inst >= a.count) break;
+        for (int e = tid; e < items; e += 64) {
+            const int half = e & 1, j = e >> 3, l = 4 + ((e >> 1) & 3);
+            const uint32_t *nd = nodes[g][((W + j) >> l) ^ 1] + 4 * half;
+            *reinterpret_cast<uint4 *>(a.branches + (size_t)inst * a.br_inst_pitch + ((size_t)j * d + l) * 32u +
+                                       16u * half) =
+                make_uint4(bswap32(nd[0]), bswap32(nd[1]), bswap32(nd[2]), bswap32(nd[3]));
         }
     }
 }
@@ -1851,10 +1925,18 @@ hipError_t rbc_launch_merkle(const MerkleArgs &a, bool check, hipStream_t st) {
     int g = a.width >= 512 ? 1 : (512 / a.width < 64 ? 512 / a.width : 64);
     while (g > 1 && (a.count + g - 1) / g < 512) g >>= 1;
     b.trees_per_block = g;
+    // W = 256 builds with branches: the top five layers in merkle_top_kernel
+    // (C4: build VALU 265 -> 158 + 35 M, the step 370.9-371.0 -> 376.7-378.6 GB/s, gpu_r04t.sh)
+    b.stop_m = (!check && a.width == 256 && a.depth == 8 && a.branches && a.n > 128) ? 32 : 0;
     const size_t lds = (size_t)b.trees_per_block * a.width * 32;  // 16 KiB at most
     const unsigned blocks = (unsigned)((a.count + b.trees_per_block - 1) / b.trees_per_block);
     if (check) hipLaunchKernelGGL(merkle_kernel<true>, dim3(blocks), dim3(64), lds, st, b);
     else hipLaunchKernelGGL(merkle_kernel<false>, dim3(blocks), dim3(64), lds, st, b);
+    if (b.stop_m) {
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(merkle_top_kernel, dim3((unsigned)((a.count + 7) / 8)), dim3(64), 0, st, b);
+    }
     return hipGetLastError();
 }
 
