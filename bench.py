@@ -65,6 +65,9 @@ SHA_PEAK_CPS = 1024 * 2.4e9 / (833 * 4 + 576 * 2) * 64
 # attainable: the same compression register-resident at 8 waves per SIMD
 # (profiles/r01_sha_probe.txt, 5782 clk at the nominal 2.4 GHz)
 SHA_PROBE_CPS = 1024 * 2.4e9 / 5782 * 64
+# the same probe's dependency-limited rate at 4 waves per SIMD (the row-hashing kernels' occupancy):
+# 6131 SIMD clk per wave-compression of 1418 wave64 VALU instructions
+SHA_CHAIN_CLK_PER_INSTR = 6131 / 1418
 GiB = 1 << 30
 
 
@@ -246,7 +249,7 @@ def run(args, world, rank, local_rank, wd, out):
     me["rccl_nranks"] = rccl["nranks"] if rccl else None
 
     rstream = ca.Stream(dev) if pipe else stream
-    names = ("t0", "enc", "leaf", "tree", "pf", "r0", "rf", "hashed", "dbeg", "ddone", "rend", "gather")
+    names = ("t0", "enc", "leaf", "tree", "pf", "r0", "rf", "hb", "rh", "hashed", "dbeg", "ddone", "rend", "gather")
     ev_sets = [{nm: ca.Event() for nm in names} for _ in range(max(args.steps, 20))]  # >= the joined leg's steps
     form = {"join": args.join, "start": 0}  # value form of the receive steps; the first step of a run
     vpo = lambda rb: (rb["out"], opitch) if form["join"] else (None, 0)  # noqa: E731
@@ -311,8 +314,8 @@ def run(args, world, rank, local_rank, wd, out):
         cur = ctx.rx_batch(I, sr["shards"], spitch, None, S, sr["branches"], sr["roots"], d_present, rb["valid"],
                            rb["leaves_r"], *vpo(rb), rb["digests"], rb["status"])
         prev = pending.pop(x - 1, None)
-        marks = {nm: ev[key] for nm, key in (("hashed", "hashed"), ("decode_begin", "dbeg"), ("decoded", "ddone"))} \
-            if ev is not None else {}
+        marks = {nm: ev[key] for nm, key in (("hashed", "hashed"), ("decode_begin", "dbeg"), ("decoded", "ddone"),
+                                             ("hash_begin", "hb"), ("rows_hashed", "rh"))} if ev is not None else {}
         ctx.dev_receive_step(R.ptr, cur, prev, **marks)
         pending[x] = cur
         rec(ev, "rend", R)
@@ -529,7 +532,10 @@ def spans(ev_sets, faults_on):
         pairs.update(fault=("tree", "pf"), verify=("pf", "hashed"), interp=("hashed", "rend"),
                      gather=("rend", "gather"))
     else:
+        # verify = compaction + the row-hashing launch + (C4) the shared-path verify; verify_rows and
+        # verify_path are the two launches alone (rbc_rx_marks hash_begin / rows_hashed, ABI 4)
         pairs.update(fault=("r0", "rf") if faults_on == "receiver" else ("tree", "pf"), verify=("rf", "hashed"),
+                     verify_rows=("hb", "rh"), verify_path=("rh", "hashed"),
                      check=("hashed", "dbeg"), decode=("dbeg", "ddone"), interp=("hashed", "rend"),
                      gather=("rend", "gather"))
     return {nm: sum(ev[a].elapsed_ms(ev[b]) for ev in ev_sets) / len(ev_sets) for nm, (a, b) in pairs.items()}
@@ -560,14 +566,26 @@ def report(args, ctx, I, n, k, d, S, present_h, corrupt_h, stage_ms, iso, elapse
     regen = int(I * n - R + (corrupt_h >= 0).sum())
     enc_kernel = "rs_fft_kernel<encode>" if ctx.codec == "fft" else "gf_rows_kernel<encode>"
     pipe = "decode" in stage_ms
+    path = ctx.verify_form(S) == "shared_path"  # rbc_ctx_verify_form: C4's leaves + merkle_path_kernel
     kern = {  # name: (stage, algorithmic HBM bytes per launch, SHA-256 compressions per launch)
         enc_kernel: ("enc", I * (k * S + n * S), 0),
         "sha_rows_kernel<leaves>": ("leaf", I * (n * S + n * 32), I * n * bps),
-        # the receive step's launch: ECHO verify of t (received rows only) + the regen hashing of t-1
-        ("sha_rx_kernel<verify+regen>" if pipe else "sha_rows_kernel<verify>"):
-            ("verify", R * (S + d * 32 + 32) + I * (32 + 2 * n) + (regen * (S + 32) if pipe else 0),
-             R * (bps + 2 * d) + (regen * bps if pipe else 0)),
     }
+    # the received ECHO rows (R) are read once; a walk also reads each row's d branch entries and the
+    # instance's root and writes its valid byte; the shared-path verify reads the leaves and branches
+    # of the received rows, the roots and present masks, and writes valid for every row
+    path_bytes = R * (32 * d + 32) + I * (32 + 2 * n)
+    if pipe:  # the receive step's row-hashing launch: ECHO rows of t + the regenerated rows of t-1
+        if path:
+            kern["sha_rx_kernel<leaves+regen>"] = ("verify_rows", (R + regen) * (S + 32), (R + regen) * bps)
+            kern["merkle_path_kernel<4>"] = ("verify_path", path_bytes, 0)
+        else:
+            kern["sha_rx_kernel<verify+regen>"] = ("verify_rows", R * (S + 32 * d + 32 + 1) + I * 32 + regen * (S + 32),
+                                                   R * (bps + 2 * d) + regen * bps)
+    elif path:  # serial: rbc_dev_verify = leaves of the received rows, then merkle_path_kernel
+        kern["verify: sha_rows_kernel<leaves> + merkle_path_kernel<4>"] = ("verify", R * (S + 32) + path_bytes, R * bps)
+    else:
+        kern["sha_rows_kernel<verify>"] = ("verify", R * (S + 32 * d + 32 + 1) + I * 32, R * (bps + 2 * d))
     if pipe:
         kern["decode: prepare + gf_regen_kernel + rs_fft_kernel<decode>"] = (
             "decode", decode_bytes(n, k, S, present_h, corrupt_h), 0)
@@ -595,6 +613,35 @@ def report(args, ctx, I, n, k, d, S, present_h, corrupt_h, stage_ms, iso, elapse
             clk, clk_path = c, os.path.join("profiles", cand)
             break
     clock_ghz = clk.get("clock_ghz_weighted")
+    mix_path = os.path.join("profiles", "isa_mix_r05.json")
+    try:
+        mix = json.load(open(os.path.join(ROOT, mix_path)))["kernels"]
+    except (OSError, ValueError, KeyError):
+        mix = {}
+    lg = max(d, 1)
+
+    def cpi(role):
+        """SIMD clk per wave64 VALU instruction of a kernel role: SHA-256 kernels at the probe's
+        dependency-limited rate at 4 waves per SIMD (issue_priced uses their static mix instead),
+        every other kernel at its static ISA mix priced per opcode (tools/isa_mix.py)."""
+        sym = {"rs_fft_kernel<encode>": f"rs_fft_kernel<{lg}, {k}, {n}, 0>",
+               "rs_fft_kernel<decode>": f"rs_fft_kernel<{lg}, {k}, {n}, 1>",
+               "sha_rows_kernel<leaves>": "sha_rows_kernel<false>", "sha_rows_kernel<verify>": "sha_rows_kernel<true>",
+               "sha_rx_kernel<verify+regen>": "sha_rx_kernel", "sha_rx_kernel<leaves+regen>": "sha_rx_kernel"}.get(
+                   role, role)
+        m = mix.get(sym)
+        if m is None:
+            return None, None
+        sha = sym.startswith(("sha_", "merkle", "digest"))
+        return m["clk_per_instr"], (SHA_CHAIN_CLK_PER_INSTR if sha else m["clk_per_instr"])
+
+    def priced(instr, role, ms):
+        c_issue, c_chain = cpi(role)
+        if c_issue is None or not clock_ghz:
+            return None
+        per_simd_ms = lambda c: instr * c / 1024 / (clock_ghz * 1e6)  # noqa: E731
+        return {"issue_priced_ms": round(per_simd_ms(c_issue), 4), "chain_priced_ms": round(per_simd_ms(c_chain), 4),
+                "issue_frac": round(per_simd_ms(c_issue) / ms, 4), "chain_frac": round(per_simd_ms(c_chain) / ms, 4)}
 
     def roofline(name, span=None):
         stage, nbytes, ncomp = kern[name]
@@ -616,15 +663,18 @@ def report(args, ctx, I, n, k, d, S, present_h, corrupt_h, stage_ms, iso, elapse
                          "frac_of_attainable": round(cps / SHA_PROBE_CPS, 4),
                          "model": "4 clk alignbit/add3/perm, 2 clk bitop3/add/shift per wave64 instr; 4484 SIMD "
                                   "clk per wave-compression @2.4 GHz nominal (the chip runs ~2.1 GHz under load)"}
-        if pk and pk.get("SQ_INSTS_VALU") and clock_ghz:
-            # measured, not modelled: the launch's wave64 VALU instructions (PMC) over the SIMD
-            # cycles of its live span at the loaded clock, each instruction at the VALU's 4 clocks
-            # (SQ_ACTIVE_INST_VALU only counts instructions on gfx950: tools/clock_summary.py)
-            r.setdefault("valu", {})["measured"] = {
-                "valu_instr_per_launch": pk["SQ_INSTS_VALU"], "clock_ghz": clock_ghz,
-                "busy_4clk": round(4 * pk["SQ_INSTS_VALU"] / (1024 * clock_ghz * 1e9 * ms / 1e3), 4),
-                "sources": [pmc_path, clk_path],
-                "note": "under the pipeline the span also issues the other stream's instructions"}
+        pr = priced(pk["SQ_INSTS_VALU"], name, ms) if pk and pk.get("SQ_INSTS_VALU") else None
+        if pr:
+            # the launch's wave64 VALU instructions (PMC) priced per opcode from the probe, over the
+            # SIMD time of its live span at the loaded clock (SQ_ACTIVE_INST_VALU only counts
+            # instructions on gfx950, so no counter gives busy cycles: tools/clock_summary.py)
+            r.setdefault("valu", {})["priced"] = {
+                "valu_instr_per_launch": pk["SQ_INSTS_VALU"], "clock_ghz": clock_ghz, **pr,
+                "sources": [pmc_path, clk_path, mix_path],
+                "note": "issue_priced: static ISA mix x per-opcode issue cost at 4 waves/SIMD (probe); "
+                        "chain_priced: SHA-256 kernels at the probe's 6131 SIMD clk per wave-compression "
+                        "(dependency-limited, 4 waves/SIMD). Under the pipeline the span also issues the other "
+                        "stream's instructions"}
         if iso and iso.get(stage) and not name.startswith("sha_rx"):  # sha_rx runs only under the pipeline
             ms_i = iso[stage]
             r["isolated"] = {"avg_ms": round(ms_i, 4), "achieved": round(nbytes / ms_i / 1e6, 1),
@@ -640,6 +690,14 @@ def report(args, ctx, I, n, k, d, S, present_h, corrupt_h, stage_ms, iso, elapse
     out["roofline_decode"] = roofline(
         "decode: prepare + gf_regen_kernel + rs_fft_kernel<decode>",
         "receive step's decode_begin -> decoded marks (rbc_rx_marks) on the receiver stream") if pipe else None
+    # the receive step's two hashing launches, each over its own span (hash_begin -> rows_hashed ->
+    # hashed marks): the row hashing, and at C4 the shared-path verify
+    rx = [x for x in kern if kern[x][0] == "verify_rows"]
+    out["roofline_verify"] = roofline(rx[0], "receive step's hash_begin -> rows_hashed marks (rbc_rx_marks)") \
+        if rx else None
+    out["roofline_verify_path"] = roofline(
+        "merkle_path_kernel<4>", "receive step's rows_hashed -> hashed marks (rbc_rx_marks)") \
+        if "merkle_path_kernel<4>" in kern else None
     # the whole step's VALU issue, measured: every data-path kernel's wave64 VALU instructions per
     # launch (PMC, one launch each per step) at the loaded clock, against the chip's SIMD cycles
     util = ("fill_random", "count_mismatch", "poison_rows", "inject_faults", "__amd", "[grid")
@@ -648,12 +706,23 @@ def report(args, ctx, I, n, k, d, S, present_h, corrupt_h, stage_ms, iso, elapse
               if v.get("SQ_INSTS_VALU") and not any(u in kk for u in util) and not kk.startswith("decode:")}
         if vk:
             tot = sum(vk.values())
-            step_s = elapsed_max / args.steps
-            out_valu = {"valu_instr_per_step": int(tot), "clock_ghz": clock_ghz,
-                        "busy_4clk": round(4 * tot / (1024 * clock_ghz * 1e9 * step_s), 4),
-                        "kernels": len(vk), "sources": [pmc_path, clk_path],
-                        "note": "wave64 VALU instructions of the step's kernels (PMC, per launch) x 4 clocks / "
-                                "(1024 SIMDs x loaded clock x ms_per_step); above 1.0 some issue in 2 clocks"}
+            step_ms = elapsed_max / args.steps * 1e3
+            parts = {kk: priced(v, kk, step_ms) for kk, v in vk.items()}
+            unpriced = sorted(kk for kk, v in parts.items() if v is None)
+            out_valu = {"valu_instr_per_step": int(tot), "clock_ghz": clock_ghz, "kernels": len(vk),
+                        "issue_priced_ms": round(sum(v["issue_priced_ms"] for v in parts.values() if v), 4),
+                        "chain_priced_ms": round(sum(v["chain_priced_ms"] for v in parts.values() if v), 4),
+                        "unpriced_kernels": unpriced, "sources": [pmc_path, clk_path, mix_path],
+                        "per_kernel": {kk: v for kk, v in parts.items() if v},
+                        "note": "every data-path kernel's wave64 VALU instructions per launch (PMC, one launch "
+                                "each per step) priced in SIMD time at the loaded clock over 1024 SIMDs. "
+                                "issue_priced: each kernel's static ISA mix at the probe's per-opcode issue cost "
+                                "(v_perm / v_alignbit / v_add3 ~4.3-4.8 clk, v_bitop3 / v_xor / v_add / shifts "
+                                "~2.4-2.8 clk at 4 waves per SIMD) -- the step if every SIMD issued back to back; "
+                                "chain_priced: the SHA-256 kernels at the probe's measured dependency-limited "
+                                "throughput instead (6131 clk per wave-compression at 4 waves per SIMD)"}
+            out_valu["issue_frac_of_step"] = round(out_valu["issue_priced_ms"] / step_ms, 4)
+            out_valu["chain_frac_of_step"] = round(out_valu["chain_priced_ms"] / step_ms, 4)
         else:
             out_valu = None
     else:

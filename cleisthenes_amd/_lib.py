@@ -13,8 +13,10 @@ from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_size_t, c_uint8
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # RBC_GPU_LIB: another build of the same ABI (an A/B candidate from tools/build_ab.sh, or a
 # test-only mutant from tests/mutants that the guard tests expect to FAIL); the bench line
-# records the file actually mapped (rbc_library_path, dladdr) so a run says what it measured
-LIB_PATH = os.environ.get("RBC_GPU_LIB") or os.path.join(_HERE, "librbc_gpu.so")
+# records the file actually mapped (rbc_library_path, dladdr) so a run says what it measured.
+# RBC_GPU_LIB_AB is round 3's name for the same override (archived run scripts still set it).
+LIB_PATH = (os.environ.get("RBC_GPU_LIB") or os.environ.get("RBC_GPU_LIB_AB")
+            or os.path.join(_HERE, "librbc_gpu.so"))
 INCLUDE_DIR = os.path.join(os.path.dirname(_HERE), "include")
 HEADER_PATH = os.path.join(INCLUDE_DIR, "rbc_gpu.h")
 
@@ -42,12 +44,14 @@ class RxBatch(ctypes.Structure):
 
 class RxMarks(ctypes.Structure):
     """rbc_rx_marks (include/rbc_gpu.h): timing events of rbc_dev_receive_step."""
-    _fields_ = [("hashed", c_void_p), ("decode_begin", c_void_p), ("decoded", c_void_p)]
+    _fields_ = [("hashed", c_void_p), ("decode_begin", c_void_p), ("decoded", c_void_p), ("hash_begin", c_void_p),
+                ("rows_hashed", c_void_p)]
 
 
 _SIGS = {
     "rbc_strerror": (c_char_p, [c_int]),
     "rbc_abi_version": (c_int, []),
+    "rbc_ctx_verify_form": (c_int, [c_void_p, c_uint32, POINTER(c_int)]),
     "rbc_library_path": (c_int, [c_char_p, c_size_t]),
     "rbc_device_count": (c_int, [POINTER(c_int)]),
     "rbc_ctx_create": (c_int, [c_int, c_int, c_int, POINTER(c_void_p)]),

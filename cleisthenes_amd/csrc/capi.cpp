@@ -338,6 +338,15 @@ int stage_merkle_build(rbc_ctx *c, hipStream_t st, int count, const uint8_t *lea
     return RBC_OK;
 }
 
+// ECHO verify's form: leaf hashes + the shared-path verify
+// (merkle_path_kernel) where the per-leaf walk's 2d compressions per row are a
+// real share of the leaf's ceil((S+9)/64) -- C4: 16 vs 13 -- and the per-leaf
+// walk fused into the row hashing where they are not (C2: 14 vs 373).
+static bool shared_path_verify(const rbc_ctx *c, const uint32_t *shard_lens, uint32_t uniform_shard_len) {
+    const uint32_t blocks_per_row = shard_lens ? 0u : (uniform_shard_len + 9 + 63) / 64;
+    return (shard_lens || 16u * (uint32_t)c->depth >= blocks_per_row) && c->depth >= 1 && c->width <= 256;
+}
+
 int stage_verify(rbc_ctx *c, hipStream_t st, int count, const uint8_t *shards, uint32_t shard_pitch,
                  const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *branches,
                  const uint8_t *roots, const uint8_t *present, uint8_t *valid, uint8_t *leaves) {
@@ -370,8 +379,7 @@ int stage_verify(rbc_ctx *c, hipStream_t st, int count, const uint8_t *shards, u
     // ceil((S+9)/64); the shared-path form pays off where that walk is a real
     // share (C4: 16 vs 13) and only adds a launch where it is not (C2: 14 vs
     // 373, measured equal alone and slower beside a second stream).
-    const uint32_t blocks_per_row = shard_lens ? 0u : (uniform_shard_len + 9 + 63) / 64;
-    const bool path_pays = shard_lens || 16u * (uint32_t)c->depth >= blocks_per_row;
+    const bool path_pays = shared_path_verify(c, shard_lens, uniform_shard_len);
     // Only the received ECHOs are validated (validateMessage runs per message):
     // with a present mask the shards to hash are compacted into a device list
     // first (N-f of N in the bench: a third fewer SHA rows than hashing all N).
@@ -388,7 +396,7 @@ int stage_verify(rbc_ctx *c, hipStream_t st, int count, const uint8_t *shards, u
         a.list = vl;
         a.list_count = vc;
     }
-    if (path_pays && c->depth >= 1 && c->width <= 256) {
+    if (path_pays) {
         uint8_t *lv = leaves;
         if (!lv) {
             std::lock_guard<std::mutex> lk(c->mu);
@@ -499,9 +507,7 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
         g.status = status;
         g.rcount = pa.rcount;
         g.prio = c->gemv_prio();
-#ifndef RBC_MUTANT_SKIP_REGEN  // tests/mutants only: a build that never regenerates, which the guards must catch
         RBC_HIP(rbc_launch_gf_regen(g, st));
-#endif
         // 2) parity positions: additive-FFT re-encode of the completed data half
         FftArgs a{};
         a.count = count;
@@ -749,8 +755,7 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
             v.list_count = vc;
         }
         // the shared-path verify where the branch walk is a real share (C4), as stage_verify
-        const uint32_t blocks_per_row = cur->shard_lens ? 0u : (cur->uniform_shard_len + 9 + 63) / 64;
-        v_path = (cur->shard_lens || 16u * (uint32_t)c->depth >= blocks_per_row) && c->depth >= 1 && c->width <= 256;
+        v_path = shared_path_verify(c, cur->shard_lens, cur->uniform_shard_len);
         v_walk = !v_path;
     }
     if (hp && nr > 0) {
@@ -775,7 +780,9 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
         RBC_HIP(w.vroot[cur_vslot].ensure((size_t)cur->count * 32));
         RBC_HIP(hipMemcpyAsync(w.vroot[cur_vslot].p, cur->roots, (size_t)cur->count * 32, hipMemcpyDeviceToDevice, st));
     }
+    if (marks && marks->hash_begin) RBC_HIP(hipEventRecord((hipEvent_t)marks->hash_begin, st));
     RBC_HIP(rbc_launch_sha_rx(v, r, v_walk, st));
+    if (marks && marks->rows_hashed) RBC_HIP(hipEventRecord((hipEvent_t)marks->rows_hashed, st));
     if (hc && v_path) {
         PathArgs p{};
         p.count = cur->count;
@@ -962,6 +969,12 @@ const char *rbc_strerror(int s) {
 }
 
 int rbc_abi_version(void) { return RBC_ABI_VERSION; }
+
+int rbc_ctx_verify_form(const rbc_ctx *c, uint32_t shard_len, int *form) {
+    if (!c || !form) return RBC_ERR_INVALID_ARG;
+    *form = shared_path_verify(c, nullptr, shard_len) ? RBC_VERIFY_SHARED_PATH : RBC_VERIFY_WALK;
+    return RBC_OK;
+}
 
 int rbc_ctx_set_recheck(rbc_ctx *c, int mode) {
     if (!c || (mode != RBC_RECHECK_REUSE && mode != RBC_RECHECK_FULL)) return RBC_ERR_INVALID_ARG;

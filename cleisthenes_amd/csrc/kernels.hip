@@ -735,15 +735,18 @@ __global__ __launch_bounds__(64) void merkle_recheck_kernel(RecheckArgs a) {
         __syncthreads();
     }
     // 4. compare the root v of every maximal valid-free subtree (level l < d)
-    //    holding a real leaf with the level-l branch entry of the first valid
-    //    leaf under its sibling (an all-padding subtree is the same constant
-    //    in both trees)
+    //    with the level-l branch entry of the first valid leaf under its
+    //    sibling.  Only an empty LEAF (l == 0, j >= n) is skipped: the walk
+    //    itself makes that sibling empty.  A padding node at l >= 1 is taken
+    //    from the proposer's branch by the walk, so a Byzantine commitment can
+    //    put any value there; it is compared like every other node (E holds
+    //    the standard padding hash, step 3), as the full recheck would.
     for (int l = 0; l < lgW; ++l) {
         const int m = W >> l;
         for (int t = lane; t < G * m; t += 64) {
             const int g = t >> (lgW - l), i = m + (t & (m - 1));
             const uint8_t *h = hv + g * 2 * W;
-            if (!active(g) || h[i] || !h[i >> 1] || ((i - m) << l) >= n) continue;
+            if (!active(g) || h[i] || !h[i >> 1] || (l == 0 && (i - m) >= n)) continue;
             int s = i ^ 1;
             while (s < W) s = h[2 * s] ? 2 * s : 2 * s + 1;  // first valid leaf under the sibling
             const int inst = inst0 + g, j = s - W;

@@ -274,6 +274,13 @@ class Context:
         with no valid ECHO leaf are hashed) or "full" (the whole tree)."""
         check(lib.rbc_ctx_set_recheck(self._p, {"reuse": 0, "full": 1}[mode]), "rbc_ctx_set_recheck")
 
+    def verify_form(self, shard_len: int) -> str:
+        """"walk" or "shared_path": the ECHO-verify form for rows of shard_len
+        bytes (rbc_ctx_verify_form)."""
+        f = c_int(0)
+        check(lib.rbc_ctx_verify_form(self._p, shard_len, ctypes.byref(f)), "rbc_ctx_verify_form")
+        return ("walk", "shared_path")[f.value]
+
     def set_codec(self, codec: str) -> None:
         check(lib.rbc_ctx_set_codec(self._p, {"auto": 0, "matrix": 1, "fft": 2}[codec]), "rbc_ctx_set_codec")
 
@@ -482,15 +489,19 @@ class Context:
         return _lib.RxBatch(count, v(shards), shard_pitch, v(shard_lens), uniform_len, v(branches), v(roots),
                             v(present), v(valid), v(leaves), v(values_out), value_pitch, v(digests), v(status))
 
-    def dev_receive_step(self, stream, cur=None, prev=None, hashed=None, decode_begin=None, decoded=None) -> None:
+    def dev_receive_step(self, stream, cur=None, prev=None, hashed=None, decode_begin=None, decoded=None,
+                         hash_begin=None, rows_hashed=None) -> None:
         """Pipelined receiver: verify(cur) + rehash(prev) in one SHA launch,
         prev's recheck + digest, cur's decode (rbc_dev_receive_step).  hashed /
         decode_begin / decoded (Events, optional) are recorded after the
-        hashing launch, before cur's decode and after it (rbc_rx_marks)."""
+        hashing launch (and the shared-path verify), before cur's decode and
+        after it; hash_begin / rows_hashed right before and after the
+        row-hashing launch alone (rbc_rx_marks)."""
         marks = None
-        if hashed is not None or decode_begin is not None or decoded is not None:
+        evs = (hashed, decode_begin, decoded, hash_begin, rows_hashed)
+        if any(e is not None for e in evs):
             ev = lambda e: e.ptr.value if e is not None else None  # noqa: E731
-            marks = ctypes.byref(_lib.RxMarks(ev(hashed), ev(decode_begin), ev(decoded)))
+            marks = ctypes.byref(_lib.RxMarks(*(ev(e) for e in evs)))
         check(lib.rbc_dev_receive_step(self._p, _dv(stream), ctypes.byref(cur) if cur is not None else None,
                                        ctypes.byref(prev) if prev is not None else None, marks),
               "rbc_dev_receive_step")

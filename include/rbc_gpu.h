@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define RBC_ABI_VERSION 3
+#define RBC_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------- */
 #define RBC_OK 0
@@ -109,6 +109,15 @@ int rbc_ctx_set_decode_priority(rbc_ctx *ctx, int gemv_prio, int reencode_prio);
 #define RBC_RECHECK_REUSE 0
 #define RBC_RECHECK_FULL 1
 int rbc_ctx_set_recheck(rbc_ctx *ctx, int mode);
+/* Which ECHO-verify form rbc_dev_verify / rbc_dev_receive_step run for rows
+ * of shard_len bytes (validateMessage, rbc/rbc.go:92-95): RBC_VERIFY_WALK,
+ * the per-leaf branch walk fused into the row hashing, or
+ * RBC_VERIFY_SHARED_PATH, leaf hashing then merkle_path_kernel (where the
+ * walk's 2d compressions per row are a real share of the row's own; C4).
+ * Both give the same valid[] bit for bit. */
+#define RBC_VERIFY_WALK 0
+#define RBC_VERIFY_SHARED_PATH 1
+int rbc_ctx_verify_form(const rbc_ctx *ctx, uint32_t shard_len, int *form);
 
 /* ---- device memory / streams / events (so a host runtime needs no other
  *      GPU library to drive the rbc_dev_* path) ---------------------------- */
@@ -230,11 +239,17 @@ typedef struct rbc_rx_batch {
 /* Timing marks (each nullable, rbc_event_create events) recorded on `stream`:
  * hashed after the hashing launch (and cur's shared-path walk), decode_begin
  * after prev's recheck, decoded after cur's decode (prepare, missing-data GF,
- * FFT re-encode + compare), so a caller can time each part live. */
+ * FFT re-encode + compare), so a caller can time each part live.  ABI 4:
+ * hash_begin right before the row-hashing launch (after cur's compaction) and
+ * rows_hashed right after it, before the shared-path verify
+ * (merkle_path_kernel, W = 256 at short rows) -- so each of the two kernels
+ * has its own span; with the per-leaf walk rows_hashed and hashed coincide. */
 typedef struct rbc_rx_marks {
     void *hashed;
     void *decode_begin;
     void *decoded;
+    void *hash_begin;
+    void *rows_hashed;
 } rbc_rx_marks;
 int rbc_dev_receive_step(rbc_ctx *ctx, void *stream, const rbc_rx_batch *cur, const rbc_rx_batch *prev,
                          const rbc_rx_marks *marks);

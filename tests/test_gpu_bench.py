@@ -48,6 +48,8 @@ def test_bench_schedules_pass_their_guard(pipeline, join):
     if pipeline:
         rd = d["roofline_decode"]
         assert rd["avg_ms"] > 0 and 0 < rd["frac"] < 1 and rd["algorithmic_bytes_per_launch"] > 0
+        # C2 walks the branches inside the row hashing: one launch, no shared-path span
+        assert d["roofline_verify"]["kernel"] == "sha_rx_kernel<verify+regen>" and d["roofline_verify_path"] is None
 
 
 def test_bench_c3_8192_instances_on_one_gpu():
@@ -80,6 +82,11 @@ def test_bench_c4_16384_instances():
     d = _run(["--config", "c4", "--steps", "3", "--warmup", "3", "--no-isolated"] + QUICK)
     assert d["config"]["instances_per_gpu"] == 16384
     assert d["decoded_ok"] == 16384 and d["values_ok"] and d["value_mismatch_chunks"] == 0 and d["oracle_sample_ok"]
+    # C4 verifies with the shared path: the row hashing and merkle_path_kernel each have their own span
+    rv, rp = d["roofline_verify"], d["roofline_verify_path"]
+    assert rv["kernel"] == "sha_rx_kernel<leaves+regen>" and rp["kernel"] == "merkle_path_kernel<4>"
+    sm = d["stage_ms"]
+    assert sm["verify_rows"] > 0 and sm["verify_path"] > 0 and sm["verify_rows"] + sm["verify_path"] <= sm["verify"]
 
 
 def test_bench_multi_rank_rehearsal_ragged_strong_scaling():
@@ -93,6 +100,26 @@ def test_bench_multi_rank_rehearsal_ragged_strong_scaling():
     assert d["config"]["instances_total"] == 250 and "rehearsal" in d["config"]
     assert d["decoded_ok"] == 250 and d["values_ok"] and d["gather_ok"] and d["oracle_sample_ok"]
     assert [r["rank"] for r in d["ranks"]] == [0, 1, 2]
+
+
+def test_bench_eight_rank_rehearsal():
+    """The driver's first 8-GPU run, rehearsed on this one GPU (VERDICT r04
+    item 5): bench.py spawns 8 ranks itself, all on device 0 with no RCCL, and
+    partitions 1,000 instances 125 apiece.  Exercised: the self-spawn, the
+    world-size-8 rendezvous, the per-stage watchdog, the HBM plan with 8 ranks
+    sharing the device, the ragged-capable partition, the guard over every
+    rank (decodes, values, gathered records through the rendezvous, oracle
+    samples) and the 8-entry ranks / rank_skew keys.  Not a multi-GPU
+    measurement: RCCL at nranks > 1 needs the driver's 8-GPU node."""
+    d = _run(["--gpus", "8", "--rehearse-on-one-gpu", "--total-instances", "1000", "--steps", "3", "--warmup", "3",
+              "--no-isolated", "--no-joined-leg"] + QUICK, timeout=600)
+    assert d["n_gpus"] == 8 and d["scaling"] == "strong" and "rehearsal" in d["config"]
+    assert d["config"]["instances_total"] == 1000 and d["config"]["instances_per_gpu"] == 125
+    assert d["decoded_ok"] == 1000 and d["values_ok"] and d["gather_ok"] and d["oracle_sample_ok"]
+    assert [r["rank"] for r in d["ranks"]] == list(range(8)) and all(r["ms_per_step"] > 0 for r in d["ranks"])
+    assert d["config"]["hbm_plan"]["ranks_sharing_device"] == 8
+    sk = d["rank_skew"]
+    assert sk["slowest_rank"] in range(8) and sk["fastest_rank"] in range(8) and sk["max_over_min"] >= 1.0
 
 
 def test_bench_one_rank_rccl_gather():

@@ -1794,3 +1794,107 @@ def test_receive_step_node_reuse_recheck_equals_full_recheck(gpu, ref, n, f, B, 
         assert (st[honest] == 0).all(), (bi, st[honest])
         for t, i in enumerate(np.flatnonzero(st == 0)):
             assert bytes(c_["out"][t][:B]) == bytes(c_["values"][i, :B])
+
+
+def _padding_nodes_with_real_sibling(n):
+    """(heap index, level, first and end leaf under its sibling) of every
+    all-padding node at levels 1 .. d-1 whose sibling holds a real leaf."""
+    W, d = orc.tree_width(n), orc.tree_depth(n)
+    out = []
+    for lvl in range(1, d):
+        m = W >> lvl
+        for i in range(m, 2 * m):
+            lo = ((i ^ 1) << lvl) - W
+            if ((i - m) << lvl) >= n and lo < n:
+                out.append((i, lvl, lo, min(n, lo + (1 << lvl))))
+    return out
+
+
+@pytest.mark.parametrize("n,f,B,I", [(33, 10, 13 * 40 + 1, 48), (100, 33, 34 * 60 + 7, 48)], ids=["n33", "n100"])
+def test_receive_step_rejects_a_byzantine_padding_node(gpu, n, f, B, I):
+    """a Byzantine proposer commits to a tree whose padding
+    node at level >= 1 is a value of its choosing.  Every ECHO verifies (the
+    walk takes that node from the branch), the full recheck rebuilds standard
+    padding and rejects the root.  The node-reuse recheck must reject it too,
+    both when a valid leaf sits under the padding node's parent and when none
+    does; honest instances of the same batches still deliver.  One-shot, FULL
+    and REUSE give identical statuses."""
+    k = n - 2 * f
+    W, d = orc.tree_width(n), orc.tree_depth(n)
+    pads = _padding_nodes_with_real_sibling(n)
+    assert pads
+
+    def make():
+        rng = np.random.default_rng(4242 + n)
+        pl = Pipeline(gpu, n, f, B, I, seed=31 * n, corrupt_frac=0.0)
+        pl.commit()
+        gpu.rbc.lib.rbc_device_sync(0)
+        leaves = pl.arr("leaves", shape=(I, n, 32))
+        roots = pl.arr("roots", shape=(I, 32)).copy()
+        brs = pl.arr("branches", shape=(I, n, d, 32)).copy()
+        byz = np.zeros(I, bool)
+        for i in range(I):
+            if i % 3 == 2:
+                continue  # honest
+            ip, lvl, lo, hi = pads[(i // 3) % len(pads)]
+            mt = [b""] * (2 * W)
+            for j in range(n):
+                mt[W + j] = bytes(leaves[i, j])
+            x = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+            for h in range(W - 1, 0, -1):
+                mt[h] = x if h == ip else orc.sha256(mt[2 * h] + mt[2 * h + 1])
+            roots[i] = np.frombuffer(mt[1], np.uint8)
+            for j in range(n):
+                for l_, sib in enumerate(orc.merkle_branch(mt, j)):
+                    brs[i, j, l_] = np.frombuffer(sib, np.uint8) if sib else 0
+            pres = np.zeros(n, np.uint8)
+            pres[rng.permutation(n)[: n - f]] = 1
+            pres[lo:hi] = 0
+            if i % 3 == 0:
+                pres[lo] = 1  # a valid leaf under the padding node's parent
+            assert pres.sum() >= k
+            pl.present[i] = pres
+            byz[i] = True
+        pl.b["roots"].upload(roots)
+        pl.b["branches"].upload(brs)
+        pl.b["present"].upload(pl.present)
+        pl.poison()
+        return pl, byz
+
+    st = {}
+    for mode in ("oneshot", "full", "reuse"):
+        pl, byz = make()
+        b, c = pl.b, pl.ctx
+        if mode == "oneshot":
+            c.dev_verify(None, I, b["shards"], pl.spitch, None, pl.S, b["branches"], b["roots"], b["present"],
+                         b["valid"], b["leaves_r"])
+            c.dev_interpolate(None, I, b["shards"], pl.spitch, None, pl.S, b["valid"], b["leaves_r"], 1,
+                              b["roots"], b["out"], pl.opitch, b["digests"], b["status"])
+        else:
+            c.set_recheck(mode)
+            cur = c.rx_batch(I, b["shards"], pl.spitch, None, pl.S, b["branches"], b["roots"], b["present"],
+                             b["valid"], b["leaves_r"], b["out"], pl.opitch, b["digests"], b["status"])
+            c.dev_receive_step(None, cur, None)
+            c.dev_receive_step(None, None, cur)
+        gpu.rbc.lib.rbc_device_sync(0)
+        valid = pl.arr("valid", shape=(I, n))
+        assert np.array_equal(valid.astype(bool), pl.present.astype(bool)), mode  # every ECHO verifies
+        st[mode] = pl.arr("status", np.int32).copy()
+        assert (st[mode][byz] == -8).all(), (mode, np.flatnonzero(st[mode][byz] != -8))
+        assert (st[mode][~byz] == 0).all(), mode
+    assert np.array_equal(st["oneshot"], st["reuse"]) and np.array_equal(st["full"], st["reuse"])
+
+
+def test_verify_form_matches_the_profiling_tools_rule(gpu):
+    """rbc_ctx_verify_form (the library's choice of ECHO-verify form) is the
+    rule tools/trace_summary.py names kernel roles by, at every bench config:
+    the per-leaf walk at C1-C3, leaves + merkle_path_kernel at C4."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import trace_summary as ts
+    for cfg, (n, f) in ts.CONFIGS.items():
+        k = n - 2 * f
+        S = (ts.VALUE_BYTES[cfg] + k - 1) // k
+        form = gpu.Context(n, f).verify_form(S)
+        assert (form == "shared_path") == ts.shared_path(cfg), (cfg, form)
+        assert form == ("shared_path" if cfg == "c4" else "walk")

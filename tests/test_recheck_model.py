@@ -84,8 +84,8 @@ def reuse_recheck(n, full, rx, valid, branches, verified_root, expect_root, flag
     for lvl in range(d):
         m = W >> lvl
         for i in range(m, 2 * m):
-            if hv[i] or not hv[i >> 1] or ((i - m) << lvl) >= n:
-                continue
+            if hv[i] or not hv[i >> 1] or (lvl == 0 and i - m >= n):
+                continue  # only an empty leaf is forced by the walk; padding nodes above are compared
             s = i ^ 1
             while s < W:  # the first valid leaf under the sibling
                 s = 2 * s if hv[2 * s] else 2 * s + 1
@@ -114,6 +114,68 @@ def test_node_reuse_recheck_equals_full_recheck(n, f):
             assert hashed <= orc.tree_width(n) - 1
     # every branch of the rule was exercised
     assert seen["ok"] and seen["mismatch"] and seen["fallback"], seen
+
+
+def byzantine_padding_commit(leaf_hashes, n, overrides):
+    """A proposer's tree whose padding node(s) at level >= 1 hold chosen
+    values (heap index -> 32 bytes) instead of the standard empty-subtree
+    hash; every ECHO walk still verifies, because the walk takes those nodes
+    from the branches.  Returns (root, branches)."""
+    W = orc.tree_width(n)
+    mt = [b""] * (2 * W)
+    for j in range(n):
+        mt[W + j] = bytes(leaf_hashes[j])
+    for i in range(W - 1, 0, -1):
+        mt[i] = overrides.get(i, orc.sha256(mt[2 * i] + mt[2 * i + 1]))
+    return mt[1], [orc.merkle_branch(mt, j) for j in range(n)]
+
+
+def padding_nodes(n):
+    """Heap indices of the all-padding nodes at levels 1 .. d-1."""
+    W, d = orc.tree_width(n), orc.tree_depth(n)
+    out = []
+    for lvl in range(1, d):
+        m = W >> lvl
+        out += [(i, lvl) for i in range(m, 2 * m) if ((i - m) << lvl) >= n]
+    return out
+
+
+@pytest.mark.parametrize("n,f", [(33, 10), (100, 33), (13, 4), (200, 66)])
+def test_node_reuse_rejects_a_byzantine_padding_node(n, f):
+    """a proposer that commits to a non-standard padding
+    node at level >= 1 passes every ECHO verify; the full recheck rebuilds the
+    tree with standard padding and rejects it.  The reuse rule must reject it
+    too whether or not a valid leaf sits under the padding node's parent --
+    otherwise two honest receivers disagree on delivery."""
+    rng = np.random.default_rng(77 + n)
+    k = n - 2 * f
+    W = orc.tree_width(n)
+    enc = orc.Encoder(k, n - k)
+    cases = 0
+    for i_pad, lvl in padding_nodes(n):
+        shards = orc.rbc_shard(enc, rng.integers(0, 256, 3 * k + 5, dtype=np.uint8))
+        leaves = [orc.sha256(s) for s in shards]
+        root, branches = byzantine_padding_commit(leaves, n, {i_pad: bytes(rng.integers(0, 256, 32, dtype=np.uint8))})
+        assert all(orc.merkle_verify(n, shards[j], root, branches[j], j) for j in range(n))
+        sib = i_pad ^ 1  # the real leaves under the padding node's sibling
+        lo, hi = (sib << lvl) - W, min(n, ((sib + 1) << lvl) - W)
+        if lo >= n:
+            continue  # the parent is padding too: the case of a higher node
+        for under_parent in (True, False):
+            valid = np.zeros(n, bool)
+            valid[rng.permutation(n)[: n - f]] = True
+            valid[lo:hi] = False
+            if under_parent:
+                valid[lo] = True
+            if valid.sum() < k:
+                continue
+            full, flagged = _decode(enc, shards, valid)
+            want = orc.merkle_tree(full)[1] == root
+            assert not want  # the full recheck rebuilds standard padding
+            got, _ = reuse_recheck(n, full, shards, valid, branches, root, root, flagged)
+            assert got == want, (n, i_pad, lvl, under_parent)
+            cases += 1
+    assert cases >= 2
 
 
 def test_node_reuse_hashes_few_nodes_at_the_bench_shapes():

@@ -11,11 +11,12 @@ execution (--pmc serialises dispatches anyway).
 
 Per role (MI355X_MICROARCH.md, "DVFS give-back"): clock = GRBM_GUI_ACTIVE / 8
 XCDs / duration.  SQ_ACTIVE_INST_VALU counts wave64 VALU instructions on
-gfx950 (it equals SQ_INSTS_VALU to 0.1 %, profiles/r04b_*), not busy cycles,
-so the issue busy fraction is priced at the VALU's 4 clocks per wave64
-instruction per SIMD: valu_busy_4clk = 4 * VALU / (1024 SIMDs * cycles).
-Above 1.0 means some instructions issued in 2 clocks (v_bitop3, v_add,
-shifts; profiles/r01_valu_probe.txt).
+gfx950 (it equals SQ_INSTS_VALU to 0.1 %, profiles/r04b_*), not busy cycles:
+no counter measures the VALU's busy fraction.  valu_at_4clk = 4 * VALU /
+(1024 SIMDs * cycles) is only a flat-4-clock reference (v_bitop3, v_add and
+shifts issue in ~2.5 clocks, v_perm / v_alignbit / v_add3 in ~4.4:
+profiles/r01_valu_probe.txt); bench.py prices the counts per opcode instead
+(tools/isa_mix.py, valu_step.issue_priced_ms / chain_priced_ms).
 """
 import argparse
 import csv
@@ -73,7 +74,7 @@ def main():
         vi = cs.get("SQ_INSTS_VALU")
         if vi:
             r["valu_instr"] = int(vi)
-            r["valu_busy_4clk"] = round(4 * vi / (SIMDS * cyc), 3)
+            r["valu_at_4clk"] = round(4 * vi / (SIMDS * cyc), 3)
         if "SQ_ACTIVE_INST_VALU" in cs and vi:
             r["active_inst_valu_over_insts_valu"] = round(cs["SQ_ACTIVE_INST_VALU"] / vi, 4)
         rows[rl] = r

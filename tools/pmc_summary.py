@@ -18,14 +18,14 @@ import sys
 from collections import defaultdict
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from trace_summary import CONFIGS, role, summarize  # noqa: E402
+from trace_summary import CONFIGS, role, shared_path, summarize  # noqa: E402
 
 
 def blocks(S):
     return (S + 9 + 63) // 64
 
 
-def load_pmc(d, n, k, inst, last):
+def load_pmc(d, n, k, inst, last, path=False):
     per = defaultdict(lambda: defaultdict(list))  # role -> counter -> [per-dispatch value]
     for sub in sorted(os.listdir(d)):
         f = os.path.join(d, sub, "run_counter_collection.csv")
@@ -34,7 +34,7 @@ def load_pmc(d, n, k, inst, last):
         acc = defaultdict(float)  # (role, grid, dispatch, counter) -> summed value (over XCDs / instances)
         for r in csv.DictReader(open(f)):
             g = int(r["Grid_Size"])
-            rl = role(r["Kernel_Name"], g, n, k, inst)
+            rl = role(r["Kernel_Name"], g, n, k, inst, path)
             acc[(rl, g, int(r["Dispatch_Id"]), r["Counter_Name"])] += float(r["Counter_Value"])
         biggest = defaultdict(int)
         for (rl, g, _, _) in acc:
@@ -66,7 +66,8 @@ def main():
     d = 0
     while (1 << d) < n:
         d += 1
-    pm = load_pmc(a.dir, n, k, a.instances, a.last)
+    path = shared_path(a.config, vb)
+    pm = load_pmc(a.dir, n, k, a.instances, a.last, path)
     tf = os.path.join(a.dir, "trace", "run_kernel_trace.csv")
     tr = summarize(tf, a.config, a.instances, a.last) if os.path.exists(tf) else {}
     # SHA-256 compressions per launch: leaves hash all N rows, ECHO verify the
@@ -76,6 +77,9 @@ def main():
             # receive step: the received rows of t + the regenerated rows of t-1
             # (the f absent rows, plus the bench's one corrupted ECHO in 10 % of instances)
             "sha_rx_kernel<verify+regen>": a.instances * (n - f) * (blocks(S) + 2 * d)
+            + (a.instances * f + a.instances // 10) * blocks(S),
+            # C4: the receive step hashes leaves only; merkle_path_kernel walks the branches
+            "sha_rx_kernel<leaves+regen>": a.instances * (n - f) * blocks(S)
             + (a.instances * f + a.instances // 10) * blocks(S)}
     rows = {}
     for rl in sorted(set(pm) | set(tr)):

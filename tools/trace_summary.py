@@ -23,13 +23,25 @@ import json
 from collections import defaultdict
 
 CONFIGS = {"c1": (64, 21), "c2": (128, 42), "c3": (128, 42), "c4": (256, 85)}
+VALUE_BYTES = {"c1": 1 << 20, "c2": 1 << 20, "c3": 4 << 20, "c4": 64 << 10}
+
+
+def shared_path(config, value_bytes=0):
+    """The receive step's ECHO-verify form at a config: the C library's rule
+    (csrc/capi.cpp shared_path_verify, rbc_ctx_verify_form): leaves + the
+    shared-path verify where 16 d >= ceil((S + 9) / 64) and W <= 256."""
+    n, f = CONFIGS[config]
+    k = n - 2 * f
+    S = ((value_bytes or VALUE_BYTES[config]) + k - 1) // k
+    d = max(1, (n - 1).bit_length())
+    return 16 * d >= (S + 9 + 63) // 64 and (1 << d) <= 256
 
 
 def base(name):
     return name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").strip()
 
 
-def role(name, grid, n, k, inst):
+def role(name, grid, n, k, inst, path=False):
     b = base(name)
     if b.startswith("rs_fft_kernel<"):
         return "rs_fft_kernel<encode>" if b.rstrip(">").endswith(", 0") else "rs_fft_kernel<decode>"
@@ -39,8 +51,8 @@ def role(name, grid, n, k, inst):
         if grid == inst * (n - k):
             return "sha_rows_kernel<regen>"
         return f"sha_rows_kernel<false>[grid {grid}]"
-    if b == "sha_rx_kernel":  # rbc_dev_receive_step: ECHO verify of t + regen hashing of t-1
-        return "sha_rx_kernel<verify+regen>"
+    if b == "sha_rx_kernel":  # rbc_dev_receive_step: ECHO verify of t (C4: leaves only) + regen hashing of t-1
+        return "sha_rx_kernel<leaves+regen>" if path else "sha_rx_kernel<verify+regen>"
     if b == "sha_rows_kernel<true>":
         return "sha_rows_kernel<verify>"
     return b
@@ -49,6 +61,7 @@ def role(name, grid, n, k, inst):
 def summarize(path, config, inst, last, before=None):
     n, f = CONFIGS[config]
     k = n - 2 * f
+    path = shared_path(config)
     durs = []
     rows = list(csv.DictReader(open(path)))
     if before:
@@ -58,7 +71,7 @@ def summarize(path, config, inst, last, before=None):
     for r in rows:
         grid = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6  # ms
-        durs.append((int(r["Dispatch_Id"]), role(r["Kernel_Name"], grid, n, k, inst), grid, d))
+        durs.append((int(r["Dispatch_Id"]), role(r["Kernel_Name"], grid, n, k, inst, path), grid, d))
     # one role may run on several batch sizes (the PCIe host-path measurement
     # uses small batches): the largest grid is the bench batch, others are
     # reported apart as role[grid G]
