@@ -112,6 +112,8 @@ def parse_args(argv):
                     help="configs the CPU port is also timed on (the bench config always is)")
     ap.add_argument("--no-pcie", action="store_true",
                     help="skip the PCIe-inclusive host-path measurement (a secondary key, never `value`)")
+    ap.add_argument("--no-batcher", action="store_true",
+                    help="skip the per-message validate lane sweep (secondary key `batcher`, C2 only, never `value`)")
     ap.add_argument("--rehearse-on-one-gpu", action="store_true",
                     help="the N-rank path on a 1-GPU box: every rank on device 0, RCCL skipped; spawn, "
                          "rendezvous, partition, HBM plan, checks and max-over-ranks run as on N GPUs")
@@ -463,6 +465,10 @@ def run(args, world, rank, local_rank, wd, out):
         import host_bench
         pcie = host_bench.measure(ca, n, f, B, batch=64, batches=8, inflight=2, pinned=True, device=dev)
         pcie["unit"] = "GB/s of committed shard bytes (N*S per instance), host memory in and out"
+    batcher = None
+    if rank == 0 and world == 1 and args.config == "c2" and not args.no_batcher:
+        wd.enter("batcher sweep", 600)
+        batcher = batcher_sweep(cpu)
     ranks, skew = rank_timing(rdz, me, elapsed, args.steps, stage_ms)
     line = {
         "metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
@@ -489,7 +495,7 @@ def run(args, world, rank, local_rank, wd, out):
                                 f"recheck(t-2), decode(t-1) (rbc_dev_receive_step), two streams, {nsets} shard "
                                 "sets") if pipe else "serial"},
         **rep, **checks, "cpu_baseline": cpu, "pcie_inclusive": pcie, "rccl": rccl, "ranks": ranks,
-        "rank_skew": skew, "library": ca.rbc.library_path(), "value_joined": joined,
+        "rank_skew": skew, "library": ca.rbc.library_path(), "value_joined": joined, "batcher": batcher,
         "host": {kk: host[kk] for kk in ("cpu_model", "nproc", "cgroup_cpu_quota", "affinity_cpus")},
     }
     ok = all(checks[c] for c in ("values_ok", "oracle_sample_ok", "gather_ok")) and checks["decoded_ok"] == total
@@ -506,6 +512,38 @@ def run(args, world, rank, local_rank, wd, out):
     rdz.barrier()
     rdz.close()
     return 0
+
+
+BATCHER_LEVELS = (1024, 8192, 32768, 88064)  # outstanding validates; 88,064 = one C2 epoch (1,024 x 86 ECHOs)
+
+
+def batcher_sweep(cpu):
+    """The drop-in path the unchanged Go handlers use: validateMessage
+    (rbc/rbc.go:92-95) once per ECHO through the batcher's validate lane
+    (tools/batcher_bench validate-sweep: 16 client threads, each with a
+    sliding window of outstanding requests, C2 messages from host memory,
+    every verdict checked).  Host memory in, verdicts out: PCIe-inclusive,
+    never `value`.  The host's own SHA-NI verify of the same message shape
+    (cpu_baseline leg) sits beside it."""
+    import subprocess
+    exe = os.path.join(ROOT, "tools", "batcher_bench")
+    if not os.path.exists(exe):
+        return {"skipped": "tools/batcher_bench is not built"}
+    r = subprocess.run([exe, "validate-sweep", "256", "16", "200"] + [str(x) for x in BATCHER_LEVELS],
+                       capture_output=True, text=True, timeout=500)
+    rows = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    sweep = [x for x in rows if x.get("phase") == "validate"]
+    out = {"unit": "GB/s of ECHO shard bytes (S per message), host memory in, verdicts out",
+           "sweep": [{kk: x[kk] for kk in ("outstanding", "window", "messages", "GBps", "msg_per_s", "launches",
+                                            "msgs_per_launch", "failed")} for x in sweep],
+           "failures": next((x["failures"] for x in rows if x.get("phase") == "check"), None), "rc": r.returncode,
+           "tool": "tools/batcher_bench validate-sweep (C2: N=128, f=42, 1 MiB values, S=23,832; 16 client threads)"}
+    if cpu and cpu.get("validate"):
+        out["host_sha_ni"] = cpu["validate"]
+        best = max((x["GBps"] for x in sweep), default=0)
+        out["gpu_over_host_at_epoch"] = round(sweep[-1]["GBps"] / cpu["validate"]["GBps"], 2) if sweep else None
+        out["best_GBps"] = best
+    return out
 
 
 def rank_timing(rdz, me, elapsed, steps, stage_ms):
@@ -858,6 +896,24 @@ def cpu_baseline(args, host):
                 "sample": f"{count} instances x {B} B (N={n} f={f}), {secs:.2f} s wall on {nthreads} threads",
                 "status_sum": st}
 
+    def validate_rate():
+        """validateMessage of one C2 epoch's ECHOs (88,064 = 1,024 instances x
+        86) on the host's cores, SHA-NI where present: the per-message
+        baseline of the batcher's validate lane (key `batcher`)."""
+        n, f, B, _, _ = CONFIGS["c2"]
+        rng = np.random.default_rng(11)
+        com = [rbc_ref.encode_commit(n, f, rng.integers(0, 256, B, dtype=np.uint8)) for _ in range(32)]
+        shards = np.stack([c[0] for c in com])
+        branches = np.stack([c[2] for c in com])
+        roots = np.stack([np.frombuffer(c[1], np.uint8) for c in com])
+        m = np.arange(88064)
+        inst, j = (m // (n - f)) % len(com), m % (n - f)
+        secs, ok = rbc_ref.verify_many(n, shards, branches, roots, inst, j, threads)
+        S = shards.shape[2]
+        return {"GBps": round(len(m) * S / secs / 1e9, 3), "msg_per_s": round(len(m) / secs), "cores": threads,
+                "all_valid": bool(ok.all()), "kind": "port",
+                "sample": f"{len(m)} C2 ECHO messages (S={S}) from {len(com)} committed values, {secs:.3f} s"}
+
     main_cfg = args.config
     res, single = run(main_cfg, 6e9, threads), run(main_cfg, 6e9 / 16, 1)
     per_config, per_config_1 = {}, {}
@@ -872,6 +928,7 @@ def cpu_baseline(args, host):
             "per_config": {c: {"value": r["value"], "phases": r["phases"], "sample": r["sample"],
                                "single_core": {"value": per_config_1[c]["value"], "phases": per_config_1[c]["phases"]}}
                            for c, r in per_config.items()},
+            "validate": validate_rate() if main_cfg == "c2" else None,
             "host": host, "simd": ("avx2 " if feats & 1 else "") + ("sha-ni" if feats & 2 else ""),
             "status_sum": res["status_sum"] + single["status_sum"] + sum(r["status_sum"] for r in per_config.values())
             + sum(r["status_sum"] for c, r in per_config_1.items() if c != main_cfg)}

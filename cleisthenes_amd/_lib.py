@@ -116,6 +116,9 @@ _SIGS = {
     "rbc_batcher_wait": (c_int, [c_void_p, c_uint64]),
     "rbc_batcher_poll": (c_int, [c_void_p, c_uint64, POINTER(c_int)]),
     "rbc_batcher_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
+    "rbc_batcher_set_validate": (c_int, [c_void_p, c_int, c_size_t]),
+    "rbc_validate_packed": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, POINTER(c_uint64)]),
     "rbc_rs_new": (c_int, [c_int, c_int, c_int, POINTER(c_void_p)]),
     "rbc_rs_free": (None, [c_void_p]),
     "rbc_rs_encode": (c_int, [c_void_p, c_void_p, szp, c_int]),

@@ -16,6 +16,16 @@
 // batch-shaped shard / value buffers are pinned (rbc_host_alloc) and pooled,
 // so the C API moves them with direct DMA (or the zero-copy gather of the
 // present rows) instead of staging them once more.
+//
+// validateMessage has its own lane (round 5): it is called once per ECHO --
+// N-f per instance per node, 88 k per C2 epoch of 1,024 instances -- so the
+// per-request work must not funnel through one thread.  The CALLING thread
+// reserves a slot in the open pinned arena (a short critical section), copies
+// its shard, branch and root there in the device layout, and leaves; a lane
+// worker seals the arena when it is full or its first message has waited
+// max_wait_us and hands it to rbc_validate_packed (one DMA, one launch), up to
+// kVInflight arenas in flight.  Results land in the callers' ok_out, tickets
+// complete in arena order.
 #include <stdlib.h>
 #include <string.h>
 
@@ -48,15 +58,8 @@ struct Req {
     size_t *shard_len_out = nullptr;
     uint8_t *root_out = nullptr;
     uint8_t *branches_out = nullptr;
-    // validate
-    const uint8_t *root = nullptr;
-    const uint8_t *branch = nullptr;
-    size_t branch_len = 0;
-    const uint8_t *shard = nullptr;
-    size_t shard_len = 0;
-    uint32_t index = 0;
-    int *ok_out = nullptr;
     // interpolate
+    const uint8_t *root = nullptr;
     std::vector<const uint8_t *> in_shards;
     std::vector<size_t> in_lens;
     uint8_t *value_out = nullptr;
@@ -112,6 +115,63 @@ struct PinnedSet {
     Pinned shards, roots, br, values;
 };
 
+// One arena of the validate lane: the messages of one launch in the layout
+// rbc_validate_packed reads (shard bytes at 64-B aligned offsets, device-form
+// branches, roots, leaf indices), the verdicts, and the callers' ok_out.
+struct VBuf {
+    enum State { FREE, OPEN, SEALED, INFLIGHT };
+    Pinned arena, meta;
+    uint64_t *offs = nullptr;
+    uint32_t *lens = nullptr;
+    uint8_t *roots = nullptr, *br = nullptr, *idx = nullptr, *ok = nullptr, *shape = nullptr;
+    std::vector<int *> out;
+    int cap = 0;                     // messages the meta block holds
+    // reservation state, under the lane's spinlock while the arena is open;
+    // final once it is sealed (v_open no longer points at it)
+    int count = 0;                   // reserved slots
+    size_t bytes = 0;                // reserved arena bytes
+    // reserved slots not yet copied, plus kSealed once sealed: == kSealed
+    // means ready to launch.  Only the returned values of its atomic updates
+    // are used, so a caller touches nothing of the arena after its last one
+    // (by then the arena may already be launched, completed and reopened).
+    static constexpr int64_t kSealed = (int64_t)1 << 40;
+    std::atomic<int64_t> pend{0};
+    uint64_t gen = 0;                // launch generation (tickets complete in this order)
+    State state = FREE;              // under vmu
+    std::chrono::steady_clock::time_point t0;
+    uint64_t ticket = 0;
+    int rc = RBC_OK;
+    bool layout(int msgs, int bslot) {  // the meta block for `msgs` messages
+        const size_t per = 8 + 4 + 32 + (size_t)bslot + 3;
+        if (!meta.ensure((size_t)msgs * per)) return false;
+        uint8_t *p = meta.p;
+        offs = reinterpret_cast<uint64_t *>(p);
+        lens = reinterpret_cast<uint32_t *>(p + (size_t)msgs * 8);
+        roots = p + (size_t)msgs * 12;
+        br = roots + (size_t)msgs * 32;
+        idx = br + (size_t)msgs * bslot;
+        ok = idx + msgs;
+        shape = ok + msgs;
+        cap = msgs;
+        out.assign(msgs, nullptr);
+        return true;
+    }
+};
+// a test-and-test-and-set spinlock for the reservation's few instructions:
+// the lane takes one per validateMessage from every client thread
+struct Spin {
+    std::atomic<bool> f{false};
+    void lock() {
+        for (;;) {
+            if (!f.exchange(true, std::memory_order_acquire)) return;
+            while (f.load(std::memory_order_relaxed)) __builtin_ia32_pause();
+        }
+    }
+    void unlock() { f.store(false, std::memory_order_release); }
+};
+constexpr uint64_t kVTicket = 1ull << 63;  // validate-lane tickets: kVTicket | gen << 20 | slot
+constexpr int kVSlotBits = 20;
+
 }  // namespace
 
 struct rbc_batcher {
@@ -137,6 +197,34 @@ struct rbc_batcher {
     bool stop = false;
     uint64_t batches = 0, requests = 0;
     std::thread worker;
+
+    // validate lane (see the file comment)
+    static constexpr int kVBufs = 6, kVInflight = 4;
+    int v_max_msgs = 65536;
+    size_t v_max_bytes = (size_t)256 << 20;
+    int bslot = 32;
+    Spin v_spin;                            // v_open and the open arena's count / bytes
+    VBuf *v_open = nullptr;
+    std::mutex vmu;                         // everything below
+    std::condition_variable v_work;         // launcher: a seal, a finished copy, a free launch slot
+    std::condition_variable v_fl;           // completer: a launch
+    std::condition_variable v_free;         // clients: a free arena
+    std::condition_variable v_done;         // clients: a completed generation
+    std::unique_ptr<VBuf> vb[kVBufs];
+    std::deque<VBuf *> v_sealed, v_flight;  // generation order
+    uint64_t v_next_gen = 1, v_next_launch = 1;
+    std::atomic<uint64_t> v_done_gen{0};
+    std::atomic<bool> v_any_failed{false};
+    std::unordered_map<uint64_t, int> v_failed;  // generations whose launch failed
+    uint64_t v_batches = 0, v_requests = 0;
+    bool v_stop = false, v_launcher_done = false;
+    std::thread v_worker, v_completer;
+    int v_reserve(size_t need, VBuf **B, int *slot, size_t *off);
+    void v_push_sealed(VBuf *B);
+    void v_launch(VBuf *B);
+    void v_complete(VBuf *B);
+    void v_run();
+    void v_finish_run();
 
     void run();
     std::vector<std::unique_ptr<PinnedSet>> pool;  // worker thread only
@@ -171,7 +259,7 @@ struct Pending {
     size_t Smax = 1;
     std::vector<int> idx;        // interpolate: requests in the batch
     std::vector<size_t> lens;
-    std::vector<uint8_t> ok, present, digests;
+    std::vector<uint8_t> present, digests;
     std::vector<uint32_t> slens;
     std::vector<int32_t> status;
     std::unique_ptr<PinnedSet> pin;  // shards / roots / branches / values of this launch
@@ -207,21 +295,6 @@ std::unique_ptr<Pending> rbc_batcher::submit(Kind kind, std::vector<Req> &&batch
                     ? RBC_ERR_DEVICE
                     : rbc_shard_commit(ctx, count, vals.data(), P->lens.data(), P->shards, P->Smax, P->slens.data(),
                                        P->roots, P->br, &P->ticket);
-    } else if (kind == K_VALIDATE) {
-        std::vector<const uint8_t *> sh(count), brs(count), rts(count);
-        std::vector<size_t> sl(count), bl(count);
-        std::vector<uint32_t> ix(count);
-        P->ok.assign(count, 0);
-        for (int i = 0; i < count; ++i) {
-            sh[i] = b[i].shard;
-            sl[i] = b[i].shard_len;
-            brs[i] = b[i].branch;
-            bl[i] = b[i].branch_len;
-            rts[i] = b[i].root;
-            ix[i] = b[i].index;
-        }
-        P->rc = rbc_validate_batch(ctx, count, sh.data(), sl.data(), ix.data(), brs.data(), bl.data(), rts.data(),
-                                   P->ok.data(), &P->ticket);
     } else {
         // interpolate: klauspost argument checks per request, then one batch
         // over the requests that pass them
@@ -291,11 +364,6 @@ void rbc_batcher::finish(Pending &P) {
             if (r.branches_out && depth)
                 memcpy(r.branches_out, P.br + (size_t)i * n * depth * 32, (size_t)n * depth * 32);
         });
-    } else if (P.kind == K_VALIDATE) {
-        for (int i = 0; i < count; ++i) {
-            if (rc) P.st[i] = rc;
-            else *b[i].ok_out = P.ok[i];
-        }
     } else {
         parallel_for((int)P.idx.size(), (size_t)k * P.Smax, [&](int t) {
             Req &r = b[P.idx[t]];
@@ -382,6 +450,180 @@ void rbc_batcher::run() {
     }
 }
 
+// ---- validate lane ----------------------------------------------------------
+
+// Hand a sealed arena (v_open no longer points at it, so its count and bytes
+// are final) to the launcher, keeping v_sealed in generation order.
+void rbc_batcher::v_push_sealed(VBuf *B) {
+    std::lock_guard<std::mutex> lk(vmu);
+    B->state = VBuf::SEALED;
+    B->pend.fetch_add(VBuf::kSealed);
+    auto it = v_sealed.begin();
+    while (it != v_sealed.end() && (*it)->gen < B->gen) ++it;
+    v_sealed.insert(it, B);
+    v_work.notify_one();
+}
+
+// A slot for one message of `need` arena bytes: the open arena's next slot
+// (spinlock only), sealing it when full; opening a free arena under vmu when
+// none is open.
+int rbc_batcher::v_reserve(size_t need, VBuf **out, int *slot, size_t *off) {
+    for (;;) {
+        v_spin.lock();
+        VBuf *B = v_open;
+        if (B && B->count < B->cap && B->bytes + need <= B->arena.cap) {
+            *out = B;
+            *slot = B->count++;
+            *off = B->bytes;
+            B->bytes += need;
+            B->pend.fetch_add(1);
+            const bool full = B->count == B->cap;
+            if (full) v_open = nullptr;
+            v_spin.unlock();
+            if (full) v_push_sealed(B);
+            return RBC_OK;
+        }
+        if (B) {  // no room for this message: seal (an empty arena goes through as a no-op)
+            v_open = nullptr;
+            v_spin.unlock();
+            v_push_sealed(B);
+            continue;
+        }
+        v_spin.unlock();
+        std::unique_lock<std::mutex> lk(vmu);
+        VBuf *f = nullptr;
+        for (;;) {
+            for (auto &x : vb)
+                if (x->state == VBuf::FREE) { f = x.get(); break; }
+            if (f || v_stop) break;
+            v_free.wait(lk);  // every arena is filling, sealed or in flight
+        }
+        if (!f) return RBC_ERR_INVALID_ARG;  // the batcher is being destroyed
+        if (f->cap != v_max_msgs && !f->layout(v_max_msgs, bslot)) return RBC_ERR_DEVICE;
+        if (!f->arena.ensure(std::max(v_max_bytes, need))) return RBC_ERR_DEVICE;
+        v_spin.lock();
+        if (v_open) {  // another caller opened one meanwhile: reserve there
+            v_spin.unlock();
+            continue;
+        }
+        // open f with this message in slot 0, so the launcher, woken here
+        // under vmu, always finds a non-empty arena to time
+        f->state = VBuf::OPEN;
+        f->gen = v_next_gen++;
+        f->count = 1;
+        f->bytes = need;
+        f->pend.store(1);
+        f->rc = RBC_OK;
+        f->ticket = 0;
+        f->t0 = std::chrono::steady_clock::now();  // max_wait runs from the first message
+        const bool full = f->cap == 1;
+        v_open = full ? nullptr : f;
+        v_spin.unlock();
+        *out = f;
+        *slot = 0;
+        *off = 0;
+        v_work.notify_one();
+        lk.unlock();
+        if (full) v_push_sealed(f);
+        return RBC_OK;
+    }
+}
+
+void rbc_batcher::v_launch(VBuf *B) {
+    B->rc = B->count ? rbc_validate_packed(ctx, B->count, B->arena.p, B->bytes, B->offs, B->lens, B->idx, B->br,
+                                           B->roots, B->ok, &B->ticket)
+                     : RBC_OK;
+    if (B->rc) B->ticket = 0;
+}
+
+void rbc_batcher::v_complete(VBuf *B) {
+    int rc = B->rc;
+    if (!rc && B->ticket) rc = rbc_wait(ctx, B->ticket);
+    for (int i = 0; i < B->count; ++i) *B->out[i] = (!rc && B->shape[i]) ? B->ok[i] : 0;
+    std::lock_guard<std::mutex> lk(vmu);
+    if (rc) {
+        v_failed[B->gen] = rc;
+        v_any_failed.store(true);
+    }
+    v_done_gen.store(B->gen);
+    v_batches += B->count > 0;
+    v_requests += B->count;
+    v_flight.pop_front();  // B: the completer takes launches in order
+    B->state = VBuf::FREE;
+    v_free.notify_all();
+    v_done.notify_all();
+    v_work.notify_one();  // a launch slot is free
+}
+
+// Lane launcher: seal the open arena when its first message has waited
+// max_wait_us and a launch slot is free (under load the arena keeps filling
+// while kVInflight launches run: fewer, larger launches), and launch sealed
+// arenas whose copies are complete, strictly in generation order.
+void rbc_batcher::v_run() {
+    std::unique_lock<std::mutex> lk(vmu);
+    for (;;) {
+        const auto now = std::chrono::steady_clock::now();
+        const bool slot_free = (int)(v_flight.size() + v_sealed.size()) < kVInflight;
+        VBuf *due = nullptr;
+        std::chrono::steady_clock::time_point wake{};
+        v_spin.lock();
+        if (v_open && v_open->count > 0) {
+            wake = v_open->t0 + std::chrono::microseconds(max_wait_us);
+            if (v_stop || (slot_free && wake <= now)) {
+                due = v_open;
+                v_open = nullptr;
+            }
+        } else if (v_open && v_stop) {  // an empty arena at shutdown: back to the free list
+            v_open->state = VBuf::FREE;
+            v_open = nullptr;
+        }
+        const bool open_pending = v_open && v_open->count > 0;
+        v_spin.unlock();
+        if (due) {
+            lk.unlock();
+            v_push_sealed(due);
+            lk.lock();
+            continue;
+        }
+        VBuf *F = v_sealed.empty() ? nullptr : v_sealed.front();
+        if (F && F->gen == v_next_launch && F->pend.load() == VBuf::kSealed && (int)v_flight.size() < kVInflight) {
+            v_sealed.pop_front();
+            v_next_launch++;
+            F->state = VBuf::INFLIGHT;
+            lk.unlock();
+            v_launch(F);
+            lk.lock();
+            v_flight.push_back(F);
+            v_fl.notify_one();
+            continue;
+        }
+        if (v_stop && !open_pending && v_sealed.empty()) {
+            v_launcher_done = true;  // everything launched: the completer drains v_flight and exits
+            v_fl.notify_one();
+            return;
+        }
+        if (open_pending && slot_free) v_work.wait_until(lk, wake);
+        else v_work.wait(lk);
+    }
+}
+
+// Lane completer: waits for the oldest launch (rbc_wait does not hold the
+// context while it waits, so the launcher keeps submitting) and completes it.
+void rbc_batcher::v_finish_run() {
+    std::unique_lock<std::mutex> lk(vmu);
+    for (;;) {
+        if (!v_flight.empty()) {
+            VBuf *B = v_flight.front();
+            lk.unlock();
+            v_complete(B);
+            lk.lock();
+            continue;
+        }
+        if (v_launcher_done) return;
+        v_fl.wait(lk);
+    }
+}
+
 namespace {
 uint64_t enqueue(rbc_batcher *b, Req &&r) {
     std::lock_guard<std::mutex> lk(b->mu);
@@ -408,8 +650,21 @@ int rbc_batcher_create(rbc_ctx *ctx, int max_batch, int max_wait_us, rbc_batcher
     b->depth = d;
     b->max_batch = max_batch;
     b->max_wait_us = max_wait_us;
+    b->bslot = std::max(d, 1) * 32;
+    for (auto &x : b->vb) x = std::make_unique<VBuf>();
     b->worker = std::thread([b] { b->run(); });
+    b->v_worker = std::thread([b] { b->v_run(); });
+    b->v_completer = std::thread([b] { b->v_finish_run(); });
     *out = b;
+    return RBC_OK;
+}
+
+int rbc_batcher_set_validate(rbc_batcher *b, int max_msgs, size_t max_bytes) {
+    if (!b || max_msgs < 1 || max_msgs >= (1 << kVSlotBits) || max_bytes < 64) return RBC_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(b->vmu);
+    if (b->v_next_gen != 1) return RBC_ERR_INVALID_ARG;  // before the first validate only
+    b->v_max_msgs = max_msgs;
+    b->v_max_bytes = max_bytes;
     return RBC_OK;
 }
 
@@ -421,6 +676,14 @@ void rbc_batcher_destroy(rbc_batcher *b) {
     }
     b->cv_work.notify_all();
     if (b->worker.joinable()) b->worker.join();
+    {
+        std::lock_guard<std::mutex> lk(b->vmu);
+        b->v_stop = true;  // the lane drains too
+    }
+    b->v_work.notify_all();
+    b->v_free.notify_all();
+    if (b->v_worker.joinable()) b->v_worker.join();
+    if (b->v_completer.joinable()) b->v_completer.join();
     delete b;
 }
 
@@ -446,16 +709,51 @@ int rbc_batcher_validate(rbc_batcher *b, const uint8_t *root, const uint8_t *bra
                          const uint8_t *shard, size_t shard_len, uint32_t index, int *ok_out, uint64_t *ticket) {
     if (!b || !ticket || !ok_out || !root) return RBC_ERR_INVALID_ARG;
     *ok_out = 0;
-    Req r;
-    r.kind = K_VALIDATE;
-    r.root = root;
-    r.branch = branch;
-    r.branch_len = branch_len;
-    r.shard = shard;
-    r.shard_len = shard_len;
-    r.index = index;
-    r.ok_out = ok_out;
-    *ticket = enqueue(b, std::move(r));
+    const int n = b->n, d = b->depth;
+    // the Go-form branch omits an empty level-0 sibling (rbc_validate_batch's shape rule)
+    const bool empty0 = d > 0 && (index ^ 1u) >= (uint32_t)n;
+    const size_t want = (size_t)32 * (d - (empty0 ? 1 : 0));
+    const bool shape_ok = index < (uint32_t)n && branch_len == want && shard_len != 0 && shard && (!want || branch);
+    const size_t need = shape_ok ? (shard_len + 63) / 64 * 64 : 64;
+    VBuf *B = nullptr;
+    int slot = 0;
+    size_t off = 0;
+    const int rc = b->v_reserve(need, &B, &slot, &off);
+    if (rc) return rc;
+    // the copy runs on the calling thread, outside the lock
+    uint8_t *row = B->arena.p + off, *br = B->br + (size_t)slot * b->bslot;
+    B->out[slot] = ok_out;
+    B->offs[slot] = off;
+    B->shape[slot] = shape_ok;
+    if (shape_ok) {
+        memcpy(row, shard, shard_len);
+        B->lens[slot] = (uint32_t)shard_len;
+        B->idx[slot] = (uint8_t)index;
+        size_t o = 0;
+        for (int l = 0; l < d; ++l) {
+            if (l == 0 && empty0) {
+                memset(br, 0, 32);  // the device form keeps a zero level-0 slot
+                continue;
+            }
+            memcpy(br + 32 * l, branch + o, 32);
+            o += 32;
+        }
+        if (d == 0) memset(br, 0, 32);
+        memcpy(B->roots + (size_t)slot * 32, root, 32);
+    } else {  // hashed as one zero byte; the verdict is discarded (0)
+        memset(row, 0, 64);
+        B->lens[slot] = 1;
+        B->idx[slot] = 0;
+        memset(br, 0, b->bslot);
+        memset(B->roots + (size_t)slot * 32, 0, 32);
+    }
+    *ticket = kVTicket | (B->gen << kVSlotBits) | (uint64_t)slot;  // gen is stable until this slot completes
+    // the last copy of a sealed arena wakes the launcher (either it sees
+    // this copy when it checks, or this update sees the seal)
+    if (B->pend.fetch_sub(1) - 1 == VBuf::kSealed) {
+        std::lock_guard<std::mutex> lk(b->vmu);
+        b->v_work.notify_one();
+    }
     return RBC_OK;
 }
 
@@ -478,6 +776,15 @@ int rbc_batcher_interpolate(rbc_batcher *b, const uint8_t *root, const uint8_t *
 
 int rbc_batcher_wait(rbc_batcher *b, uint64_t ticket) {
     if (!b) return RBC_ERR_INVALID_ARG;
+    if (ticket & kVTicket) {  // validate lane: complete when its arena's generation is
+        const uint64_t gen = (ticket & ~kVTicket) >> kVSlotBits;
+        if (gen > 0 && b->v_done_gen.load() >= gen && !b->v_any_failed.load()) return RBC_OK;  // no lock
+        std::unique_lock<std::mutex> lk(b->vmu);
+        if (gen == 0 || gen >= b->v_next_gen) return RBC_ERR_INVALID_ARG;
+        b->v_done.wait(lk, [&] { return b->v_done_gen.load() >= gen; });
+        const auto it = b->v_failed.find(gen);
+        return it == b->v_failed.end() ? RBC_OK : it->second;
+    }
     if (ticket == 0 || ticket >= b->next.load()) return RBC_ERR_INVALID_ARG;
     auto &sh = b->shard[ticket % rbc_batcher::kShards];
     std::unique_lock<std::mutex> lk(sh.mu);
@@ -493,6 +800,13 @@ int rbc_batcher_wait(rbc_batcher *b, uint64_t ticket) {
 
 int rbc_batcher_poll(rbc_batcher *b, uint64_t ticket, int *done_out) {
     if (!b || !done_out) return RBC_ERR_INVALID_ARG;
+    if (ticket & kVTicket) {
+        const uint64_t gen = (ticket & ~kVTicket) >> kVSlotBits;
+        std::lock_guard<std::mutex> lk(b->vmu);
+        if (gen == 0 || gen >= b->v_next_gen) return RBC_ERR_INVALID_ARG;
+        *done_out = b->v_done_gen.load() >= gen;
+        return RBC_OK;
+    }
     if (ticket == 0 || ticket >= b->next.load()) return RBC_ERR_INVALID_ARG;
     auto &sh = b->shard[ticket % rbc_batcher::kShards];
     std::lock_guard<std::mutex> lk(sh.mu);
@@ -502,9 +816,9 @@ int rbc_batcher_poll(rbc_batcher *b, uint64_t ticket, int *done_out) {
 
 int rbc_batcher_stats(rbc_batcher *b, uint64_t *batches, uint64_t *requests) {
     if (!b) return RBC_ERR_INVALID_ARG;
-    std::lock_guard<std::mutex> lk(b->mu);
-    if (batches) *batches = b->batches;
-    if (requests) *requests = b->requests;
+    std::scoped_lock lk(b->mu, b->vmu);
+    if (batches) *batches = b->batches + b->v_batches;
+    if (requests) *requests = b->requests + b->v_requests;
     return RBC_OK;
 }
 

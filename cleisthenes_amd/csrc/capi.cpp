@@ -120,7 +120,8 @@ struct Ws {
 // batch t computes.  `finish` copies the pinned results into the caller's
 // buffers at completion (rbc_wait / rbc_poll / slot reuse).
 struct Slot {
-    DevBuf d_values, d_shards, d_leaves, d_roots, d_branches, d_valid, d_status, d_digests, d_lens, d_slens, d_idx;
+    DevBuf d_values, d_shards, d_leaves, d_roots, d_branches, d_valid, d_status, d_digests, d_lens, d_slens, d_idx,
+        d_offs;
     DevBuf h_in{nullptr, 0, true}, h_out{nullptr, 0, true};
     Ws ws;
     hipStream_t stream = nullptr;
@@ -137,7 +138,7 @@ struct Slot {
     int d2h_rc = 0;
     void release() {
         for (DevBuf *b : {&d_values, &d_shards, &d_leaves, &d_roots, &d_branches, &d_valid, &d_status, &d_digests,
-                          &d_lens, &d_slens, &d_idx, &h_in, &h_out})
+                          &d_lens, &d_slens, &d_idx, &d_offs, &h_in, &h_out})
             b->release();
         ws.release();
         if (stream) (void)hipStreamDestroy(stream);
@@ -1680,6 +1681,69 @@ int rbc_validate_batch(rbc_ctx *c, int count, const uint8_t *const *shards, cons
     });
 }
 
+// The packed form of rbc_validate_batch: the caller (the batcher's validate
+// lane, or a Go batcher with its own rbc_host_alloc rings) has already laid the
+// messages out as the device reads them, so this is one DMA of the shard arena,
+// the metadata, one launch and a deferred D2H of the verdicts -- no per-message
+// staging copy on the submitting thread.
+int rbc_validate_packed(rbc_ctx *c, int count, const uint8_t *arena, size_t arena_bytes, const uint64_t *offs,
+                        const uint32_t *lens, const uint8_t *idx, const uint8_t *branches, const uint8_t *roots,
+                        uint8_t *ok_out, uint64_t *ticket) {
+    if (!c || count < 0 ||
+        (count > 0 && (!arena || !arena_bytes || !offs || !lens || !idx || !branches || !roots || !ok_out)))
+        return RBC_ERR_INVALID_ARG;
+    if (count == 0) { if (ticket) *ticket = 0; return RBC_OK; }
+    // every message's 64-B blocks must lie inside the arena (the kernel reads
+    // whole blocks) and its leaf index inside the tree
+    for (int i = 0; i < count; ++i)
+        if (offs[i] % 64 || lens[i] == 0 || offs[i] + round_up((size_t)lens[i], 64) > arena_bytes || idx[i] >= c->n)
+            return RBC_ERR_INVALID_ARG;
+    const int d = c->depth;
+    const size_t bslot = (size_t)std::max(d, 1) * 32;
+    std::lock_guard<std::mutex> lk(c->mu);
+    RBC_HIP(hipSetDevice(c->device));
+    Slot *sp = acquire_slot(c);
+    if (!sp) return RBC_ERR_DEVICE;
+    Slot &s = *sp;
+    hipStream_t st = s.stream;
+    RBC_HIP(s.d_shards.ensure(arena_bytes));
+    RBC_HIP(s.d_branches.ensure((size_t)count * bslot));
+    RBC_HIP(s.d_roots.ensure((size_t)count * 32));
+    RBC_HIP(s.d_slens.ensure((size_t)count * 4));
+    RBC_HIP(s.d_idx.ensure((size_t)count));
+    RBC_HIP(s.d_offs.ensure((size_t)count * 8));
+    RBC_HIP(s.d_valid.ensure((size_t)count));
+    RBC_HIP(hipMemcpyAsync(s.d_shards.p, arena, arena_bytes, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(s.d_offs.p, offs, (size_t)count * 8, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(s.d_slens.p, lens, (size_t)count * 4, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(s.d_idx.p, idx, (size_t)count, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(s.d_branches.p, branches, (size_t)count * bslot, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(s.d_roots.p, roots, (size_t)count * 32, hipMemcpyHostToDevice, st));
+    ShaArgs a{};
+    a.count = count;
+    a.rows_per_inst = 1;
+    a.rows = s.d_shards.as<uint8_t>();
+    a.row_offs = s.d_offs.as<uint64_t>();
+    a.lens = s.d_slens.as<uint32_t>();
+    a.idx = s.d_idx.as<uint8_t>();
+    a.idx_stride = 1;
+    a.per_message = 1;
+    a.n = c->n;
+    a.depth = d;
+    a.branches = s.d_branches.as<uint8_t>();
+    a.br_inst_pitch = bslot;
+    a.roots = s.d_roots.as<uint8_t>();
+    a.valid = s.d_valid.as<uint8_t>();
+    a.prio = c->rx_prio;
+    RBC_HIP(rbc_launch_sha_rows(a, true, st));
+    void *d_valid = s.d_valid.p;
+    auto d2h = [=]() -> int {  // behind the next submission's H2D (Slot::d2h)
+        RBC_HIP(hipMemcpyAsync(ok_out, d_valid, (size_t)count, hipMemcpyDeviceToHost, st));
+        return RBC_OK;
+    };
+    return submit(c, s, ticket, []() { return RBC_OK; }, d2h);
+}
+
 int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t shard_pitch,
                           const size_t *shard_lens, const uint8_t *present, const uint8_t *roots,
                           uint8_t *values_out, size_t value_pitch, uint8_t *digests_out, int32_t *status_out,
@@ -1795,11 +1859,26 @@ int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t s
 // in an rbc_poll that finds it done, or when its slot is needed again.
 int rbc_wait(rbc_ctx *c, uint64_t ticket) {
     if (!c || ticket == 0) return RBC_ERR_INVALID_ARG;
-    std::lock_guard<std::mutex> lk(c->mu);
+    std::unique_lock<std::mutex> lk(c->mu);
     if (ticket >= c->next_ticket) return RBC_ERR_INVALID_ARG;
     (void)hipSetDevice(c->device);
+    // Wait for the submission's completion event WITHOUT the context lock, so
+    // other threads keep submitting (the batcher's validate lane launches
+    // while its completer waits); then retire it under the lock -- unless
+    // another thread retired it meanwhile (its status is then in `retired`).
+    hipEvent_t ev = nullptr;
     for (auto &sl : c->slots)
-        if (sl->busy && sl->ticket == ticket) return retire(c, *sl);
+        if (sl->busy && sl->ticket == ticket) {
+            flush_d2h(*sl);
+            ev = sl->done;
+        }
+    if (ev) {
+        lk.unlock();
+        (void)hipEventSynchronize(ev);  // a reused slot's later event only waits longer
+        lk.lock();
+        for (auto &sl : c->slots)
+            if (sl->busy && sl->ticket == ticket) return retire(c, *sl);
+    }
     auto it = c->retired.find(ticket);
     if (it == c->retired.end()) return RBC_OK;  // completed and already collected
     const int st = it->second;

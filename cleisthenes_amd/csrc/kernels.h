@@ -60,6 +60,7 @@ struct ShaArgs {
     uint8_t *leaves;           // [I][N][32] (nullable)
     uint64_t leaves_inst_pitch;
     int per_message;           // 1: each instance is one ECHO message (leaf index = idx[inst])
+    const uint64_t *row_offs;  // per_message: message i's bytes at rows + row_offs[i] (nullable: i * inst_pitch)
     const uint32_t *list;      // list mode: rows (inst << 8 | pos), count in *list_count
     const uint32_t *list_count;
     // verify

@@ -223,7 +223,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
     if (a.status && a.status[inst] != 0) return;
     const int rowsel = a.per_message ? 0 : pos;
     const uint32_t S = inst_len(a.lens, a.uniform_len, inst);
-    const uint8_t *row = a.rows + (size_t)inst * a.inst_pitch + (size_t)rowsel * a.row_pitch;
+    const uint8_t *row = a.row_offs ? a.rows + a.row_offs[inst]  // packed per-message arena (64-B aligned)
+                                    : a.rows + (size_t)inst * a.inst_pitch + (size_t)rowsel * a.row_pitch;
     Sha256State s;
     sha256_row(row, S, s);
     uint32_t h[8];

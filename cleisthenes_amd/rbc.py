@@ -716,6 +716,10 @@ class Batcher:
                     "root": bytes(h["root"]), "shard_len": S}
         return {"value": bytes(h["value"][: h["vlen"].value]), "digest": bytes(h["dig"])}
 
+    def set_validate(self, max_msgs: int, max_bytes: int) -> None:
+        """The validate lane's arena size (rbc_batcher_set_validate; before the first validate)."""
+        check(lib.rbc_batcher_set_validate(self._p, max_msgs, max_bytes), "rbc_batcher_set_validate")
+
     def stats(self):
         b, r = c_uint64(0), c_uint64(0)
         check(lib.rbc_batcher_stats(self._p, byref(b), byref(r)))

@@ -275,6 +275,20 @@ int rbc_shard_commit(rbc_ctx *ctx, int count, const uint8_t *const *values, cons
 int rbc_validate_batch(rbc_ctx *ctx, int count, const uint8_t *const *shards, const size_t *shard_lens,
                        const uint32_t *indices, const uint8_t *const *branches, const size_t *branch_lens,
                        const uint8_t *const *roots, uint8_t *ok_out, uint64_t *ticket);
+/* rbc_validate_batch with the messages already laid out as the device reads
+ * them -- for a caller that keeps its own pinned request rings (the batcher's
+ * validate lane; a Go batcher over rbc_host_alloc memory).  Message i's shard
+ * bytes are arena[offs[i] .. offs[i] + lens[i]) with offs[i] % 64 == 0 and the
+ * arena readable to offs[i] + round_up(lens[i], 64); branches[i] is the
+ * device form [depth][32] (a zero slot for an empty level-0 sibling); roots[i]
+ * 32 bytes; idx[i] < n the sender's leaf index.  One DMA of arena[0,
+ * arena_bytes), one launch, the verdicts into ok_out[count] (1 = valid).
+ * Every host buffer must stay valid until the ticket completes; pinned
+ * (rbc_host_alloc) memory gives direct DMA.  Replaces the per-message staging
+ * of validateMessage (rbc/rbc.go:92-95) for coalesced ECHOs. */
+int rbc_validate_packed(rbc_ctx *ctx, int count, const uint8_t *arena, size_t arena_bytes, const uint64_t *offs,
+                        const uint32_t *lens, const uint8_t *idx, const uint8_t *branches, const uint8_t *roots,
+                        uint8_t *ok_out, uint64_t *ticket);
 /* interpolate() for `count` instances: shards [count][n][shard_pitch] with
  * present [count][n] (0 = missing, the Go `len == 0`), shard_lens [count],
  * roots [count][32] -> values_out [count][value_pitch] (k*S_i bytes),
@@ -312,9 +326,16 @@ void rbc_batcher_destroy(rbc_batcher *b); /* drains pending requests first */
 /* shard(): shards_out n*S (shard j at j*S), root 32 B, branches n*d*32 (device form, nullable) */
 int rbc_batcher_shard(rbc_batcher *b, const uint8_t *data, size_t len, uint8_t *shards_out, size_t shards_cap,
                       size_t *shard_len_out, uint8_t *root_out, uint8_t *branches_out, uint64_t *ticket);
-/* validateMessage(): *ok_out set when the ticket completes */
+/* validateMessage(): *ok_out set when the ticket completes.  Validates have
+ * their own lane: the calling thread copies the message into the open pinned
+ * arena (device layout) and returns; an arena is launched through
+ * rbc_validate_packed when it holds max_msgs messages or max_bytes of shards,
+ * or its first message has waited max_wait_us (max_batch does not apply). */
 int rbc_batcher_validate(rbc_batcher *b, const uint8_t *root, const uint8_t *branch, size_t branch_len,
                          const uint8_t *shard, size_t shard_len, uint32_t index, int *ok_out, uint64_t *ticket);
+/* The validate lane's arena size (default 65,536 messages / 256 MiB of
+ * shards, six arenas, four in flight); before the first validate only. */
+int rbc_batcher_set_validate(rbc_batcher *b, int max_msgs, size_t max_bytes);
 /* interpolate(): shards/lens are n entries (lens[j] == 0: missing) */
 int rbc_batcher_interpolate(rbc_batcher *b, const uint8_t *root, const uint8_t *const *shards, const size_t *lens,
                             uint8_t *value_out, size_t value_cap, size_t *value_len, uint8_t *digest_out,

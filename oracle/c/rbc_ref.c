@@ -609,3 +609,48 @@ double rbcref_pipeline2(int n, int f, int count, size_t B, int threads, const ui
     if (dec_secs) *dec_secs = ds;
     return (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
 }
+
+/* validateMessage (rbc/rbc.go:92-95) for `count` ECHO messages on `threads`
+ * host threads (SHA-NI where present): message m verifies shard j[m] of
+ * instance inst[m] against its branch and root, from a committed set of
+ * shards [ninst][n][S], branches [ninst][n][d][32], roots [ninst][32].  The
+ * batcher's CPU baseline (bench.py cpu_baseline leg).  Returns wall seconds. */
+typedef struct {
+    int n, d, first, count;
+    size_t S;
+    const uint8_t *shards, *branches, *roots;
+    const int32_t *inst, *j;
+    uint8_t *ok;
+} vjob_t;
+
+static void *verify_worker(void *arg) {
+    vjob_t *jb = (vjob_t *)arg;
+    for (int m = jb->first; m < jb->first + jb->count; m++) {
+        const size_t i = (size_t)jb->inst[m], j = (size_t)jb->j[m];
+        jb->ok[m] = (uint8_t)rbcref_merkle_verify(jb->n, jb->shards + (i * jb->n + j) * jb->S, jb->S, (uint32_t)j,
+                                                  jb->branches + (i * jb->n + j) * jb->d * 32, jb->roots + 32 * i);
+    }
+    return NULL;
+}
+
+double rbcref_verify_many(int n, size_t S, const uint8_t *shards, const uint8_t *branches, const uint8_t *roots,
+                          int count, const int32_t *inst, const int32_t *j, int threads, uint8_t *ok) {
+    cpu_detect();
+    if (threads < 1) threads = 1;
+    if (threads > count) threads = count;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    vjob_t jobs[256];
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    int per = count / threads, extra = count % threads, first = 0;
+    for (int t = 0; t < threads; t++) {
+        int c = per + (t < extra);
+        jobs[t] = (vjob_t){n, tree_depth(n), first, c, S, shards, branches, roots, inst, j, ok};
+        pthread_create(&th[t], NULL, verify_worker, &jobs[t]);
+        first += c;
+    }
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+}

@@ -43,6 +43,9 @@ def load():
     lib.rbcref_cpu_features.restype = c_int
     lib.rbcref_force_scalar.argtypes = [c_int]
     lib.rbcref_force_scalar.restype = None
+    lib.rbcref_verify_many.argtypes = [c_int, c_size_t, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
+                                       c_void_p]
+    lib.rbcref_verify_many.restype = c_double
     return lib
 
 
@@ -136,3 +139,18 @@ def pipeline(n, f, count, B, threads, values, present, corrupt, phases=False):
     if phases:
         return secs, st.value, es.value, ds.value
     return secs, st.value
+
+
+def verify_many(n, shards, branches, roots, inst, j, threads):
+    """validateMessage of messages (inst[m], j[m]) over a committed set
+    (shards [I][n][S], branches [I][n][d][32], roots [I][32]) on `threads`
+    host threads -> (wall seconds, ok [count])."""
+    shards = np.ascontiguousarray(shards, dtype=np.uint8)
+    branches = np.ascontiguousarray(branches, dtype=np.uint8)
+    roots = np.ascontiguousarray(roots, dtype=np.uint8)
+    inst = np.ascontiguousarray(inst, dtype=np.int32)
+    j = np.ascontiguousarray(j, dtype=np.int32)
+    ok = np.zeros(len(inst), dtype=np.uint8)
+    secs = lib().rbcref_verify_many(n, shards.shape[2], p(shards), p(branches), p(roots), len(inst), p(inst), p(j),
+                                    threads, p(ok))
+    return secs, ok

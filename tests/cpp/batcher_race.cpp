@@ -139,6 +139,23 @@ int rbc_validate_batch(rbc_ctx *c, int count, const uint8_t *const *shards, cons
     return RBC_OK;
 }
 
+int rbc_validate_packed(rbc_ctx *c, int count, const uint8_t *arena, size_t arena_bytes, const uint64_t *offs,
+                        const uint32_t *lens, const uint8_t *idx, const uint8_t *branches, const uint8_t *roots,
+                        uint8_t *ok_out, uint64_t *ticket) {
+    // the real API's argument checks, then the arena read at some point before completion
+    for (int i = 0; i < count; ++i)
+        if (offs[i] % 64 || !lens[i] || offs[i] + (lens[i] + 63) / 64 * 64 > arena_bytes || idx[i] >= c->n)
+            return RBC_ERR_INVALID_ARG;
+    const size_t bslot = (size_t)std::max(c->d, 1) * 32;
+    *ticket = launch(c, [=] {
+        for (int i = 0; i < count; ++i)
+            ok_out[i] = rbcref_merkle_verify(c->n, arena + offs[i], lens[i], idx[i], branches + i * bslot,
+                                             roots + 32 * i);
+        return RBC_OK;
+    });
+    return RBC_OK;
+}
+
 int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t pitch, const size_t *shard_lens,
                           const uint8_t *present, const uint8_t *roots, uint8_t *values_out, size_t value_pitch,
                           uint8_t *digests_out, int32_t *status_out, uint64_t *ticket) {
@@ -361,6 +378,8 @@ int main(int argc, char **argv) {
         for (const int max_batch : {1, 5, 64}) {
             rbc_batcher *bt = nullptr;
             if (rbc_batcher_create(&ctx, max_batch, 300, &bt) != RBC_OK) return 2;
+            // small validate arenas: sealed by count, by bytes, and grown for one large message
+            if (rbc_batcher_set_validate(bt, max_batch, max_batch == 64 ? 1024 : 4096) != RBC_OK) return 2;
             std::vector<std::thread> th;
             for (int t = 0; t < T; ++t) th.emplace_back(client, bt, n, f, t, R, &pool);
             for (auto &x : th) x.join();

@@ -1,0 +1,99 @@
+"""The batcher's validate lane on the GPU at epoch scale:
+validateMessage (rbc/rbc.go:92-95) arrives once per ECHO from every
+instance's goroutine, so tens of thousands are outstanding per node.  Here
+16,384 are submitted from 8 threads before any is waited on; every verdict
+must equal the C oracle's (oracle/rbc_ref.verify) on the same message, and
+the lane must coalesce them into few launches.  Messages come from proposals
+committed by the oracle, with mixed shard lengths in one arena (ragged
+values), honest and tampered: a flipped shard byte, a flipped branch byte, a
+wrong root, a wrong index, a truncated branch, an empty shard."""
+import threading
+
+import numpy as np
+import pytest
+
+import rbc_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _unflatten(flat, j, n, d):
+    """Go flat branch -> device slots [d][32] (zero level-0 slot when j ^ 1 >= n), or None on a bad length."""
+    empty0 = d > 0 and (j ^ 1) >= n
+    if j >= n or len(flat) != 32 * (d - empty0):
+        return None
+    slots = np.zeros((max(d, 1), 32), np.uint8)
+    body = np.frombuffer(flat, np.uint8).reshape(-1, 32) if flat else np.zeros((0, 32), np.uint8)
+    slots[int(empty0):d] = body
+    return slots[:d]
+
+
+def _messages(n, f, count, seed):
+    rng = np.random.default_rng(seed)
+    d = max(1, (n - 1).bit_length()) if n > 1 else 0
+    commits = []
+    for _ in range(24):
+        v = rng.integers(0, 256, int(rng.integers(1, 180_000)), dtype=np.uint8)
+        shards, root, br, _ = rbc_ref.encode_commit(n, f, v)
+        commits.append((shards, root, br))
+    msgs = []
+    for m in range(count):
+        shards, root, br = commits[int(rng.integers(len(commits)))]
+        j = int(rng.integers(n))
+        flat = b"".join(bytes(br[j, l]) for l in range(d) if not (l == 0 and (j ^ 1) >= n))
+        shard = shards[j].tobytes()
+        idx = j
+        kind = int(rng.integers(10))
+        if kind == 1:
+            b = bytearray(shard)
+            b[int(rng.integers(len(b)))] ^= 0x10
+            shard = bytes(b)
+        elif kind == 2 and flat:
+            b = bytearray(flat)
+            b[int(rng.integers(len(b)))] ^= 0x02
+            flat = bytes(b)
+        elif kind == 3:
+            root = bytes([root[0] ^ 1]) + root[1:]
+        elif kind == 4:
+            idx = (j + 1 + int(rng.integers(n - 1))) % n if n > 1 else j
+        elif kind == 5 and flat:
+            flat = flat[:-32]
+        elif kind == 6:
+            shard = b""
+        slots = _unflatten(flat, idx, n, d)
+        want = bool(shard) and slots is not None and rbc_ref.verify(n, np.frombuffer(shard, np.uint8), idx, slots,
+                                                                    root)
+        msgs.append((root, flat, shard, idx, want))
+    return msgs
+
+
+@pytest.mark.parametrize("n,f", [(128, 42), (37, 12)])
+def test_validate_lane_16k_outstanding_matches_oracle(gpu, n, f):
+    msgs = _messages(n, f, 16384, seed=n)
+    ctx = gpu.Context(n, f)
+    for arena_msgs, max_wait in ((65536, 3_000_000), (1000, 200)):
+        bt = gpu.Batcher(ctx, max_batch=256, max_wait_us=max_wait)
+        bt.set_validate(arena_msgs, 256 << 20)
+        handles = [None] * len(msgs)
+
+        def submit(t):
+            for m in range(t, len(msgs), 8):
+                root, flat, shard, idx, _ = msgs[m]
+                handles[m] = bt.submit_validate(root, flat, shard, idx)
+
+        th = [threading.Thread(target=submit, args=(t,)) for t in range(8)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        got = [bt.wait(h) for h in handles]  # all 16,384 were outstanding before the first wait
+        want = [m[4] for m in msgs]
+        assert got == want, [i for i, (a, b) in enumerate(zip(got, want)) if a != b][:10]
+        launches, requests = bt.stats()
+        assert requests == len(msgs)
+        if arena_msgs == 65536:  # one arena holds every outstanding message: one launch, at most a few
+            assert launches <= 2, launches
+        else:  # 1,000-message arenas rotate through the lane's six, four in flight
+            assert launches >= len(msgs) // 1000, launches
+        bt.close()
+    assert 0.3 < np.mean(want) < 0.9  # honest and tampered messages both present

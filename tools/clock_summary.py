@@ -26,7 +26,7 @@ import sys
 from collections import defaultdict
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from trace_summary import CONFIGS, role, summarize  # noqa: E402
+from trace_summary import CONFIGS, read_lines, role, summarize  # noqa: E402
 
 SIMDS = 1024
 
@@ -36,7 +36,7 @@ def counters(d, sub, n, k, inst, last):
     if not os.path.exists(f):
         return {}
     acc = defaultdict(float)
-    for r in csv.DictReader(open(f)):
+    for r in csv.DictReader(read_lines(f)):
         g = int(r["Grid_Size"])
         acc[(role(r["Kernel_Name"], g, n, k, inst), g, int(r["Dispatch_Id"]), r["Counter_Name"])] += float(
             r["Counter_Value"])

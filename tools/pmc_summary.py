@@ -18,7 +18,7 @@ import sys
 from collections import defaultdict
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from trace_summary import CONFIGS, role, shared_path, summarize  # noqa: E402
+from trace_summary import CONFIGS, read_lines, role, shared_path, summarize  # noqa: E402
 
 
 def blocks(S):
@@ -32,7 +32,7 @@ def load_pmc(d, n, k, inst, last, path=False):
         if not os.path.exists(f) or sub == "trace":
             continue
         acc = defaultdict(float)  # (role, grid, dispatch, counter) -> summed value (over XCDs / instances)
-        for r in csv.DictReader(open(f)):
+        for r in csv.DictReader(read_lines(f)):
             g = int(r["Grid_Size"])
             rl = role(r["Kernel_Name"], g, n, k, inst, path)
             acc[(rl, g, int(r["Dispatch_Id"]), r["Counter_Name"])] += float(r["Counter_Value"])

@@ -26,6 +26,30 @@ CONFIGS = {"c1": (64, 21), "c2": (128, 42), "c3": (128, 42), "c4": (256, 85)}
 VALUE_BYTES = {"c1": 1 << 20, "c2": 1 << 20, "c3": 4 << 20, "c4": 64 << 10}
 
 
+def read_lines(path, tries=5):
+    """A CSV file's lines, read with os.read (retried: reads of freshly merged
+    gpurun_out files have failed here with EBADF)."""
+    import os
+    import time
+    for t in range(tries):
+        try:
+            fd = os.open(path, os.O_RDONLY)
+            try:
+                chunks = []
+                while True:
+                    b = os.read(fd, 1 << 20)
+                    if not b:
+                        break
+                    chunks.append(b)
+            finally:
+                os.close(fd)
+            return b"".join(chunks).decode().splitlines()
+        except OSError:
+            if t == tries - 1:
+                raise
+            time.sleep(0.2)
+
+
 def shared_path(config, value_bytes=0):
     """The receive step's ECHO-verify form at a config: the C library's rule
     (csrc/capi.cpp shared_path_verify, rbc_ctx_verify_form): leaves + the
@@ -61,9 +85,9 @@ def role(name, grid, n, k, inst, path=False):
 def summarize(path, config, inst, last, before=None):
     n, f = CONFIGS[config]
     k = n - 2 * f
-    path = shared_path(config)
+    on_path = shared_path(config)
     durs = []
-    rows = list(csv.DictReader(open(path)))
+    rows = list(csv.DictReader(read_lines(path)))
     if before:
         cut = min((int(r["Start_Timestamp"]) for r in rows if base(r["Kernel_Name"]) == before), default=None)
         if cut is not None:
@@ -71,7 +95,7 @@ def summarize(path, config, inst, last, before=None):
     for r in rows:
         grid = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6  # ms
-        durs.append((int(r["Dispatch_Id"]), role(r["Kernel_Name"], grid, n, k, inst, path), grid, d))
+        durs.append((int(r["Dispatch_Id"]), role(r["Kernel_Name"], grid, n, k, inst, on_path), grid, d))
     # one role may run on several batch sizes (the PCIe host-path measurement
     # uses small batches): the largest grid is the bench batch, others are
     # reported apart as role[grid G]
