@@ -192,3 +192,70 @@ def test_rank_timing_keys_for_a_three_rank_rehearsal(tmp_path):
             assert rec["stage_ms"] == {"enc": 1.0 + r, "leaf": 2.0}
         assert x["skew"] == {"elapsed_min_s": 0.5, "elapsed_max_s": 1.0, "slowest_rank": 2, "fastest_rank": 0,
                              "max_over_min": 2.0}
+
+
+class _Ctx:
+    """What bench.report reads of a Context, without a GPU."""
+    codec = "fft"
+
+    def __init__(self, form):
+        self._form = form
+
+    def verify_form(self, S):
+        return self._form
+
+
+def _report(config, pipe=True):
+    import argparse
+    import numpy as np
+    import bench
+    n, f, B, I, _ = bench.CONFIGS[config]
+    k, d = n - 2 * f, max(1, (n - 1).bit_length())
+    S = (B + k - 1) // k
+    rng = np.random.default_rng(0)
+    present = np.zeros((I, n), np.uint8)
+    corrupt = np.full(I, -1, np.int32)
+    for i in range(I):
+        present[i, rng.permutation(n)[: n - f]] = 1
+        if rng.random() < 0.1:
+            corrupt[i] = int(rng.choice(np.flatnonzero(present[i])))
+    stage = {"enc": 2.5, "leaf": 2.9, "tree": 0.13, "fault": 0.03, "verify": 3.1, "verify_rows": 2.95,
+             "verify_path": 1.8 if config == "c4" else 0.005, "check": 0.06, "decode": 2.6, "interp": 2.7,
+             "gather": 0.005}
+    if not pipe:
+        stage = {kk: v for kk, v in stage.items() if kk not in ("verify_rows", "verify_path", "check", "decode")}
+    args = argparse.Namespace(config=config, join=False, steps=10)
+    form = "shared_path" if config == "c4" else "walk"
+    return bench.report(args, _Ctx(form), I, n, k, d, S, present, corrupt, stage, None, 10 * 5.9e-3)
+
+
+def test_report_attributes_each_verify_launch_to_its_own_kernel():
+    """at C4 the receive step's verify span holds two
+    launches; the line gives each its own roofline entry with its own
+    algorithmic bytes, and where the committed PMC file of the config has the
+    kernel, traffic covers the algorithmic bytes (tests/test_profiles.py
+    checks the same on the committed bench lines)."""
+    out = _report("c4")
+    rv, rp = out["roofline_verify"], out["roofline_verify_path"]
+    assert rv["kernel"] == "sha_rx_kernel<leaves+regen>" and rp["kernel"] == "merkle_path_kernel<4>"
+    assert rv["avg_ms"] == 2.95 and rp["avg_ms"] == 1.8
+    for r in (rv, rp, out["roofline_encode"], out["roofline_decode"]):
+        if r["traffic"] is not None:
+            assert r["traffic"] >= 0.98 * r["algorithmic_bytes_per_launch"], (r["kernel"], r["traffic"])
+    c2 = _report("c2")
+    assert c2["roofline_verify"]["kernel"] == "sha_rx_kernel<verify+regen>" and c2["roofline_verify_path"] is None
+    serial = _report("c4", pipe=False)
+    assert "verify: sha_rows_kernel<leaves> + merkle_path_kernel<4>" == serial["roofline"]["kernel"] or \
+        serial["roofline"]["kernel"] in ("sha_rows_kernel<leaves>", "rs_fft_kernel<encode>")
+
+
+def test_report_prices_the_step_per_opcode_not_at_four_clocks():
+    """valu_step prices every kernel's PMC VALU count from its static ISA mix
+    (tools/isa_mix.py, profiles/isa_mix_r05.json) and, for the SHA-256
+    kernels, at the probe's dependency-limited rate; no 4-clock figure."""
+    out = _report("c2")
+    v = out["valu_step"]
+    assert v is not None and "busy_4clk" not in v
+    assert 0 < v["issue_priced_ms"] < v["chain_priced_ms"]
+    assert not v["unpriced_kernels"], v["unpriced_kernels"]
+    assert "priced" in out["roofline_verify"]["valu"] and "measured" not in out["roofline_verify"]["valu"]
