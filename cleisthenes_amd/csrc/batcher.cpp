@@ -199,7 +199,10 @@ struct rbc_batcher {
     std::thread worker;
 
     // validate lane (see the file comment)
-    static constexpr int kVBufs = 6, kVInflight = 4;
+    // six arenas, four launches in flight (the context's host slots); a due
+    // arena is sealed by time only while fewer than kVEager launches are
+    // queued or running -- beyond that it keeps filling until it is full
+    static constexpr int kVBufs = 6, kVInflight = 4, kVEager = 2;
     int v_max_msgs = 65536;
     size_t v_max_bytes = (size_t)256 << 20;
     int bslot = 32;
@@ -556,14 +559,15 @@ void rbc_batcher::v_complete(VBuf *B) {
 }
 
 // Lane launcher: seal the open arena when its first message has waited
-// max_wait_us and a launch slot is free (under load the arena keeps filling
-// while kVInflight launches run: fewer, larger launches), and launch sealed
-// arenas whose copies are complete, strictly in generation order.
+// max_wait_us and fewer than kVEager launches are queued or running (under
+// load the arena keeps filling until full: each launch pays the SHA chain's
+// fixed ~1 ms latency, so fewer, larger launches carry more per unit time),
+// and launch sealed arenas whose copies are complete, in generation order.
 void rbc_batcher::v_run() {
     std::unique_lock<std::mutex> lk(vmu);
     for (;;) {
         const auto now = std::chrono::steady_clock::now();
-        const bool slot_free = (int)(v_flight.size() + v_sealed.size()) < kVInflight;
+        const bool slot_free = (int)(v_flight.size() + v_sealed.size()) < kVEager;
         VBuf *due = nullptr;
         std::chrono::steady_clock::time_point wake{};
         v_spin.lock();

@@ -86,6 +86,13 @@ struct Ws {
     // branches were verified against (two slots: cur and prev), and the
     // instances handed to the full recheck
     DevBuf vroot[2], need_full;
+    // receive step's list counters (16 B each): V[2] the compaction of cur,
+    // R[2] cur's regen list (decode) / prev's (hashing); parity flips per
+    // call.  One lane of the hashing launch zeroes the next users' counters
+    // (no memset launches on the receiver stream); v_clean tracks V[] on the host.
+    DevBuf rxcnt;
+    int rx_par = 0;
+    bool rxcnt_init = false, v_clean[2] = {true, true};
     int rx_vslot = 0;           // slot of the pending batch's verified roots
     bool rx_vreuse = false;     // ... kept (the recheck mode when it was verified was REUSE)
     // fork the join onto an aux stream (device API); host-API slots keep one
@@ -103,7 +110,7 @@ struct Ws {
     }
     void release() {
         for (DevBuf *b : {&used, &regen, &dmat, &nmiss, &flags, &list, &counter, &rcount, &cls, &vleaves, &vlist,
-                          &vroot[0], &vroot[1], &need_full})
+                          &vroot[0], &vroot[1], &need_full, &rxcnt})
             b->release();
         if (aux) (void)hipStreamDestroy(aux);
         if (ev_fork) (void)hipEventDestroy(ev_fork);
@@ -446,10 +453,13 @@ int ensure_ws(rbc_ctx *c, Ws &w, int count) {
 // and the rows that need hashing are collected in ws_list
 int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shards, uint32_t shard_pitch,
                      const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *valid,
-                     int32_t *status, int compare = 0) {
+                     int32_t *status, int compare = 0, uint32_t *zeroed_counter = nullptr) {
     int rc = ensure_ws(c, w, count);
     if (rc) return rc;
-    if (compare) RBC_HIP(hipMemsetAsync(w.counter.p, 0, 16, st));
+    // the regen list's counter: the workspace's own (zeroed here), or one the
+    // caller's stream has already zeroed (the receive step's R[])
+    uint32_t *counter = zeroed_counter ? zeroed_counter : w.counter.as<uint32_t>();
+    if (compare && !zeroed_counter) RBC_HIP(hipMemsetAsync(counter, 0, 16, st));
     const int nr = c->n - c->k;
     PrepArgs pa{};
     pa.count = count;
@@ -470,7 +480,7 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
         pa.nmiss = w.nmiss.as<int32_t>();
         pa.flags = w.flags.as<uint32_t>();
         pa.list = w.list.as<uint32_t>();
-        pa.counter = w.counter.as<uint32_t>();
+        pa.counter = counter;
     }
     if (c->fft) {
         pa.fft = 1;
@@ -730,6 +740,25 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
     ShaArgs v{}, r{};
     v.prio = c->rx_prio;  // the launch's wave priority (also when only prev's rows are hashed)
     bool v_walk = false, v_path = false;
+    // list counters: cur's compaction V[par], cur's regen list R[par], prev's
+    // regen list R[par ^ 1] (its decode ran in the previous call, whose parity
+    // was par ^ 1); the hashing launch zeroes R[par] and V[par ^ 1]
+    RBC_HIP(w.rxcnt.ensure(64));
+    if (!w.rxcnt_init) {
+        RBC_HIP(hipMemsetAsync(w.rxcnt.p, 0, 64, st));
+        w.rxcnt_init = true;
+        w.v_clean[0] = w.v_clean[1] = true;
+    }
+    const int par = w.rx_par;
+    uint32_t *cnt = w.rxcnt.as<uint32_t>();
+    uint32_t *v_cnt = cnt + 4 * par, *v_next = cnt + 4 * (par ^ 1), *r_cnt = cnt + 8 + 4 * par,
+             *r_prev = cnt + 8 + 4 * (par ^ 1);
+    // node-reuse recheck (merkle_recheck_kernel): keep the roots cur's branches
+    // are verified against now, for cur's recheck in the next call
+    const bool reuse = c->recheck == RBC_RECHECK_REUSE && c->depth >= 1 && c->width <= 256;
+    const int cur_vslot = w.rx_vslot ^ (hp ? 1 : 0);
+    bool roots_kept = false;
+    if (hc && reuse) RBC_HIP(w.vroot[cur_vslot].ensure((size_t)cur->count * 32));
     if (hc) {
         v.count = cur->count;
         v.rows_per_inst = c->n;
@@ -749,11 +778,15 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
         v.valid = cur->valid;
         if (cur->present && c->n <= 256) {  // hash only the received shards (stage_verify)
             RBC_HIP(w.vlist.ensure((size_t)cur->count * c->n * 4 + 64));
-            uint32_t *vl = w.vlist.as<uint32_t>(), *vc = vl + (size_t)cur->count * c->n;
-            RBC_HIP(hipMemsetAsync(vc, 0, 4, st));
-            RBC_HIP(rbc_launch_compact_present(cur->present, c->n, cur->count, cur->valid, vl, vc, st, c->rx_prio));
+            uint32_t *vl = w.vlist.as<uint32_t>();
+            if (!w.v_clean[par]) RBC_HIP(hipMemsetAsync(v_cnt, 0, 4, st));  // after an error or a one-shot call
+            RBC_HIP(rbc_launch_compact_present(cur->present, c->n, cur->count, cur->valid, vl, v_cnt, st, c->rx_prio,
+                                               reuse ? cur->roots : nullptr,
+                                               reuse ? w.vroot[cur_vslot].as<uint8_t>() : nullptr));
+            w.v_clean[par] = false;
+            roots_kept = reuse;
             v.list = vl;
-            v.list_count = vc;
+            v.list_count = v_cnt;
         }
         // the shared-path verify where the branch walk is a real share (C4), as stage_verify
         v_path = shared_path_verify(c, cur->shard_lens, cur->uniform_shard_len);
@@ -771,18 +804,13 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
         r.leaves = prev->leaves;
         r.leaves_inst_pitch = (uint64_t)c->n * 32;
         r.list = w.list.as<uint32_t>();
-        r.list_count = w.counter.as<uint32_t>();
+        r.list_count = r_prev;
     }
-    // node-reuse recheck (merkle_recheck_kernel): keep the roots cur's branches
-    // are verified against now, for cur's recheck in the next call
-    const bool reuse = c->recheck == RBC_RECHECK_REUSE && c->depth >= 1 && c->width <= 256;
-    const int cur_vslot = w.rx_vslot ^ (hp ? 1 : 0);
-    if (hc && reuse) {
-        RBC_HIP(w.vroot[cur_vslot].ensure((size_t)cur->count * 32));
+    if (hc && reuse && !roots_kept)  // no compaction to carry the copy
         RBC_HIP(hipMemcpyAsync(w.vroot[cur_vslot].p, cur->roots, (size_t)cur->count * 32, hipMemcpyDeviceToDevice, st));
-    }
     if (marks && marks->hash_begin) RBC_HIP(hipEventRecord((hipEvent_t)marks->hash_begin, st));
-    RBC_HIP(rbc_launch_sha_rx(v, r, v_walk, st));
+    RBC_HIP(rbc_launch_sha_rx(v, r, v_walk, st, reinterpret_cast<uint4 *>(r_cnt), reinterpret_cast<uint4 *>(v_next)));
+    w.v_clean[par ^ 1] = true;
     if (marks && marks->rows_hashed) RBC_HIP(hipEventRecord((hipEvent_t)marks->rows_hashed, st));
     if (hc && v_path) {
         PathArgs p{};
@@ -861,7 +889,7 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
     if (hc) {
         if (marks && marks->decode_begin) RBC_HIP(hipEventRecord((hipEvent_t)marks->decode_begin, st));
         rc = stage_regenerate(c, w, st, cur->count, cur->shards, cur->shard_pitch, cur->shard_lens,
-                              cur->uniform_shard_len, cur->valid, cur->status, 1);
+                              cur->uniform_shard_len, cur->valid, cur->status, 1, r_cnt);
         if (rc) return rc;
         if (marks && marks->decoded) RBC_HIP(hipEventRecord((hipEvent_t)marks->decoded, st));
         if (cur->values_out) {  // the row-view form (values_out NULL) has no join
@@ -876,6 +904,7 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
         w.rx_vslot = cur_vslot;
         w.rx_vreuse = reuse;  // its verified roots were kept
     }
+    w.rx_par ^= 1;  // the next call reads R[par] (cur's regen list) as its prev's
     return RBC_OK;  // pj: `st` waits for prev's join + digest
 }
 

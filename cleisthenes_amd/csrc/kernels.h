@@ -219,7 +219,9 @@ hipError_t rbc_launch_gf_regen(const GfArgs &a, hipStream_t st);
 hipError_t rbc_launch_sha_rows(const ShaArgs &a, bool verify, hipStream_t st);
 // receive step: v's rows (list or all; branch walk + verdict when v_walk) and
 // r's listed regen rows in one launch (count <= 0 disables a side)
-hipError_t rbc_launch_sha_rx(const ShaArgs &v, const ShaArgs &r, bool v_walk, hipStream_t st);
+// zero0 / zero1 (nullable, 16 B each): counters one lane zeroes during the launch (receive step)
+hipError_t rbc_launch_sha_rx(const ShaArgs &v, const ShaArgs &r, bool v_walk, hipStream_t st, uint4 *zero0 = nullptr,
+                             uint4 *zero1 = nullptr);
 hipError_t rbc_launch_merkle(const MerkleArgs &a, bool check, hipStream_t st);
 hipError_t rbc_launch_merkle_path(const PathArgs &a, hipStream_t st);
 hipError_t rbc_launch_decode_prepare(const PrepArgs &a, hipStream_t st);
@@ -228,8 +230,10 @@ hipError_t rbc_launch_digest(const uint8_t *leaves, uint64_t leaves_inst_pitch, 
 hipError_t rbc_launch_join(const JoinArgs &a, hipStream_t st);
 hipError_t rbc_launch_inject_faults(uint8_t *shards, uint64_t inst_pitch, uint32_t row_pitch,
                                     const int32_t *corrupt, int count, hipStream_t st);
+// roots_src -> roots_dst (nullable): each instance's 32-B root copied on the way (receive step)
 hipError_t rbc_launch_compact_present(const uint8_t *present, int n, int count, uint8_t *valid, uint32_t *list,
-                                     uint32_t *counter, hipStream_t st, int prio = 0);
+                                     uint32_t *counter, hipStream_t st, int prio = 0,
+                                     const uint8_t *roots_src = nullptr, uint8_t *roots_dst = nullptr);
 hipError_t rbc_launch_pack_records(const uint8_t *roots, const uint8_t *digests, const int32_t *status, int count,
                                    int slots, uint8_t *out, hipStream_t st);
 hipError_t rbc_launch_fill_random(uint8_t *dst, uint64_t first_row, uint64_t rows, uint64_t pitch, uint64_t seed,

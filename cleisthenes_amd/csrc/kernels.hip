@@ -277,9 +277,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
 // t-1's regen hashing is a latency-bound tail (42 rows x 1024 instances at
 // C2 = 672 waves of 373 serial compressions for 1,024 SIMDs) and the
 // verify 1,376 waves; together they are 2,048 waves, as full as the leaves.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void sha_rx_kernel(ShaArgs v, ShaArgs r, int v_walk) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void sha_rx_kernel(ShaArgs v, ShaArgs r, int v_walk,
+                                                                                                   uint4 *zero0,
+                                                                                                   uint4 *zero1) {
     set_wave_prio(v.prio);
     int t = blockIdx.x * blockDim.x + threadIdx.x;
+    // the receive step's list counters for the NEXT list builders (this call's
+    // decode, the next call's compaction), which nothing here reads: zeroed
+    // by one lane instead of two memset launches on the receiver's stream
+    if (t == 0) {
+        if (zero0) *zero0 = make_uint4(0u, 0u, 0u, 0u);
+        if (zero1) *zero1 = make_uint4(0u, 0u, 0u, 0u);
+    }
     const int nv = v.count <= 0 ? 0 : (v.list ? (int)*v.list_count : v.count * v.rows_per_inst);
     // r's rows start at the next whole wave after v's, so every wave is all-v
     // or all-r and the choice between the two argument blocks is scalar (the
@@ -1537,7 +1546,7 @@ __global__ void inject_faults_kernel(uint8_t *shards, uint64_t inst_pitch, uint3
 constexpr int COMPACT_IPB = 16;
 __global__ __launch_bounds__(256) void compact_present_kernel(const uint8_t *present, int n, int count,
                                                               uint8_t *valid, uint32_t *list, uint32_t *counter,
-                                                              int prio) {
+                                                              int prio, const uint8_t *roots_src, uint8_t *roots_dst) {
     set_wave_prio(prio);
     __shared__ uint32_t s_cnt[COMPACT_IPB];
     __shared__ uint32_t s_base;
@@ -1559,6 +1568,12 @@ __global__ __launch_bounds__(256) void compact_present_kernel(const uint8_t *pre
             if (inst < count && pos < n && !p[q][c]) valid[(size_t)inst * n + pos] = 0;
         }
         if (lane == 0) s_cnt[4 * q + w] = (uint32_t)total;
+        // the receive step keeps the roots the branches are verified against
+        // (merkle_recheck_kernel's vroots): a copy here instead of a separate
+        // D2D copy launch on the receiver's critical path
+        if (roots_dst && inst < count && lane < 8)
+            reinterpret_cast<uint32_t *>(roots_dst)[(size_t)inst * 8 + lane] =
+                reinterpret_cast<const uint32_t *>(roots_src)[(size_t)inst * 8 + lane];
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1740,11 +1755,12 @@ __global__ __launch_bounds__(256) void gather_present_kernel(const uint8_t *host
 // launchers
 // ============================================================================
 hipError_t rbc_launch_compact_present(const uint8_t *present, int n, int count, uint8_t *valid, uint32_t *list,
-                                     uint32_t *counter, hipStream_t st, int prio) {
+                                     uint32_t *counter, hipStream_t st, int prio, const uint8_t *roots_src,
+                                     uint8_t *roots_dst) {
     if (count <= 0) return hipSuccess;
     if (n > 256) return hipErrorInvalidValue;
     hipLaunchKernelGGL(compact_present_kernel, dim3((count + COMPACT_IPB - 1) / COMPACT_IPB), dim3(256), 0, st,
-                       present, n, count, valid, list, counter, prio);
+                       present, n, count, valid, list, counter, prio, roots_src, roots_dst);
     return hipGetLastError();
 }
 
@@ -1879,10 +1895,18 @@ hipError_t rbc_launch_sha_rows(const ShaArgs &a, bool verify, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t rbc_launch_sha_rx(const ShaArgs &v, const ShaArgs &r, bool v_walk, hipStream_t st) {
+hipError_t rbc_launch_sha_rx(const ShaArgs &v, const ShaArgs &r, bool v_walk, hipStream_t st, uint4 *zero0,
+                             uint4 *zero1) {
     const long total = (v.count > 0 ? ((long)v.count * v.rows_per_inst + 63) / 64 * 64 : 0) +
                        (r.count > 0 ? (long)r.count * r.rows_per_inst : 0);
-    if (total <= 0) return hipSuccess;
+    if (total <= 0) {  // no rows: the counters still have to be zero for their next users
+        for (uint4 *z : {zero0, zero1})
+            if (z) {
+                const hipError_t e = hipMemsetAsync(z, 0, sizeof(uint4), st);
+                if (e != hipSuccess) return e;
+            }
+        return hipSuccess;
+    }
     if ((v.count > 0 && (!v.rows || (v_walk && (!v.valid || !v.roots)))) || (r.count > 0 && (!r.list || !r.list_count)))
         return hipErrorInvalidValue;
     // one-wave blocks: 4.78-4.82 ms per C2 receive step against 5.03 with
@@ -1890,7 +1914,8 @@ hipError_t rbc_launch_sha_rx(const ShaArgs &v, const ShaArgs &r, bool v_walk, hi
     // 526-531 GB/s against 477-486 (256) and 439-447 (128), C1 and C4 within
     // 3 % (tools/gpu_runs/gpu_r03y.sh)
     constexpr int tpb = 64;
-    hipLaunchKernelGGL(sha_rx_kernel, dim3((unsigned)((total + tpb - 1) / tpb)), dim3(tpb), 0, st, v, r, v_walk ? 1 : 0);
+    hipLaunchKernelGGL(sha_rx_kernel, dim3((unsigned)((total + tpb - 1) / tpb)), dim3(tpb), 0, st, v, r, v_walk ? 1 : 0,
+                       zero0, zero1);
     return hipGetLastError();
 }
 
