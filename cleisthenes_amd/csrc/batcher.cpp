@@ -126,19 +126,27 @@ struct VBuf {
     uint8_t *roots = nullptr, *br = nullptr, *idx = nullptr, *ok = nullptr, *shape = nullptr;
     std::vector<int *> out;
     int cap = 0;                     // messages the meta block holds
-    // reservation state, under the lane's spinlock while the arena is open;
-    // final once it is sealed (v_open no longer points at it)
-    int count = 0;                   // reserved slots
-    size_t bytes = 0;                // reserved arena bytes
-    // reserved slots not yet copied, plus kSealed once sealed: == kSealed
-    // means ready to launch.  Only the returned values of its atomic updates
-    // are used, so a caller touches nothing of the arena after its last one
-    // (by then the arena may already be launched, completed and reopened).
+    // Copies done, then at seal time + (kSealed - count): == kSealed exactly
+    // when the arena is sealed and every reserved slot copied.  One atomic
+    // add per message (the caller's, after its copy); only the returned values
+    // are used, so a caller touches nothing of the arena after it (by then the
+    // arena may already be launched, completed and reopened).
     static constexpr int64_t kSealed = (int64_t)1 << 40;
-    std::atomic<int64_t> pend{0};
-    uint64_t gen = 0;                // launch generation (tickets complete in this order)
+    alignas(64) std::atomic<int64_t> pend{0};
+    // Reservations: ONE atomic add per message of (1 << 40 | bytes) to `word`
+    // (slot = old count, offset = old bytes).  A reservation whose slot is
+    // < cap but whose bytes do not fit leaves a hole (its slot is launched as
+    // an empty message).  Sealing adds kBump to the count so later adds fail;
+    // count / bytes below are the final values the seal takes from `word`.
+    static constexpr uint64_t kCountOne = (uint64_t)1 << 40, kBytesMask = kCountOne - 1;
+    static constexpr uint64_t kBump = (uint64_t)1 << 62;
+    alignas(64) std::atomic<uint64_t> word{0};
+    alignas(64) int count = 0;       // slots launched (final at the seal)
+    size_t bytes = 0;                // arena bytes launched (final at the seal)
+    uint64_t seen = 0;               // the launcher's last sample of the slot count (quiet detection)
+    std::chrono::steady_clock::time_point t0, t_seen;  // opening / when `seen` last changed
+    alignas(64) uint64_t gen = 0;    // launch generation (tickets complete in this order)
     State state = FREE;              // under vmu
-    std::chrono::steady_clock::time_point t0;
     uint64_t ticket = 0;
     int rc = RBC_OK;
     bool layout(int msgs, int bslot) {  // the meta block for `msgs` messages
@@ -156,18 +164,6 @@ struct VBuf {
         out.assign(msgs, nullptr);
         return true;
     }
-};
-// a test-and-test-and-set spinlock for the reservation's few instructions:
-// the lane takes one per validateMessage from every client thread
-struct Spin {
-    std::atomic<bool> f{false};
-    void lock() {
-        for (;;) {
-            if (!f.exchange(true, std::memory_order_acquire)) return;
-            while (f.load(std::memory_order_relaxed)) __builtin_ia32_pause();
-        }
-    }
-    void unlock() { f.store(false, std::memory_order_release); }
 };
 constexpr uint64_t kVTicket = 1ull << 63;  // validate-lane tickets: kVTicket | gen << 20 | slot
 constexpr int kVSlotBits = 20;
@@ -199,16 +195,17 @@ struct rbc_batcher {
     std::thread worker;
 
     // validate lane (see the file comment)
-    // six arenas, four launches in flight (the context's host slots); a due
-    // arena is sealed by time only while fewer than kVEager launches are
-    // queued or running -- beyond that it keeps filling until it is full
-    static constexpr int kVBufs = 6, kVInflight = 4, kVEager = 2;
+    // six arenas, four launches in flight (the context's host slots); with a
+    // launch running, an arena is sealed once it holds kVTarget bytes (each
+    // launch pays the SHA chain's fixed ~1 ms: 16 MiB arenas four deep keep
+    // the H2D copy engine, ~55 GB/s, busy) or when arrivals pause
+    static constexpr int kVBufs = 6, kVInflight = 4;
+    static constexpr size_t kVTarget = (size_t)16 << 20;
     int v_max_msgs = 65536;
     size_t v_max_bytes = (size_t)256 << 20;
     int bslot = 32;
-    Spin v_spin;                            // v_open and the open arena's count / bytes
-    VBuf *v_open = nullptr;
-    std::mutex vmu;                         // everything below
+    alignas(64) std::atomic<VBuf *> v_open{nullptr};  // the arena reservations go to
+    alignas(64) std::mutex vmu;             // everything below (own cache line: off the spinlock's)
     std::condition_variable v_work;         // launcher: a seal, a finished copy, a free launch slot
     std::condition_variable v_fl;           // completer: a launch
     std::condition_variable v_free;         // clients: a free arena
@@ -223,6 +220,7 @@ struct rbc_batcher {
     bool v_stop = false, v_launcher_done = false;
     std::thread v_worker, v_completer;
     int v_reserve(size_t need, VBuf **B, int *slot, size_t *off);
+    bool v_seal(VBuf *B);
     void v_push_sealed(VBuf *B);
     void v_launch(VBuf *B);
     void v_complete(VBuf *B);
@@ -455,45 +453,67 @@ void rbc_batcher::run() {
 
 // ---- validate lane ----------------------------------------------------------
 
-// Hand a sealed arena (v_open no longer points at it, so its count and bytes
-// are final) to the launcher, keeping v_sealed in generation order.
+// Seal B if it is still the open arena: take it out of v_open, fix its final
+// count / bytes with one add of kBump (every later reservation fails and
+// retries), credit the slots nobody will copy into pend, and hand it to the
+// launcher in generation order.  False if another caller sealed it first.
+bool rbc_batcher::v_seal(VBuf *B) {
+    VBuf *expect = B;
+    if (!v_open.compare_exchange_strong(expect, nullptr)) return false;
+    const uint64_t w = B->word.fetch_add(VBuf::kBump);
+    B->count = (int)std::min<uint64_t>(w >> 40, (uint64_t)B->cap);
+    B->bytes = std::min<uint64_t>(w & VBuf::kBytesMask, B->arena.cap);
+    v_push_sealed(B);
+    return true;
+}
+
 void rbc_batcher::v_push_sealed(VBuf *B) {
     std::lock_guard<std::mutex> lk(vmu);
     B->state = VBuf::SEALED;
-    B->pend.fetch_add(VBuf::kSealed);
+    B->pend.fetch_add(VBuf::kSealed - B->count);
     auto it = v_sealed.begin();
     while (it != v_sealed.end() && (*it)->gen < B->gen) ++it;
     v_sealed.insert(it, B);
     v_work.notify_one();
 }
 
-// A slot for one message of `need` arena bytes: the open arena's next slot
-// (spinlock only), sealing it when full; opening a free arena under vmu when
-// none is open.
+// A slot for one message of `need` arena bytes: one atomic add on the open
+// arena; opening a free arena under vmu (this message in slot 0) when none is.
 int rbc_batcher::v_reserve(size_t need, VBuf **out, int *slot, size_t *off) {
     for (;;) {
-        v_spin.lock();
-        VBuf *B = v_open;
-        if (B && B->count < B->cap && B->bytes + need <= B->arena.cap) {
-            *out = B;
-            *slot = B->count++;
-            *off = B->bytes;
-            B->bytes += need;
-            B->pend.fetch_add(1);
-            const bool full = B->count == B->cap;
-            if (full) v_open = nullptr;
-            v_spin.unlock();
-            if (full) v_push_sealed(B);
-            return RBC_OK;
-        }
-        if (B) {  // no room for this message: seal (an empty arena goes through as a no-op)
-            v_open = nullptr;
-            v_spin.unlock();
-            v_push_sealed(B);
+        VBuf *B = v_open.load();
+        if (B) {
+            const uint64_t w = B->word.fetch_add(VBuf::kCountOne | need);
+            const uint64_t oc = w >> 40, ob = w & VBuf::kBytesMask;
+            if (oc >= (uint64_t)B->cap) {  // sealed, or full and being sealed: the next arena
+                __builtin_ia32_pause();
+                continue;
+            }
+            if (ob + need <= B->arena.cap) {
+                *out = B;
+                *slot = (int)oc;
+                *off = ob;
+                if (oc + 1 == (uint64_t)B->cap) v_seal(B);  // the last slot
+                else if (ob < kVTarget && ob + need >= kVTarget) v_work.notify_one();  // a hint; the launcher also polls
+                return RBC_OK;
+            }
+            // no room for these bytes: slot oc is launched as an empty message
+            B->out[oc] = nullptr;
+            B->offs[oc] = 0;
+            B->lens[oc] = 1;
+            B->idx[oc] = 0;
+            B->shape[oc] = 0;
+            memset(B->br + (size_t)oc * bslot, 0, bslot);
+            memset(B->roots + oc * 32, 0, 32);
+            if (B->pend.fetch_add(1) + 1 == VBuf::kSealed) {
+                std::lock_guard<std::mutex> lk(vmu);
+                v_work.notify_one();
+            }
+            v_seal(B);
             continue;
         }
-        v_spin.unlock();
         std::unique_lock<std::mutex> lk(vmu);
+        if (v_open.load()) continue;  // another caller opened one meanwhile
         VBuf *f = nullptr;
         for (;;) {
             for (auto &x : vb)
@@ -502,32 +522,36 @@ int rbc_batcher::v_reserve(size_t need, VBuf **out, int *slot, size_t *off) {
             v_free.wait(lk);  // every arena is filling, sealed or in flight
         }
         if (!f) return RBC_ERR_INVALID_ARG;  // the batcher is being destroyed
+        if (v_open.load()) continue;
+        // an arena's buffers are allocated once, before it is first published,
+        // and never moved (a caller holding a stale arena pointer only ever
+        // reads them); messages larger than an arena take the direct path
         if (f->cap != v_max_msgs && !f->layout(v_max_msgs, bslot)) return RBC_ERR_DEVICE;
-        if (!f->arena.ensure(std::max(v_max_bytes, need))) return RBC_ERR_DEVICE;
-        v_spin.lock();
-        if (v_open) {  // another caller opened one meanwhile: reserve there
-            v_spin.unlock();
-            continue;
-        }
+        if (!f->arena.ensure(v_max_bytes)) return RBC_ERR_DEVICE;
         // open f with this message in slot 0, so the launcher, woken here
         // under vmu, always finds a non-empty arena to time
         f->state = VBuf::OPEN;
         f->gen = v_next_gen++;
-        f->count = 1;
-        f->bytes = need;
-        f->pend.store(1);
+        f->count = 0;
+        f->bytes = 0;
+        f->pend.store(0);
+        f->word.store(VBuf::kCountOne | need);
         f->rc = RBC_OK;
         f->ticket = 0;
-        f->t0 = std::chrono::steady_clock::now();  // max_wait runs from the first message
-        const bool full = f->cap == 1;
-        v_open = full ? nullptr : f;
-        v_spin.unlock();
+        f->t0 = f->t_seen = std::chrono::steady_clock::now();  // max_wait runs from the first message
+        f->seen = 1;
         *out = f;
         *slot = 0;
         *off = 0;
+        if (f->cap == 1) {  // full at once
+            f->count = 1;
+            f->bytes = need;
+            lk.unlock();
+            v_push_sealed(f);
+            return RBC_OK;
+        }
+        v_open.store(f);
         v_work.notify_one();
-        lk.unlock();
-        if (full) v_push_sealed(f);
         return RBC_OK;
     }
 }
@@ -542,15 +566,20 @@ void rbc_batcher::v_launch(VBuf *B) {
 void rbc_batcher::v_complete(VBuf *B) {
     int rc = B->rc;
     if (!rc && B->ticket) rc = rbc_wait(ctx, B->ticket);
-    for (int i = 0; i < B->count; ++i) *B->out[i] = (!rc && B->shape[i]) ? B->ok[i] : 0;
+    int real = 0;
+    for (int i = 0; i < B->count; ++i)
+        if (B->out[i]) {  // holes have no caller
+            *B->out[i] = (!rc && B->shape[i]) ? B->ok[i] : 0;
+            ++real;
+        }
     std::lock_guard<std::mutex> lk(vmu);
     if (rc) {
         v_failed[B->gen] = rc;
         v_any_failed.store(true);
     }
     v_done_gen.store(B->gen);
-    v_batches += B->count > 0;
-    v_requests += B->count;
+    v_batches += real > 0;
+    v_requests += real;
     v_flight.pop_front();  // B: the completer takes launches in order
     B->state = VBuf::FREE;
     v_free.notify_all();
@@ -559,35 +588,39 @@ void rbc_batcher::v_complete(VBuf *B) {
 }
 
 // Lane launcher: seal the open arena when its first message has waited
-// max_wait_us and fewer than kVEager launches are queued or running (under
-// load the arena keeps filling until full: each launch pays the SHA chain's
-// fixed ~1 ms latency, so fewer, larger launches carry more per unit time),
-// and launch sealed arenas whose copies are complete, in generation order.
+// max_wait_us and the lane is idle; with launches running, once it holds
+// kVTarget bytes, or when no message has arrived for max_wait_us either (an
+// arena sealed right after a completion, before the callers refill it, would
+// launch only the stragglers).  Launch sealed arenas whose copies are
+// complete, in generation order, at most kVInflight deep.
 void rbc_batcher::v_run() {
     std::unique_lock<std::mutex> lk(vmu);
     for (;;) {
         const auto now = std::chrono::steady_clock::now();
-        const bool slot_free = (int)(v_flight.size() + v_sealed.size()) < kVEager;
-        VBuf *due = nullptr;
+        const int queued = (int)(v_flight.size() + v_sealed.size());
+        const bool slot_free = queued < kVInflight;
+        const auto mw = std::chrono::microseconds(max_wait_us);
         std::chrono::steady_clock::time_point wake{};
-        v_spin.lock();
-        if (v_open && v_open->count > 0) {
-            wake = v_open->t0 + std::chrono::microseconds(max_wait_us);
-            if (v_stop || (slot_free && wake <= now)) {
-                due = v_open;
-                v_open = nullptr;
+        VBuf *O = v_open.load();
+        bool open_pending = false;
+        if (O) {
+            const uint64_t w = O->word.load();
+            const uint64_t cnt = std::min<uint64_t>(w >> 40, (uint64_t)O->cap), bytes = w & VBuf::kBytesMask;
+            // arrivals are sampled here (no per-message timestamp): `seen` moves when the count has
+            if (cnt != O->seen) {
+                O->seen = cnt;
+                O->t_seen = now;
             }
-        } else if (v_open && v_stop) {  // an empty arena at shutdown: back to the free list
-            v_open->state = VBuf::FREE;
-            v_open = nullptr;
-        }
-        const bool open_pending = v_open && v_open->count > 0;
-        v_spin.unlock();
-        if (due) {
-            lk.unlock();
-            v_push_sealed(due);
-            lk.lock();
-            continue;
+            // idle lane: max_wait from the first message; busy: also max_wait of quiet, or kVTarget bytes
+            wake = queued == 0 ? O->t0 + mw : std::max(O->t0, O->t_seen) + mw;
+            const bool big = bytes >= kVTarget && O->t0 + mw <= now;
+            if (v_stop || (slot_free && (wake <= now || big))) {
+                lk.unlock();
+                v_seal(O);
+                lk.lock();
+                continue;
+            }
+            open_pending = true;
         }
         VBuf *F = v_sealed.empty() ? nullptr : v_sealed.front();
         if (F && F->gen == v_next_launch && F->pend.load() == VBuf::kSealed && (int)v_flight.size() < kVInflight) {
@@ -601,7 +634,7 @@ void rbc_batcher::v_run() {
             v_fl.notify_one();
             continue;
         }
-        if (v_stop && !open_pending && v_sealed.empty()) {
+        if (v_stop && !v_open.load() && v_sealed.empty()) {
             v_launcher_done = true;  // everything launched: the completer drains v_flight and exits
             v_fl.notify_one();
             return;
@@ -719,6 +752,18 @@ int rbc_batcher_validate(rbc_batcher *b, const uint8_t *root, const uint8_t *bra
     const size_t want = (size_t)32 * (d - (empty0 ? 1 : 0));
     const bool shape_ok = index < (uint32_t)n && branch_len == want && shard_len != 0 && shard && (!want || branch);
     const size_t need = shape_ok ? (shard_len + 63) / 64 * 64 : 64;
+    if (need > b->v_max_bytes) {  // larger than an arena: validated on this thread, complete at return
+        uint8_t ok = 0;
+        const uint8_t *sh = shard, *bp = branch, *rp = root;
+        const int rc = rbc_validate_batch(b->ctx, 1, &sh, &shard_len, &index, &bp, &branch_len, &rp, &ok, nullptr);
+        if (rc) return rc;
+        *ok_out = ok;
+        *ticket = kVTicket | 1;  // generation 0: already complete
+        std::lock_guard<std::mutex> lk(b->vmu);
+        b->v_batches++;
+        b->v_requests++;
+        return RBC_OK;
+    }
     VBuf *B = nullptr;
     int slot = 0;
     size_t off = 0;
@@ -754,7 +799,7 @@ int rbc_batcher_validate(rbc_batcher *b, const uint8_t *root, const uint8_t *bra
     *ticket = kVTicket | (B->gen << kVSlotBits) | (uint64_t)slot;  // gen is stable until this slot completes
     // the last copy of a sealed arena wakes the launcher (either it sees
     // this copy when it checks, or this update sees the seal)
-    if (B->pend.fetch_sub(1) - 1 == VBuf::kSealed) {
+    if (B->pend.fetch_add(1) + 1 == VBuf::kSealed) {
         std::lock_guard<std::mutex> lk(b->vmu);
         b->v_work.notify_one();
     }
@@ -782,7 +827,8 @@ int rbc_batcher_wait(rbc_batcher *b, uint64_t ticket) {
     if (!b) return RBC_ERR_INVALID_ARG;
     if (ticket & kVTicket) {  // validate lane: complete when its arena's generation is
         const uint64_t gen = (ticket & ~kVTicket) >> kVSlotBits;
-        if (gen > 0 && b->v_done_gen.load() >= gen && !b->v_any_failed.load()) return RBC_OK;  // no lock
+        if (gen == 0) return RBC_OK;  // validated at submission (larger than an arena)
+        if (b->v_done_gen.load() >= gen && !b->v_any_failed.load()) return RBC_OK;  // no lock
         std::unique_lock<std::mutex> lk(b->vmu);
         if (gen == 0 || gen >= b->v_next_gen) return RBC_ERR_INVALID_ARG;
         b->v_done.wait(lk, [&] { return b->v_done_gen.load() >= gen; });
@@ -807,8 +853,8 @@ int rbc_batcher_poll(rbc_batcher *b, uint64_t ticket, int *done_out) {
     if (ticket & kVTicket) {
         const uint64_t gen = (ticket & ~kVTicket) >> kVSlotBits;
         std::lock_guard<std::mutex> lk(b->vmu);
-        if (gen == 0 || gen >= b->v_next_gen) return RBC_ERR_INVALID_ARG;
-        *done_out = b->v_done_gen.load() >= gen;
+        if (gen >= b->v_next_gen) return RBC_ERR_INVALID_ARG;
+        *done_out = gen == 0 || b->v_done_gen.load() >= gen;
         return RBC_OK;
     }
     if (ticket == 0 || ticket >= b->next.load()) return RBC_ERR_INVALID_ARG;

@@ -133,6 +133,11 @@ struct Slot {
     Ws ws;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
+    // recorded after the submission's kernels, before its deferred D2H: a
+    // waiter enqueues the D2H only once the kernels are done, so the copy
+    // engine (one queue, served in enqueue order) never holds a later
+    // submission's H2D behind a D2H that still waits on kernels
+    hipEvent_t kdone = nullptr;
     uint64_t ticket = 0;
     bool busy = false;
     std::function<int()> finish;
@@ -150,8 +155,10 @@ struct Slot {
         ws.release();
         if (stream) (void)hipStreamDestroy(stream);
         if (done) (void)hipEventDestroy(done);
+        if (kdone) (void)hipEventDestroy(kdone);
         stream = nullptr;
         done = nullptr;
+        kdone = nullptr;
     }
 };
 
@@ -1349,7 +1356,12 @@ Slot *acquire_slot(rbc_ctx *c) {
     if ((int)c->slots.size() < kHostSlots) {
         auto sl = std::make_unique<Slot>();
         if (hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&sl->done, hipEventDisableTiming) != hipSuccess || !sl->ws.init()) {
+            // blocking-sync events: a host-API waiter (the batcher's completer, a
+            // goroutine's cgo call) sleeps instead of spinning a core the
+            // submitting threads need for their staging copies
+            hipEventCreateWithFlags(&sl->done, hipEventDisableTiming | hipEventBlockingSync) != hipSuccess ||
+            hipEventCreateWithFlags(&sl->kdone, hipEventDisableTiming | hipEventBlockingSync) != hipSuccess ||
+            !sl->ws.init()) {
             sl->release();
             return nullptr;
         }
@@ -1375,6 +1387,10 @@ int submit(rbc_ctx *c, Slot &s, uint64_t *ticket, std::function<int()> finish,
         if (o.get() != &s && o->busy) flush_d2h(*o);
     s.d2h_rc = 0;
     if (d2h && ticket) {
+        if (hipEventRecord(s.kdone, s.stream) != hipSuccess) {
+            s.finish = nullptr;
+            return RBC_ERR_DEVICE;
+        }
         s.d2h = std::move(d2h);
     } else {
         const int rc = d2h ? d2h() : RBC_OK;
@@ -1895,18 +1911,32 @@ int rbc_wait(rbc_ctx *c, uint64_t ticket) {
     // other threads keep submitting (the batcher's validate lane launches
     // while its completer waits); then retire it under the lock -- unless
     // another thread retired it meanwhile (its status is then in `retired`).
-    hipEvent_t ev = nullptr;
-    for (auto &sl : c->slots)
-        if (sl->busy && sl->ticket == ticket) {
-            flush_d2h(*sl);
-            ev = sl->done;
-        }
-    if (ev) {
-        lk.unlock();
-        (void)hipEventSynchronize(ev);  // a reused slot's later event only waits longer
-        lk.lock();
+    // A D2H still deferred is enqueued only after the kernels it follows are
+    // done (Slot::kdone): enqueued earlier it would wait on them at the head
+    // of the copy engine's queue, in front of the next submission's H2D.
+    auto find = [&]() -> Slot * {
         for (auto &sl : c->slots)
-            if (sl->busy && sl->ticket == ticket) return retire(c, *sl);
+            if (sl->busy && sl->ticket == ticket) return sl.get();
+        return nullptr;
+    };
+    // (an event of a slot retired and reused meanwhile only waits longer; the
+    // ticket's status is then in `retired`)
+    if (Slot *s = find()) {
+        if (s->d2h) {
+            const hipEvent_t kd = s->kdone;
+            lk.unlock();
+            (void)hipEventSynchronize(kd);
+            lk.lock();
+            s = find();
+            if (s) flush_d2h(*s);
+        }
+        if (s) {
+            const hipEvent_t ev = s->done;
+            lk.unlock();
+            (void)hipEventSynchronize(ev);
+            lk.lock();
+            if ((s = find())) return retire(c, *s);
+        }
     }
     auto it = c->retired.find(ticket);
     if (it == c->retired.end()) return RBC_OK;  // completed and already collected
@@ -1922,6 +1952,13 @@ int rbc_poll(rbc_ctx *c, uint64_t ticket, int *done) {
     *done = 1;
     for (auto &sl : c->slots)
         if (sl->busy && sl->ticket == ticket) {
+            if (sl->d2h) {  // kernels still running: not done, and the D2H stays deferred (Slot::kdone)
+                const hipError_t k = hipEventQuery(sl->kdone);
+                if (k == hipErrorNotReady) {
+                    *done = 0;
+                    return RBC_OK;
+                }
+            }
             flush_d2h(*sl);  // nothing completes while its copies are unqueued
             const hipError_t q = hipEventQuery(sl->done);
             if (q == hipErrorNotReady) {

@@ -217,7 +217,9 @@ hipError_t rbc_launch_sha_rows(const ShaArgs &a, bool verify, hipStream_t) {
     if (verify && a.valid) touch(a.valid, (size_t)a.count * (a.per_message ? 1 : a.n));
     return hipSuccess;
 }
-hipError_t rbc_launch_sha_rx(const ShaArgs &v, const ShaArgs &r, bool v_walk, hipStream_t) {
+hipError_t rbc_launch_sha_rx(const ShaArgs &v, const ShaArgs &r, bool v_walk, hipStream_t, uint4 *zero0, uint4 *zero1) {
+    for (uint4 *z : {zero0, zero1})
+        if (z) touch(z, sizeof(uint4));
     if (v.count > 0) {
         touch(v.leaves, (size_t)v.count * v.leaves_inst_pitch);
         if (v_walk) touch(v.valid, (size_t)v.count * v.n);
@@ -278,9 +280,14 @@ hipError_t rbc_launch_inject_faults(uint8_t *shards, uint64_t inst_pitch, uint32
     return hipSuccess;
 }
 hipError_t rbc_launch_compact_present(const uint8_t *present, int n, int count, uint8_t *valid, uint32_t *list,
-                                      uint32_t *counter, hipStream_t, int) {
+                                      uint32_t *counter, hipStream_t, int, const uint8_t *roots_src,
+                                      uint8_t *roots_dst) {
     if (count <= 0) return hipSuccess;
     peek(present, (size_t)count * n - 1);
+    if (roots_dst) {
+        peek(roots_src, (size_t)count * 32 - 1);
+        touch(roots_dst, (size_t)count * 32);
+    }
     touch(valid, (size_t)count * n);
     touch(list, (size_t)count * n * 4);
     touch(counter, 4);

@@ -209,7 +209,10 @@ int validate_sweep(int argc, char **argv) {
         double dt = 0;
         uint64_t nb0 = 0, nr0 = 0, nb = 0, nr = 0;
         std::atomic<int> bad{0};
+        std::atomic<long> ns_submit{0}, ns_wait{0};  // client time inside validate / wait (second pass)
         for (int pass = 0; pass < 2; ++pass) {  // the second pass (arenas allocated, device buffers grown) counts
+            ns_submit = 0;
+            ns_wait = 0;
             std::atomic<int> next{0};
             bad = 0;
             rbc_batcher_stats(b, &nb0, &nr0);
@@ -219,9 +222,13 @@ int validate_sweep(int argc, char **argv) {
                 th.emplace_back([&] {
                     std::vector<std::pair<uint64_t, int>> win;  // (ticket, message) oldest first
                     size_t head = 0;
+                    long my_sub = 0, my_wait = 0;
                     auto drain_one = [&] {
                         const auto [tk, e] = win[head++];
+                        const auto w0 = std::chrono::steady_clock::now();
                         if (rbc_batcher_wait(b, tk) != RBC_OK) ++bad;
+                        my_wait += std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                       std::chrono::steady_clock::now() - w0).count();
                         const int want = (e % 97) != 13;
                         if (ok[e] != want) ++bad;
                     };
@@ -230,12 +237,17 @@ int validate_sweep(int argc, char **argv) {
                         const int i = (e / (n - f)) % I, j = e % (n - f);
                         const uint8_t *rt = ((e % 97) == 13 ? bad_roots.data() : roots.data()) + (size_t)i * 32;
                         uint64_t tk;
+                        const auto s0 = std::chrono::steady_clock::now();
                         CK(rbc_batcher_validate(b, rt, br.data() + ((size_t)i * n + j) * d * 32, d * 32,
                                                 shards.data() + ((size_t)i * n + j) * S, S, (uint32_t)j, &ok[e], &tk));
+                        my_sub += std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                      std::chrono::steady_clock::now() - s0).count();
                         win.emplace_back(tk, e);
                         if ((int)(win.size() - head) >= W) drain_one();
                     }
                     while (head < win.size()) drain_one();
+                    ns_submit += my_sub;
+                    ns_wait += my_wait;
                 });
             for (auto &t : th) t.join();
             dt = now() - t0;
@@ -245,9 +257,11 @@ int validate_sweep(int argc, char **argv) {
         const double launches = (double)(nb - nb0);
         printf("{\"phase\": \"validate\", \"outstanding\": %d, \"threads\": %d, \"window\": %d, \"messages\": %d, "
                "\"shard_bytes\": %zu, \"max_wait_us\": %d, \"seconds\": %.4f, \"msg_per_s\": %.0f, \"GBps\": %.3f, "
-               "\"launches\": %.0f, \"msgs_per_launch\": %.1f, \"failed\": %d}\n",
+               "\"launches\": %.0f, \"msgs_per_launch\": %.1f, \"failed\": %d, \"client_us_per_msg\": "
+               "{\"submit\": %.2f, \"wait\": %.2f}}\n",
                L, T, W, M, S, WAIT, dt, M / dt, (double)M * S / dt / 1e9, launches,
-               launches ? (double)(nr - nr0) / launches : 0.0, bad.load());
+               launches ? (double)(nr - nr0) / launches : 0.0, bad.load(), ns_submit.load() / 1e3 / M,
+               ns_wait.load() / 1e3 / M);
         fflush(stdout);
         fails += bad.load();
     }
