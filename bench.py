@@ -99,6 +99,8 @@ def parse_args(argv):
     ap.add_argument("--decode-prio", default="",
                     help="gemv,reencode levels of interpolate's GF transforms: c (commit level), r (receive "
                          "level) or 0..3 (default per config, DECODE_PRIO; serial: commit level)")
+    ap.add_argument("--regen", default="auto", choices=("auto", "inline", "fork"),
+                    help="where the receive step hashes the regenerated rows (rbc_ctx_set_regen_hashing)")
     ap.add_argument("--hbm-budget", type=float, default=0,
                     help="bytes of HBM this rank may use (default: free device memory / ranks sharing the device)")
     ap.add_argument("--shard-align", type=int, default=128,
@@ -212,6 +214,7 @@ def run(args, world, rank, local_rank, wd, out):
     gv, rv = (lv[x] if x in lv else int(x)
               for x in (args.decode_prio or (DECODE_PRIO[args.config] if pipe else "c,c")).split(","))
     ctx.set_decode_priority(gv, rv)
+    ctx.set_regen_hashing(args.regen)
     stream = ca.Stream(dev)
     mb = lambda x: ca.DeviceBuffer(x, device=dev)  # noqa: E731
     # ---- synthetic inputs: values on the device (the global instance id
@@ -486,6 +489,7 @@ def run(args, world, rank, local_rank, wd, out):
                                   + (", RCCL all-gather of {root,digest} records" if gather else ""),
                    "gf_codec": ctx.codec,
                    "wave_priority": {"commit": tx, "receive": rx, "decode_gemv": gv, "decode_reencode": rv},
+                   "regen_hashing": args.regen,
                    "value_form": "joined (k*S bytes per instance)" if args.join else
                                  "row view (the k data rows of the shard set, no join)",
                    "faults_on": args.faults_on, "hbm_plan": plan,

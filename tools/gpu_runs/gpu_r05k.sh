@@ -1,6 +1,7 @@
 # Round 5 evidence: GPU suite, smoke, the default bench twice (with the
 # batcher key), C1 / C3 / C4 lines, C3 at 8,192 on one GPU, and the rocprof
-# kernel trace + stats of exactly `python bench.py`.
+# kernel trace + stats of exactly `python bench.py`; A/B of the forked
+# regen hashing (rbc_ctx_set_regen_hashing) at C4, C2, C1.
 set -o pipefail
 O=gpurun_out/r05k; mkdir -p $O
 R=$(pwd)
@@ -17,6 +18,15 @@ done
 for cfg in c1 c3 c4; do
   timeout -k 10 300 python bench.py --config $cfg --steps 60 --no-joined-leg $Q > $O/$cfg.json 2> $O/$cfg.err || { echo BENCHFAIL $cfg; tail -20 $O/$cfg.err; exit 1; }
   line $O/$cfg.json $cfg
+done
+# A/B: the regenerated rows hashed on the aux stream (RBC_REGEN_FORK) against inline
+for rep in 1 2; do
+  for cfg in c4 c2 c1; do
+    for rg in inline fork; do
+      timeout -k 10 300 python bench.py --config $cfg --steps 60 --no-joined-leg --regen $rg $Q > $O/ab_${cfg}_${rg}_$rep.json 2> $O/ab_${cfg}_${rg}_$rep.err || { echo BENCHFAIL ab $cfg $rg; tail -20 $O/ab_${cfg}_${rg}_$rep.err; exit 1; }
+      line $O/ab_${cfg}_${rg}_$rep.json ab_${cfg}_${rg}_$rep
+    done
+  done
 done
 timeout -k 10 600 python bench.py --config c3 --total-instances 8192 --steps 4 --warmup 1 --no-joined-leg $Q > $O/c3_8192.json 2> $O/c3_8192.err || { echo BENCHFAIL c3_8192; tail -20 $O/c3_8192.err; exit 1; }
 line $O/c3_8192.json c3_8192
