@@ -7,6 +7,8 @@ O=gpurun_out/r05k; mkdir -p $O
 R=$(pwd)
 Q="--no-cpu-baseline --no-pcie --no-batcher"
 line() { python -c "import json,sys; d=json.load(open(sys.argv[1])); v=d.get('valu_step') or {}; print(sys.argv[2], d['value'], d['ms_per_step'], d['decoded_ok'], d['values_ok'], (d.get('value_joined') or {}).get('value'), v.get('chain_frac_of_step'), v.get('issue_frac_of_step'))" "$@"; }
+timeout -k 10 60 tools/gf_probe 2.4 > $O/gf_probe.txt 2>&1 || { echo GFPROBEFAIL; cat $O/gf_probe.txt; exit 1; }
+cat $O/gf_probe.txt
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread > $O/gputest.log 2>&1 || { echo TESTFAIL; grep -E "FAILED|Error|error|assert" $O/gputest.log | tail -40; exit 1; }
 tail -1 $O/gputest.log
 timeout -k 10 200 python -c 'import __graft_entry__ as g; g.smoke(); print("smoke ok")' > $O/smoke.log 2>&1 || { echo SMOKEFAIL; tail -30 $O/smoke.log; exit 1; }
