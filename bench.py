@@ -99,8 +99,6 @@ def parse_args(argv):
     ap.add_argument("--decode-prio", default="",
                     help="gemv,reencode levels of interpolate's GF transforms: c (commit level), r (receive "
                          "level) or 0..3 (default per config, DECODE_PRIO; serial: commit level)")
-    ap.add_argument("--regen", default="auto", choices=("auto", "inline", "fork"),
-                    help="where the receive step hashes the regenerated rows (rbc_ctx_set_regen_hashing)")
     ap.add_argument("--hbm-budget", type=float, default=0,
                     help="bytes of HBM this rank may use (default: free device memory / ranks sharing the device)")
     ap.add_argument("--shard-align", type=int, default=128,
@@ -214,7 +212,6 @@ def run(args, world, rank, local_rank, wd, out):
     gv, rv = (lv[x] if x in lv else int(x)
               for x in (args.decode_prio or (DECODE_PRIO[args.config] if pipe else "c,c")).split(","))
     ctx.set_decode_priority(gv, rv)
-    ctx.set_regen_hashing(args.regen)
     stream = ca.Stream(dev)
     mb = lambda x: ca.DeviceBuffer(x, device=dev)  # noqa: E731
     # ---- synthetic inputs: values on the device (the global instance id
@@ -489,7 +486,6 @@ def run(args, world, rank, local_rank, wd, out):
                                   + (", RCCL all-gather of {root,digest} records" if gather else ""),
                    "gf_codec": ctx.codec,
                    "wave_priority": {"commit": tx, "receive": rx, "decode_gemv": gv, "decode_reencode": rv},
-                   "regen_hashing": args.regen,
                    "value_form": "joined (k*S bytes per instance)" if args.join else
                                  "row view (the k data rows of the shard set, no join)",
                    "faults_on": args.faults_on, "hbm_plan": plan,
@@ -735,8 +731,9 @@ def report(args, ctx, I, n, k, d, S, present_h, corrupt_h, stage_ms, iso, elapse
     # the receive step's two hashing launches, each over its own span (hash_begin -> rows_hashed ->
     # hashed marks): the row hashing, and at C4 the shared-path verify
     rx = [x for x in kern if kern[x][0] == "verify_rows"]
+    sv = [x for x in kern if kern[x][0] == "verify"]  # serial schedule: rbc_dev_verify's launch(es)
     out["roofline_verify"] = roofline(rx[0], "receive step's hash_begin -> rows_hashed marks (rbc_rx_marks)") \
-        if rx else None
+        if rx else (roofline(sv[0]) if sv else None)
     out["roofline_verify_path"] = roofline(
         "merkle_path_kernel<4>", "receive step's rows_hashed -> hashed marks (rbc_rx_marks)") \
         if "merkle_path_kernel<4>" in kern else None

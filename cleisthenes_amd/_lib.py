@@ -62,7 +62,6 @@ _SIGS = {
     "rbc_ctx_set_wave_priority": (c_int, [c_void_p, c_int, c_int]),
     "rbc_ctx_set_decode_priority": (c_int, [c_void_p, c_int, c_int]),
     "rbc_ctx_set_recheck": (c_int, [c_void_p, c_int]),
-    "rbc_ctx_set_regen_hashing": (c_int, [c_void_p, c_int]),
     "rbc_ctx_codec": (c_int, [c_void_p, POINTER(c_int)]),
     "rbc_dev_malloc": (c_int, [c_int, c_size_t, POINTER(c_void_p)]),
     "rbc_dev_free": (c_int, [c_void_p]),

@@ -102,16 +102,11 @@ struct Ws {
     int rx_count = 0;           // receive_step: batch decoded by the last call, awaiting its rehash + check
     const uint8_t *rx_shards = nullptr;  // ... and its shard buffer (identity check of `prev`)
     hipStream_t aux = nullptr;  // created on first use
-    // receive step, RBC_REGEN_FORK: the pending batch's regenerated rows were
-    // hashed on the aux stream after its decode; the next call's recheck waits
-    // for ev_regen instead of hashing them in its own SHA launch
-    bool rx_regen_forked = false;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_hashed = nullptr, ev_regen = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_hashed = nullptr;
     bool init() {
         return hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) == hipSuccess &&
                hipEventCreateWithFlags(&ev_join, hipEventDisableTiming) == hipSuccess &&
-               hipEventCreateWithFlags(&ev_hashed, hipEventDisableTiming) == hipSuccess &&
-               hipEventCreateWithFlags(&ev_regen, hipEventDisableTiming) == hipSuccess;
+               hipEventCreateWithFlags(&ev_hashed, hipEventDisableTiming) == hipSuccess;
     }
     void release() {
         for (DevBuf *b : {&used, &regen, &dmat, &nmiss, &flags, &list, &counter, &rcount, &cls, &vleaves, &vlist,
@@ -121,9 +116,8 @@ struct Ws {
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         if (ev_join) (void)hipEventDestroy(ev_join);
         if (ev_hashed) (void)hipEventDestroy(ev_hashed);
-        if (ev_regen) (void)hipEventDestroy(ev_regen);
         aux = nullptr;
-        ev_fork = ev_join = ev_hashed = ev_regen = nullptr;
+        ev_fork = ev_join = ev_hashed = nullptr;
     }
 };
 
@@ -188,9 +182,6 @@ struct rbc_ctx {
     // the receive step's root recheck: RBC_RECHECK_REUSE (default: over the
     // nodes ECHO verify established) or RBC_RECHECK_FULL (the whole tree)
     int recheck = RBC_RECHECK_REUSE;
-    // where the receive step hashes interpolate's regenerated rows:
-    // rbc_ctx_set_regen_hashing (RBC_REGEN_AUTO / INLINE / FORK)
-    int regen = RBC_REGEN_AUTO;
     int gemv_prio() const { return gemv_prio_ < 0 ? tx_prio : gemv_prio_; }
     int reencode_prio() const { return reencode_prio_ < 0 ? tx_prio : reencode_prio_; }
     std::vector<uint8_t> h_M;      // n x k encode matrix
@@ -262,9 +253,6 @@ hipStream_t host_stream(rbc_ctx *c) {
     if (!c->stream && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) c->stream = nullptr;
     return c->stream;
 }
-// RBC_REGEN_AUTO resolves to the inline form
-bool regen_fork(const rbc_ctx *c) { return c->regen == RBC_REGEN_FORK; }
-
 hipStream_t aux_stream(Ws &w) {
     if (!w.aux && hipStreamCreateWithFlags(&w.aux, hipStreamNonBlocking) != hipSuccess) w.aux = nullptr;
     return w.aux;
@@ -811,8 +799,7 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
         v_path = shared_path_verify(c, cur->shard_lens, cur->uniform_shard_len);
         v_walk = !v_path;
     }
-    const bool fork_regen = regen_fork(c);
-    if (hp && nr > 0 && !w.rx_regen_forked) {
+    if (hp && nr > 0) {
         r.count = prev->count;
         r.rows_per_inst = nr;
         r.rows = prev->shards;
@@ -861,8 +848,6 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
         }
     } pj{w, st};
     if (hp) {
-        // prev's regenerated rows hashed on the aux stream (the previous call forked them)
-        if (w.rx_regen_forked) RBC_HIP(hipStreamWaitEvent(st, w.ev_regen, 0));
         if (prev->digests) {  // beside the recheck, on the aux stream (after prev's join)
             RBC_HIP(hipEventRecord(w.ev_hashed, st));
             RBC_HIP(hipStreamWaitEvent(w.aux, w.ev_hashed, 0));
@@ -908,41 +893,15 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
         RBC_HIP(rbc_launch_merkle(m, true, st));
     }
     w.rx_count = 0;  // prev is complete once this call's work on `st` is; cur is pending only on success
-    w.rx_regen_forked = false;
     if (hc) {
         if (marks && marks->decode_begin) RBC_HIP(hipEventRecord((hipEvent_t)marks->decode_begin, st));
         rc = stage_regenerate(c, w, st, cur->count, cur->shards, cur->shard_pitch, cur->shard_lens,
                               cur->uniform_shard_len, cur->valid, cur->status, 1, r_cnt);
         if (rc) return rc;
         if (marks && marks->decoded) RBC_HIP(hipEventRecord((hipEvent_t)marks->decoded, st));
-        const bool regen_aux = fork_regen && nr > 0;
-        if (regen_aux || cur->values_out) {
+        if (cur->values_out) {  // the row-view form (values_out NULL) has no join
             RBC_HIP(hipEventRecord(w.ev_fork, st));
             RBC_HIP(hipStreamWaitEvent(w.aux, w.ev_fork, 0));
-        }
-        if (regen_aux) {
-            // cur's regenerated rows (the decode's list R[par]) hashed off the
-            // receiver stream, beside the next call's ECHO verify
-            ShaArgs g{};
-            g.count = cur->count;
-            g.rows_per_inst = nr;
-            g.rows = cur->shards;
-            g.inst_pitch = (uint64_t)c->n * cur->shard_pitch;
-            g.row_pitch = cur->shard_pitch;
-            g.lens = cur->shard_lens;
-            g.uniform_len = cur->uniform_shard_len;
-            g.status = cur->status;
-            g.leaves = cur->leaves;
-            g.leaves_inst_pitch = (uint64_t)c->n * 32;
-            g.n = c->n;
-            g.depth = c->depth;
-            g.list = w.list.as<uint32_t>();
-            g.list_count = r_cnt;
-            g.prio = c->rx_prio;
-            RBC_HIP(rbc_launch_sha_rows(g, false, w.aux));
-            RBC_HIP(hipEventRecord(w.ev_regen, w.aux));
-        }
-        if (cur->values_out) {  // the row-view form (values_out NULL) has no join
             rc = launch_join(c, w.aux, cur->count, cur->shards, cur->shard_pitch, cur->shard_lens,
                              cur->uniform_shard_len, cur->values_out, cur->value_pitch, cur->status);
             if (rc) return rc;
@@ -951,7 +910,6 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
         w.rx_shards = cur->shards;
         w.rx_vslot = cur_vslot;
         w.rx_vreuse = reuse;  // its verified roots were kept
-        w.rx_regen_forked = regen_aux;
     }
     w.rx_par ^= 1;  // the next call reads R[par] (cur's regen list) as its prev's
     return RBC_OK;  // pj: `st` waits for prev's join + digest
@@ -1059,13 +1017,6 @@ int rbc_ctx_set_recheck(rbc_ctx *c, int mode) {
     if (!c || (mode != RBC_RECHECK_REUSE && mode != RBC_RECHECK_FULL)) return RBC_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
     c->recheck = mode;
-    return RBC_OK;
-}
-
-int rbc_ctx_set_regen_hashing(rbc_ctx *c, int mode) {
-    if (!c || mode < RBC_REGEN_AUTO || mode > RBC_REGEN_FORK) return RBC_ERR_INVALID_ARG;
-    std::lock_guard<std::mutex> lk(c->mu);
-    c->regen = mode;
     return RBC_OK;
 }
 

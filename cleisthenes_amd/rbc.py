@@ -274,13 +274,6 @@ class Context:
         with no valid ECHO leaf are hashed) or "full" (the whole tree)."""
         check(lib.rbc_ctx_set_recheck(self._p, {"reuse": 0, "full": 1}[mode]), "rbc_ctx_set_recheck")
 
-    def set_regen_hashing(self, mode: str) -> None:
-        """Where the receive step hashes interpolate's regenerated rows:
-        "auto" (default), "inline" (the next call's SHA launch) or "fork"
-        (the aux stream, right after the batch's decode)."""
-        check(lib.rbc_ctx_set_regen_hashing(self._p, {"auto": 0, "inline": 1, "fork": 2}[mode]),
-              "rbc_ctx_set_regen_hashing")
-
     def verify_form(self, shard_len: int) -> str:
         """"walk" or "shared_path": the ECHO-verify form for rows of shard_len
         bytes (rbc_ctx_verify_form)."""

@@ -109,16 +109,6 @@ int rbc_ctx_set_decode_priority(rbc_ctx *ctx, int gemv_prio, int reencode_prio);
 #define RBC_RECHECK_REUSE 0
 #define RBC_RECHECK_FULL 1
 int rbc_ctx_set_recheck(rbc_ctx *ctx, int mode);
-/* Where rbc_dev_receive_step hashes the rows interpolate regenerated for a
- * batch (their leaves feed the next call's root recheck):
- * RBC_REGEN_INLINE, in the next call's SHA launch beside the ECHO verify;
- * RBC_REGEN_FORK, on the context's aux stream right after the batch's
- * decode, the next call's recheck waiting for it; RBC_REGEN_AUTO (default)
- * picks per geometry.  Same leaves and statuses either way. */
-#define RBC_REGEN_AUTO 0
-#define RBC_REGEN_INLINE 1
-#define RBC_REGEN_FORK 2
-int rbc_ctx_set_regen_hashing(rbc_ctx *ctx, int mode);
 /* Which ECHO-verify form rbc_dev_verify / rbc_dev_receive_step run for rows
  * of shard_len bytes (validateMessage, rbc/rbc.go:92-95): RBC_VERIFY_WALK,
  * the per-leaf branch walk fused into the row hashing, or

@@ -1329,16 +1329,13 @@ def test_merkle_build_branches_every_depth(gpu, ref, n, f):
 @pytest.mark.parametrize("n,f,B,I,all_present", [(128, 42, 1 << 16, 96, False), (16, 5, 3001, 64, False),
                                                   (256, 85, 86 * 40, 48, False), (64, 21, 22 * 700, 40, True),
                                                   (7, 2, 1000, 33, False)])
-@pytest.mark.parametrize("regen", ["inline", "fork"])
-def test_receive_step_pipeline_equals_verify_then_interpolate(gpu, ref, n, f, B, I, all_present, regen):
+def test_receive_step_pipeline_equals_verify_then_interpolate(gpu, ref, n, f, B, I, all_present):
     """rbc_dev_receive_step over three batches (verify(t) + rehash(t-1) in
     one SHA launch, recheck(t-1), decode(t), join on the aux stream, a final
     flush) yields exactly rbc_dev_verify + rbc_dev_interpolate(leaves_verified
     = 1) per batch: valid masks, statuses, values, digests and leaves, with
     corrupted ECHO shards, wrong committed roots and (all_present) no present
-    mask; the C4 shape takes the shared-path verify inside the step.  With
-    regen = "fork" the regenerated rows of t are hashed on the aux stream
-    after decode(t) and recheck(t) waits for them (RBC_REGEN_FORK).  Sampled
+    mask; the C4 shape takes the shared-path verify inside the step.  Sampled
     instances are also checked against the C oracle."""
     nb = 3
     want, got = [], []
@@ -1371,7 +1368,6 @@ def test_receive_step_pipeline_equals_verify_then_interpolate(gpu, ref, n, f, B,
                                   b["roots"], b["out"], pl.opitch, b["digests"], b["status"])
         else:
             rx = gpu.Context(n, f)
-            rx.set_regen_hashing(regen)
             st = gpu.Stream(0)
             bs = [rx.rx_batch(I, pl.b["shards"], pl.spitch, None, pl.S, pl.b["branches"], pl.b["roots"],
                               present(pl), pl.b["valid"], pl.b["leaves_r"], pl.b["out"], pl.opitch,
