@@ -417,6 +417,28 @@ class Context:
         check(lib.rbc_wait(self._p, t.value))
         return ok.astype(bool)
 
+    def validate_packed(self, arena: np.ndarray, offs, lens, idx, branches: np.ndarray, roots: np.ndarray,
+                        arena_bytes: Optional[int] = None) -> np.ndarray:
+        """rbc_validate_packed: message i is arena[offs[i] : offs[i] + lens[i]]
+        (offs[i] % 64 == 0), its branch branches[i] in the device form
+        [depth][32], its root roots[i], its leaf index idx[i]; waits and returns
+        the verdicts."""
+        count = len(offs)
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        o = np.ascontiguousarray(offs, dtype=np.uint64)
+        ln = np.ascontiguousarray(lens, dtype=np.uint32)
+        ix = np.ascontiguousarray(idx, dtype=np.uint8)
+        br = np.ascontiguousarray(branches, dtype=np.uint8)
+        rt = np.ascontiguousarray(roots, dtype=np.uint8)
+        ok = np.zeros(max(count, 1), dtype=np.uint8)
+        t = c_uint64(0)
+        check(lib.rbc_validate_packed(self._p, count, _ptr(arena), arena.nbytes if arena_bytes is None else arena_bytes,
+                                      _ptr(o), _ptr(ln), _ptr(ix), _ptr(br), _ptr(rt), _ptr(ok), byref(t)),
+              "rbc_validate_packed")
+        if t.value:
+            check(lib.rbc_wait(self._p, t.value))
+        return ok[:count].astype(bool)
+
     def interpolate_batch(self, shards: np.ndarray, shard_lens, present: np.ndarray, roots: np.ndarray,
                           values_out: Optional[np.ndarray] = None) -> dict:
         return self.interpolate_submit(shards, shard_lens, present, roots, values_out).wait()

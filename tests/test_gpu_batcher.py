@@ -97,3 +97,43 @@ def test_validate_lane_16k_outstanding_matches_oracle(gpu, n, f):
             assert launches >= len(msgs) // 1000, launches
         bt.close()
     assert 0.3 < np.mean(want) < 0.9  # honest and tampered messages both present
+
+
+@pytest.mark.parametrize("n,f", [(128, 42), (37, 12), (256, 85)])
+def test_validate_packed_matches_oracle_and_checks_its_layout(gpu, n, f):
+    """rbc_validate_packed, the launch the lane (and a Go batcher with its own
+    pinned rings) calls: messages packed at 64-B aligned offsets with gaps, in
+    pageable and in pinned memory, ragged lengths, device-form branches (zero
+    level-0 slot where j ^ 1 >= n), honest and tampered -- every verdict equals
+    the C oracle's.  A misaligned offset, a message past the arena's end, a
+    zero length and a leaf index >= n are refused before any work; count 0 is
+    a no-op."""
+    rng = np.random.default_rng(7 * n)
+    d = max(1, (n - 1).bit_length())
+    msgs = [m for m in _messages(n, f, 3000, seed=11 * n) if m[2] and _unflatten(m[1], m[3], n, d) is not None]
+    count = len(msgs)
+    offs, pos = np.zeros(count, np.uint64), 0
+    for i, m in enumerate(msgs):
+        offs[i] = pos
+        pos += (len(m[2]) + 63) // 64 * 64 + 64 * int(rng.integers(0, 3))  # gaps of 0-2 blocks
+    lens = np.array([len(m[2]) for m in msgs], np.uint32)
+    idx = np.array([m[3] for m in msgs], np.uint8)
+    br = np.stack([_unflatten(m[1], m[3], n, d).reshape(-1) for m in msgs])
+    roots = np.stack([np.frombuffer(m[0], np.uint8) for m in msgs])
+    want = np.array([m[4] for m in msgs])
+    ctx = gpu.Context(n, f)
+    for pinned in (False, True):
+        arena = gpu.pinned_empty((pos,)) if pinned else np.zeros(pos, np.uint8)
+        arena[:] = rng.integers(0, 256, pos, dtype=np.uint8)  # the gaps hold garbage
+        for i, m in enumerate(msgs):
+            arena[int(offs[i]): int(offs[i]) + len(m[2])] = np.frombuffer(m[2], np.uint8)
+        got = ctx.validate_packed(arena, offs, lens, idx, br, roots)
+        assert np.array_equal(got, want), np.flatnonzero(got != want)[:10]
+    assert 0.3 < want.mean() < 0.95
+    small = np.zeros(4096, np.uint8)
+    one = dict(branches=br[:1], roots=roots[:1])
+    bad = [(8, 100, 0), (4096 - 64, 100, 0), (0, 0, 0)] + ([(0, 100, n)] if n < 256 else [])  # idx is a byte
+    for o, ln, ix in bad:
+        with pytest.raises(gpu.RBCError):
+            ctx.validate_packed(small, [o], [ln], [ix], **one)
+    assert ctx.validate_packed(small, [], [], [], br[:0], roots[:0]).size == 0
