@@ -534,7 +534,7 @@ def batcher_sweep(cpu):
     rows = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     sweep = [x for x in rows if x.get("phase") == "validate"]
     out = {"unit": "GB/s of ECHO shard bytes (S per message), host memory in, verdicts out",
-           "sweep": [{kk: x[kk] for kk in ("outstanding", "window", "messages", "GBps", "msg_per_s", "launches",
+           "sweep": [{kk: x[kk] for kk in ("outstanding", "window", "messages", "seconds", "GBps", "msg_per_s", "launches",
                                             "msgs_per_launch", "failed")} for x in sweep],
            "failures": next((x["failures"] for x in rows if x.get("phase") == "check"), None), "rc": r.returncode,
            "tool": "tools/batcher_bench validate-sweep (C2: N=128, f=42, 1 MiB values, S=23,832; 16 client threads)"}
@@ -909,11 +909,17 @@ def cpu_baseline(args, host):
         roots = np.stack([np.frombuffer(c[1], np.uint8) for c in com])
         m = np.arange(88064)
         inst, j = (m // (n - f)) % len(com), m % (n - f)
-        secs, ok = rbc_ref.verify_many(n, shards, branches, roots, inst, j, threads)
+        # three passes over the epoch (each ~0.1 s on 16 cores), the median reported: one short pass
+        # moved with the shared host's load by ~12 %
+        runs = [rbc_ref.verify_many(n, shards, branches, roots, inst, j, threads) for _ in range(3)]
+        secs = sorted(r[0] for r in runs)[1]
+        ok = np.logical_and.reduce([r[1] for r in runs])
         S = shards.shape[2]
         return {"GBps": round(len(m) * S / secs / 1e9, 3), "msg_per_s": round(len(m) / secs), "cores": threads,
                 "all_valid": bool(ok.all()), "kind": "port",
-                "sample": f"{len(m)} C2 ECHO messages (S={S}) from {len(com)} committed values, {secs:.3f} s"}
+                "runs_GBps": [round(len(m) * S / r[0] / 1e9, 3) for r in runs],
+                "sample": f"{len(m)} C2 ECHO messages (S={S}) from {len(com)} committed values, median of 3 "
+                          f"passes, {secs:.3f} s"}
 
     main_cfg = args.config
     res, single = run(main_cfg, 6e9, threads), run(main_cfg, 6e9 / 16, 1)
