@@ -45,7 +45,7 @@ class RxBatch(ctypes.Structure):
 class RxMarks(ctypes.Structure):
     """rbc_rx_marks (include/rbc_gpu.h): timing events of rbc_dev_receive_step."""
     _fields_ = [("hashed", c_void_p), ("decode_begin", c_void_p), ("decoded", c_void_p), ("hash_begin", c_void_p),
-                ("rows_hashed", c_void_p)]
+                ("rows_hashed", c_void_p), ("prev_released", c_void_p)]
 
 
 _SIGS = {

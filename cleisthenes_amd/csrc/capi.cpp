@@ -102,11 +102,12 @@ struct Ws {
     int rx_count = 0;           // receive_step: batch decoded by the last call, awaiting its rehash + check
     const uint8_t *rx_shards = nullptr;  // ... and its shard buffer (identity check of `prev`)
     hipStream_t aux = nullptr;  // created on first use
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_hashed = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_hashed = nullptr, ev_rel = nullptr;
     bool init() {
         return hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) == hipSuccess &&
                hipEventCreateWithFlags(&ev_join, hipEventDisableTiming) == hipSuccess &&
-               hipEventCreateWithFlags(&ev_hashed, hipEventDisableTiming) == hipSuccess;
+               hipEventCreateWithFlags(&ev_hashed, hipEventDisableTiming) == hipSuccess &&
+               hipEventCreateWithFlags(&ev_rel, hipEventDisableTiming) == hipSuccess;
     }
     void release() {
         for (DevBuf *b : {&used, &regen, &dmat, &nmiss, &flags, &list, &counter, &rcount, &cls, &vleaves, &vlist,
@@ -116,8 +117,9 @@ struct Ws {
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         if (ev_join) (void)hipEventDestroy(ev_join);
         if (ev_hashed) (void)hipEventDestroy(ev_hashed);
+        if (ev_rel) (void)hipEventDestroy(ev_rel);
         aux = nullptr;
-        ev_fork = ev_join = ev_hashed = nullptr;
+        ev_fork = ev_join = ev_hashed = ev_rel = nullptr;
     }
 };
 
@@ -891,6 +893,14 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
             m.only = ra.need_full;
         }
         RBC_HIP(rbc_launch_merkle(m, true, st));
+        if (marks && marks->prev_released) {
+            // the recheck was the last reader of prev's set on `st`; the aux
+            // stream already holds prev's join and digest: the mark completes
+            // after all three, and `st` goes on to cur's decode without waiting
+            RBC_HIP(hipEventRecord(w.ev_rel, st));
+            RBC_HIP(hipStreamWaitEvent(w.aux, w.ev_rel, 0));
+            RBC_HIP(hipEventRecord((hipEvent_t)marks->prev_released, w.aux));
+        }
     }
     w.rx_count = 0;  // prev is complete once this call's work on `st` is; cur is pending only on success
     if (hc) {

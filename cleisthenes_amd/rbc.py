@@ -512,15 +512,16 @@ class Context:
                             v(present), v(valid), v(leaves), v(values_out), value_pitch, v(digests), v(status))
 
     def dev_receive_step(self, stream, cur=None, prev=None, hashed=None, decode_begin=None, decoded=None,
-                         hash_begin=None, rows_hashed=None) -> None:
+                         hash_begin=None, rows_hashed=None, prev_released=None) -> None:
         """Pipelined receiver: verify(cur) + rehash(prev) in one SHA launch,
         prev's recheck + digest, cur's decode (rbc_dev_receive_step).  hashed /
         decode_begin / decoded (Events, optional) are recorded after the
         hashing launch (and the shared-path verify), before cur's decode and
         after it; hash_begin / rows_hashed right before and after the
-        row-hashing launch alone (rbc_rx_marks)."""
+        row-hashing launch alone; prev_released once nothing of the call reads
+        prev's shard set any more (rbc_rx_marks)."""
         marks = None
-        evs = (hashed, decode_begin, decoded, hash_begin, rows_hashed)
+        evs = (hashed, decode_begin, decoded, hash_begin, rows_hashed, prev_released)
         if any(e is not None for e in evs):
             ev = lambda e: e.ptr.value if e is not None else None  # noqa: E731
             marks = ctypes.byref(_lib.RxMarks(*(ev(e) for e in evs)))

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define RBC_ABI_VERSION 4
+#define RBC_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------- */
 #define RBC_OK 0
@@ -243,13 +243,20 @@ typedef struct rbc_rx_batch {
  * hash_begin right before the row-hashing launch (after cur's compaction) and
  * rows_hashed right after it, before the shared-path verify
  * (merkle_path_kernel, W = 256 at short rows) -- so each of the two kernels
- * has its own span; with the per-leaf walk rows_hashed and hashed coincide. */
+ * has its own span; with the per-leaf walk rows_hashed and hashed coincide.
+ * ABI 5: prev_released completes once nothing of this call reads prev's
+ * shards, branches or roots any more (its recheck on `stream`, its digest and
+ * a join from the previous call on the context's aux stream; recorded on the
+ * aux stream, so `stream` does not wait for it): a producer may refill prev's
+ * shard set from then on while cur's decode still runs.  Not recorded when
+ * prev is NULL. */
 typedef struct rbc_rx_marks {
     void *hashed;
     void *decode_begin;
     void *decoded;
     void *hash_begin;
     void *rows_hashed;
+    void *prev_released;
 } rbc_rx_marks;
 int rbc_dev_receive_step(rbc_ctx *ctx, void *stream, const rbc_rx_batch *cur, const rbc_rx_batch *prev,
                          const rbc_rx_marks *marks);

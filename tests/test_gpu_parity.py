@@ -1329,14 +1329,18 @@ def test_merkle_build_branches_every_depth(gpu, ref, n, f):
 @pytest.mark.parametrize("n,f,B,I,all_present", [(128, 42, 1 << 16, 96, False), (16, 5, 3001, 64, False),
                                                   (256, 85, 86 * 40, 48, False), (64, 21, 22 * 700, 40, True),
                                                   (7, 2, 1000, 33, False)])
-def test_receive_step_pipeline_equals_verify_then_interpolate(gpu, ref, n, f, B, I, all_present):
+@pytest.mark.parametrize("clobber", [False, True], ids=["", "released-set-clobbered"])
+def test_receive_step_pipeline_equals_verify_then_interpolate(gpu, ref, n, f, B, I, all_present, clobber):
     """rbc_dev_receive_step over three batches (verify(t) + rehash(t-1) in
     one SHA launch, recheck(t-1), decode(t), join on the aux stream, a final
     flush) yields exactly rbc_dev_verify + rbc_dev_interpolate(leaves_verified
     = 1) per batch: valid masks, statuses, values, digests and leaves, with
     corrupted ECHO shards, wrong committed roots and (all_present) no present
-    mask; the C4 shape takes the shared-path verify inside the step.  Sampled
-    instances are also checked against the C oracle."""
+    mask; the C4 shape takes the shared-path verify inside the step.  With
+    clobber, a second stream waits for each call's prev_released mark and
+    then overwrites prev's shards, branches and roots with garbage while the
+    call's decode of cur runs: nothing of prev may be read after the mark.
+    Sampled instances are also checked against the C oracle."""
     nb = 3
     want, got = [], []
     for mode in ("oneshot", "step"):
@@ -1373,8 +1377,18 @@ def test_receive_step_pipeline_equals_verify_then_interpolate(gpu, ref, n, f, B,
                               present(pl), pl.b["valid"], pl.b["leaves_r"], pl.b["out"], pl.opitch,
                               pl.b["digests"], pl.b["status"]) for pl in pls]
             prev = None
+            cl = gpu.Stream(0)
             for cur in bs + [None]:
-                rx.dev_receive_step(st.ptr, cur, prev)
+                if clobber and prev is not None:
+                    rel = gpu.Event()
+                    rx.dev_receive_step(st.ptr, cur, prev, prev_released=rel)
+                    cl.wait(rel)  # prev's set is the producer's again: refill it with garbage
+                    pp = pls[[id(b_) for b_ in bs].index(id(prev))]
+                    gpu.rbc.fill_random(0, cl.ptr, pp.b["shards"], 0, I, n * pp.spitch, 99)
+                    gpu.rbc.fill_random(0, cl.ptr, pp.b["branches"], 0, I, n * max(pp.d, 1) * 32, 98)
+                    gpu.rbc.fill_random(0, cl.ptr, pp.b["roots"], 0, I, 32, 97)
+                else:
+                    rx.dev_receive_step(st.ptr, cur, prev)
                 if cur is not None and prev is None:  # a batch is pending: interpolate must refuse
                     pl = pls[0]
                     with pytest.raises(gpu.RBCError):
@@ -1385,6 +1399,7 @@ def test_receive_step_pipeline_equals_verify_then_interpolate(gpu, ref, n, f, B,
             with pytest.raises(gpu.RBCError):  # prev must be the last call's cur
                 rx.dev_receive_step(st.ptr, None, bs[0])
             st.sync()
+            cl.sync()
         gpu.rbc.lib.rbc_device_sync(0)
         res = []
         for pl in pls:
