@@ -99,9 +99,6 @@ def parse_args(argv):
     ap.add_argument("--decode-prio", default="",
                     help="gemv,reencode levels of interpolate's GF transforms: c (commit level), r (receive "
                          "level) or 0..3 (default per config, DECODE_PRIO; serial: commit level)")
-    ap.add_argument("--p-release", default="recheck", choices=("recheck", "step"),
-                    help="when the proposer may refill batch t-2's shard set: after its recheck (the receive "
-                         "step's prev_released mark) or after the whole receive step (A/B)")
     ap.add_argument("--hbm-budget", type=float, default=0,
                     help="bytes of HBM this rank may use (default: free device memory / ranks sharing the device)")
     ap.add_argument("--shard-align", type=int, default=128,
@@ -321,12 +318,8 @@ def run(args, world, rank, local_rank, wd, out):
         prev = pending.pop(x - 1, None)
         marks = {nm: ev[key] for nm, key in (("hashed", "hashed"), ("decode_begin", "dbeg"), ("decoded", "ddone"),
                                              ("hash_begin", "hb"), ("rows_hashed", "rh"))} if ev is not None else {}
-        # batch t-2's set is free once its recheck (and the aux stream's digest / join) is done, before
-        # t-1's decode: P refills it while that decode runs.  With the RCCL gather the set's roots are
-        # read after the receive step, so the release waits for the gather.
-        early = prev is not None and not gather and args.p_release == "recheck"
-        if early:
-            marks["prev_released"] = evR[(x - 1) % nsets]
+        # batch t-2's set goes back to P after the whole receive step, not at its prev_released mark
+        # (after t-2's recheck): P's encode beside t-1's decode lost 14 % at C4 (gpu_r05q.sh)
         ctx.dev_receive_step(R.ptr, cur, prev, **marks)
         pending[x] = cur
         rec(ev, "rend", R)
@@ -335,7 +328,7 @@ def run(args, world, rank, local_rank, wd, out):
             ctx.dev_allgather_records(R.ptr, I, slots, sets[(x - 1) % nsets]["roots"], pb["digests"], pb["status"],
                                       d_gather)
         rec(ev, "gather", R)
-        if prev is not None and not early:
+        if prev is not None:
             evR[(x - 1) % nsets].record(R)
 
     def barrier():
@@ -495,8 +488,6 @@ def run(args, world, rank, local_rank, wd, out):
                                   + (", RCCL all-gather of {root,digest} records" if gather else ""),
                    "gf_codec": ctx.codec,
                    "wave_priority": {"commit": tx, "receive": rx, "decode_gemv": gv, "decode_reencode": rv},
-                   "set_release": ("after the recheck (prev_released mark)" if args.p_release == "recheck" and not gather
-                                   else "after the receive step") if pipe else None,
                    "value_form": "joined (k*S bytes per instance)" if args.join else
                                  "row view (the k data rows of the shard set, no join)",
                    "faults_on": args.faults_on, "hbm_plan": plan,
