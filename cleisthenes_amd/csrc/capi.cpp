@@ -1751,7 +1751,8 @@ int rbc_validate_packed(rbc_ctx *c, int count, const uint8_t *arena, size_t aren
     // every message's 64-B blocks must lie inside the arena (the kernel reads
     // whole blocks) and its leaf index inside the tree
     for (int i = 0; i < count; ++i)
-        if (offs[i] % 64 || lens[i] == 0 || offs[i] + round_up((size_t)lens[i], 64) > arena_bytes || idx[i] >= c->n)
+        if (offs[i] % 64 || lens[i] == 0 || offs[i] > arena_bytes ||
+            round_up((size_t)lens[i], 64) > arena_bytes - offs[i] || idx[i] >= c->n)  // no wrap-around
             return RBC_ERR_INVALID_ARG;
     const int d = c->depth;
     const size_t bslot = (size_t)std::max(d, 1) * 32;

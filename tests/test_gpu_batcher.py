@@ -132,7 +132,8 @@ def test_validate_packed_matches_oracle_and_checks_its_layout(gpu, n, f):
     assert 0.3 < want.mean() < 0.95
     small = np.zeros(4096, np.uint8)
     one = dict(branches=br[:1], roots=roots[:1])
-    bad = [(8, 100, 0), (4096 - 64, 100, 0), (0, 0, 0)] + ([(0, 100, n)] if n < 256 else [])  # idx is a byte
+    bad = [(8, 100, 0), (4096 - 64, 100, 0), (0, 0, 0), (2 ** 64 - 64, 100, 0)]  # the last wraps past 2^64
+    bad += [(0, 100, n)] if n < 256 else []  # idx is a byte
     for o, ln, ix in bad:
         with pytest.raises(gpu.RBCError):
             ctx.validate_packed(small, [o], [ln], [ix], **one)
