@@ -697,7 +697,9 @@ int rbc_batcher_create(rbc_ctx *ctx, int max_batch, int max_wait_us, rbc_batcher
 }
 
 int rbc_batcher_set_validate(rbc_batcher *b, int max_msgs, size_t max_bytes) {
-    if (!b || max_msgs < 1 || max_msgs >= (1 << kVSlotBits) || max_bytes < 64) return RBC_ERR_INVALID_ARG;
+    // a message's length travels as uint32 (rbc_validate_packed): arenas stay below 4 GiB
+    if (!b || max_msgs < 1 || max_msgs >= (1 << kVSlotBits) || max_bytes < 64 || max_bytes > ((size_t)1 << 32) - 64)
+        return RBC_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(b->vmu);
     if (b->v_next_gen != 1) return RBC_ERR_INVALID_ARG;  // before the first validate only
     b->v_max_msgs = max_msgs;

@@ -341,7 +341,8 @@ int rbc_batcher_shard(rbc_batcher *b, const uint8_t *data, size_t len, uint8_t *
 int rbc_batcher_validate(rbc_batcher *b, const uint8_t *root, const uint8_t *branch, size_t branch_len,
                          const uint8_t *shard, size_t shard_len, uint32_t index, int *ok_out, uint64_t *ticket);
 /* The validate lane's arena size (default 65,536 messages / 256 MiB of
- * shards, six arenas, four in flight); before the first validate only. */
+ * shards, six arenas, four in flight); before the first validate only.
+ * max_msgs < 2^20, 64 <= max_bytes <= 4 GiB - 64. */
 int rbc_batcher_set_validate(rbc_batcher *b, int max_msgs, size_t max_bytes);
 /* interpolate(): shards/lens are n entries (lens[j] == 0: missing) */
 int rbc_batcher_interpolate(rbc_batcher *b, const uint8_t *root, const uint8_t *const *shards, const size_t *lens,
