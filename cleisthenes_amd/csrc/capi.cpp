@@ -460,9 +460,15 @@ int ensure_ws(rbc_ctx *c, Ws &w, int count) {
 // decode_prepare + GF regeneration (in place), no hashing
 // compare != 0: valid-but-unused rows are compared, not blindly rewritten,
 // and the rows that need hashing are collected in ws_list
+// values_out (optional): interpolate's joined value, assembled by the FFT
+// re-encode from the data rows it loads (no separate join pass) where that
+// applies -- the FFT codec, uniform S, a value row at most 256 B longer than
+// k*S; *joined tells the caller whether it happened
 int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shards, uint32_t shard_pitch,
                      const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *valid,
-                     int32_t *status, int compare = 0, uint32_t *zeroed_counter = nullptr) {
+                     int32_t *status, int compare = 0, uint32_t *zeroed_counter = nullptr,
+                     uint8_t *values_out = nullptr, uint32_t value_pitch = 0, bool *joined = nullptr) {
+    if (joined) *joined = false;
     int rc = ensure_ws(c, w, count);
     if (rc) return rc;
     // the regen list's counter: the workspace's own (zeroed here), or one the
@@ -548,6 +554,12 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
             a.counter = pa.counter;
         }
         a.prio = c->reencode_prio();
+        if (values_out && joined && !shard_lens && value_pitch >= (uint64_t)c->k * uniform_shard_len &&
+            value_pitch - (uint64_t)c->k * uniform_shard_len <= 256) {
+            a.join = values_out;
+            a.join_pitch = value_pitch;
+            *joined = true;
+        }
         RBC_HIP(rbc_launch_rs_fft(a, st));
     } else if (nr > 0) {
         GfArgs g{};
@@ -640,12 +652,13 @@ int stage_interpolate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *sha
         return RBC_ERR_INVALID_ARG;
     if ((uint64_t)c->n * shard_pitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
     if (count == 0) return RBC_OK;
+    bool joined = false;
     int rc = stage_regenerate(c, w, st, count, shards, shard_pitch, shard_lens, uniform_shard_len, valid, status,
-                              leaves_verified);
+                              leaves_verified, nullptr, values_out, value_pitch, &joined);
     if (rc) return rc;
     JoinBack jb{w, st};
     if (w.fork && (values_out || digests) && !aux_stream(w)) return RBC_ERR_DEVICE;
-    if (values_out) {
+    if (values_out && !joined) {
         hipStream_t js = st;
         if (w.fork) {
             RBC_HIP(hipEventRecord(w.ev_fork, st));
@@ -905,11 +918,13 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
     w.rx_count = 0;  // prev is complete once this call's work on `st` is; cur is pending only on success
     if (hc) {
         if (marks && marks->decode_begin) RBC_HIP(hipEventRecord((hipEvent_t)marks->decode_begin, st));
+        bool joined = false;
         rc = stage_regenerate(c, w, st, cur->count, cur->shards, cur->shard_pitch, cur->shard_lens,
-                              cur->uniform_shard_len, cur->valid, cur->status, 1, r_cnt);
+                              cur->uniform_shard_len, cur->valid, cur->status, 1, r_cnt, cur->values_out,
+                              cur->value_pitch, &joined);
         if (rc) return rc;
         if (marks && marks->decoded) RBC_HIP(hipEventRecord((hipEvent_t)marks->decoded, st));
-        if (cur->values_out) {  // the row-view form (values_out NULL) has no join
+        if (cur->values_out && !joined) {  // the row view (values_out NULL) has no join; the FFT decode joins
             RBC_HIP(hipEventRecord(w.ev_fork, st));
             RBC_HIP(hipStreamWaitEvent(w.aux, w.ev_fork, 0));
             rc = launch_join(c, w.aux, cur->count, cur->shards, cur->shard_pitch, cur->shard_lens,

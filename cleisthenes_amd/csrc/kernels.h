@@ -190,6 +190,11 @@ struct FftArgs {
     uint32_t *list;
     uint32_t *counter;
     int prio;                  // wave issue priority 0..3 (set_wave_prio)
+    // decode, optional: also assemble interpolate's value from the k data rows
+    // the kernel loads anyway -- join[i][0 .. k*S) = data rows 0..k-1 of S
+    // bytes, zeros up to join_pitch (uniform S only, join_pitch - k*S < 256)
+    uint8_t *join;
+    uint32_t join_pitch;
 };
 
 // VAL / ECHO marshaling (wire.hip): message (i, j) = pb.Message bytes of

@@ -340,6 +340,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void rs
         });
     } else {
         lch::sfor<0, K>([&](auto J) { v[decltype(J)::value] = row_load(decltype(J)::value); });
+        if (a.join) {
+            // interpolate's value (rbc/rbc.go:88) straight from the loaded rows:
+            // data row j at j*S, dword stores at byte offsets that need not be
+            // aligned, the lane that straddles S writes its bytes one by one;
+            // tile 0 zeroes the value's tail up to join_pitch.  The buffer
+            // descriptor bounds every store to the instance's value row.
+            const auto rj = __builtin_amdgcn_make_buffer_rsrc(a.join + (size_t)inst * a.join_pitch, (short)0,
+                                                              (int)a.join_pitch, 0x00020000);
+            const int nb = (int)S - (int)off;  // this lane's valid bytes per row
+            lch::sfor<0, K>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                const int so = (int)((uint32_t)j * S);
+                if (nb >= 4) {
+                    __builtin_amdgcn_raw_buffer_store_b32(v[j], rj, (int)off, so, 0);
+                } else if (nb > 0) {
+                    for (int b = 0; b < nb; ++b)
+                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v[j] >> (8 * b)), rj, (int)off + b, so, 0);
+                }
+            });
+            if (tile_x == 0) {
+                const uint32_t end = (uint32_t)K * S;
+                for (int b = 0; b < 4; ++b) {
+                    const uint32_t o = end + 4u * threadIdx.x + (uint32_t)b;
+                    if (o < a.join_pitch) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, rj, (int)o, 0, 0);
+                }
+            }
+        }
     }
 
     lch::solve<LOGW, 0, 0, K>(v);

@@ -208,6 +208,7 @@ hipError_t rbc_launch_gf_regen(const GfArgs &a, hipStream_t st) {
 }
 hipError_t rbc_launch_rs_fft(const FftArgs &a, hipStream_t) {
     if (a.count > 0) touch(a.shards, (size_t)a.count * a.inst_pitch);
+    if (a.count > 0 && a.join) touch(a.join, (size_t)a.count * a.join_pitch);  // the fused value join
     return hipSuccess;
 }
 hipError_t rbc_launch_sha_rows(const ShaArgs &a, bool verify, hipStream_t) {
