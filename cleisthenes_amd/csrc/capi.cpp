@@ -91,9 +91,6 @@ struct Ws {
     // call.  One lane of the hashing launch zeroes the next users' counters
     // (no memset launches on the receiver stream); v_clean tracks V[] on the host.
     DevBuf rxcnt;
-    // receive step: the decode's change flags of cur (written) and prev (read
-    // by its recheck), by parity, so cur's prepare can run beside prev's recheck
-    DevBuf rxflags[2];
     int rx_par = 0;
     bool rxcnt_init = false, v_clean[2] = {true, true};
     int rx_vslot = 0;           // slot of the pending batch's verified roots
@@ -105,29 +102,24 @@ struct Ws {
     int rx_count = 0;           // receive_step: batch decoded by the last call, awaiting its rehash + check
     const uint8_t *rx_shards = nullptr;  // ... and its shard buffer (identity check of `prev`)
     hipStream_t aux = nullptr;  // created on first use
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_hashed = nullptr, ev_rel = nullptr, ev_prep_in = nullptr,
-               ev_prep = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_hashed = nullptr, ev_rel = nullptr;
     bool init() {
         return hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) == hipSuccess &&
                hipEventCreateWithFlags(&ev_join, hipEventDisableTiming) == hipSuccess &&
                hipEventCreateWithFlags(&ev_hashed, hipEventDisableTiming) == hipSuccess &&
-               hipEventCreateWithFlags(&ev_rel, hipEventDisableTiming) == hipSuccess &&
-               hipEventCreateWithFlags(&ev_prep_in, hipEventDisableTiming) == hipSuccess &&
-               hipEventCreateWithFlags(&ev_prep, hipEventDisableTiming) == hipSuccess;
+               hipEventCreateWithFlags(&ev_rel, hipEventDisableTiming) == hipSuccess;
     }
     void release() {
         for (DevBuf *b : {&used, &regen, &dmat, &nmiss, &flags, &list, &counter, &rcount, &cls, &vleaves, &vlist,
-                          &vroot[0], &vroot[1], &need_full, &rxcnt, &rxflags[0], &rxflags[1]})
+                          &vroot[0], &vroot[1], &need_full, &rxcnt})
             b->release();
         if (aux) (void)hipStreamDestroy(aux);
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         if (ev_join) (void)hipEventDestroy(ev_join);
         if (ev_hashed) (void)hipEventDestroy(ev_hashed);
         if (ev_rel) (void)hipEventDestroy(ev_rel);
-        if (ev_prep_in) (void)hipEventDestroy(ev_prep_in);
-        if (ev_prep) (void)hipEventDestroy(ev_prep);
         aux = nullptr;
-        ev_fork = ev_join = ev_hashed = ev_rel = ev_prep_in = ev_prep = nullptr;
+        ev_fork = ev_join = ev_hashed = ev_rel = nullptr;
     }
 };
 
@@ -475,8 +467,7 @@ int ensure_ws(rbc_ctx *c, Ws &w, int count) {
 int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shards, uint32_t shard_pitch,
                      const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *valid,
                      int32_t *status, int compare = 0, uint32_t *zeroed_counter = nullptr,
-                     uint8_t *values_out = nullptr, uint32_t value_pitch = 0, bool *joined = nullptr,
-                     uint32_t *flags_buf = nullptr, hipStream_t prep_st = nullptr, hipEvent_t prep_in = nullptr) {
+                     uint8_t *values_out = nullptr, uint32_t value_pitch = 0, bool *joined = nullptr) {
     if (joined) *joined = false;
     int rc = ensure_ws(c, w, count);
     if (rc) return rc;
@@ -502,7 +493,7 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
     pa.prio = c->rx_prio;
     if (compare) {
         pa.nmiss = w.nmiss.as<int32_t>();
-        pa.flags = flags_buf ? flags_buf : w.flags.as<uint32_t>();
+        pa.flags = w.flags.as<uint32_t>();
         pa.list = w.list.as<uint32_t>();
         pa.counter = counter;
     }
@@ -514,16 +505,7 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
         pa.gf_exp = c->d_M + c->h_M.size();
         pa.gf_log = pa.gf_exp + 512;
     }
-    if (prep_st) {
-        // the receive step: prepare on prep_st once prep_in (cur's verdicts
-        // final) has fired, beside whatever `st` runs meanwhile (prev's recheck)
-        RBC_HIP(hipStreamWaitEvent(prep_st, prep_in, 0));
-        RBC_HIP(rbc_launch_decode_prepare(pa, prep_st));
-        RBC_HIP(hipEventRecord(w.ev_prep, prep_st));
-        RBC_HIP(hipStreamWaitEvent(st, w.ev_prep, 0));
-    } else {
-        RBC_HIP(rbc_launch_decode_prepare(pa, st));
-    }
+    RBC_HIP(rbc_launch_decode_prepare(pa, st));
     if (c->fft && nr > 0) {
         // 1) missing data rows: D (rcount[i] x k, per instance) times the used rows
         const int rmax = std::min(c->k, nr);
@@ -870,31 +852,24 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
         RBC_HIP(rbc_launch_merkle_path(p, st));
     }
     if (marks && marks->hashed) RBC_HIP(hipEventRecord((hipEvent_t)marks->hashed, st));
-    // the decode's change flags by parity: cur's (cleared by its prepare, set
-    // by its re-encode) and prev's (read by its recheck) are separate buffers
-    uint32_t *fl_cur = nullptr, *fl_prev = w.rxflags[par ^ 1].as<uint32_t>();
-    if (hc) {
-        RBC_HIP(w.rxflags[par].ensure((size_t)cur->count * c->n * 4));
-        fl_cur = w.rxflags[par].as<uint32_t>();
-    }
-    // cur's prepare runs on the aux stream beside prev's recheck: both are
-    // short latency-bound kernels on the receiver's critical chain
-    const bool prep_aux = hc && hp;
-    if (prep_aux) RBC_HIP(hipEventRecord(w.ev_prep_in, st));  // cur's verdicts are final
-    // From here on the aux stream's work (prev's join from the previous call,
-    // prev's digest, cur's prepare) is joined back into `st` on every exit,
-    // errors included.
+    // From here on prev's aux-stream work (its join from the previous call and
+    // its digest) is joined back into `st` on every exit, errors included.
     struct PrevJoin {
         Ws &w;
         hipStream_t st;
-        bool armed = false, recorded = false;
+        bool armed = false;
         ~PrevJoin() {
-            if (!armed) return;
-            if (!recorded) (void)hipEventRecord(w.ev_join, w.aux);
-            (void)hipStreamWaitEvent(st, w.ev_join, 0);
+            if (armed) (void)hipStreamWaitEvent(st, w.ev_join, 0);
         }
     } pj{w, st};
     if (hp) {
+        if (prev->digests) {  // beside the recheck, on the aux stream (after prev's join)
+            RBC_HIP(hipEventRecord(w.ev_hashed, st));
+            RBC_HIP(hipStreamWaitEvent(w.aux, w.ev_hashed, 0));
+            RBC_HIP(rbc_launch_digest(prev->leaves, (uint64_t)c->n * 32, c->k, prev->status, prev->digests,
+                                      prev->count, w.aux, c->rx_prio));
+        }
+        RBC_HIP(hipEventRecord(w.ev_join, w.aux));  // prev's join (+ digest) done
         pj.armed = true;
         MerkleArgs m{};
         m.count = prev->count;
@@ -921,7 +896,7 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
             ra.branches = prev->branches;
             ra.br_inst_pitch = (uint64_t)c->n * c->depth * 32;
             ra.valid = prev->valid;
-            ra.flags = fl_prev;
+            ra.flags = w.flags.as<uint32_t>();
             ra.vroots = w.vroot[w.rx_vslot].as<uint8_t>();
             ra.expect_roots = prev->roots;
             ra.status = prev->status;
@@ -931,37 +906,24 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
             m.only = ra.need_full;
         }
         RBC_HIP(rbc_launch_merkle(m, true, st));
-        if (marks && marks->prev_released) RBC_HIP(hipEventRecord(w.ev_rel, st));  // the last reader of prev's set on `st`
-    }
-    w.rx_count = 0;  // prev is complete once this call's work on `st` is; cur is pending only on success
-    bool joined = false;
-    if (hc) {
-        if (marks && marks->decode_begin) RBC_HIP(hipEventRecord((hipEvent_t)marks->decode_begin, st));
-        rc = stage_regenerate(c, w, st, cur->count, cur->shards, cur->shard_pitch, cur->shard_lens,
-                              cur->uniform_shard_len, cur->valid, cur->status, 1, r_cnt, cur->values_out,
-                              cur->value_pitch, &joined, fl_cur, prep_aux ? w.aux : nullptr, w.ev_prep_in);
-        if (rc) return rc;
-        if (marks && marks->decoded) RBC_HIP(hipEventRecord((hipEvent_t)marks->decoded, st));
-    }
-    if (hp) {
-        if (prev->digests) {  // on the aux stream (after cur's prepare), beside the recheck / cur's decode
-            if (!prep_aux) {
-                RBC_HIP(hipEventRecord(w.ev_hashed, st));
-                RBC_HIP(hipStreamWaitEvent(w.aux, w.ev_hashed, 0));
-            }
-            RBC_HIP(rbc_launch_digest(prev->leaves, (uint64_t)c->n * 32, c->k, prev->status, prev->digests,
-                                      prev->count, w.aux, c->rx_prio));
-        }
-        RBC_HIP(hipEventRecord(w.ev_join, w.aux));  // prev's join + digest (and cur's prepare) done
-        pj.recorded = true;
         if (marks && marks->prev_released) {
-            // prev's join, digest and recheck are its set's last readers: the
-            // mark completes after all of them, and `st` does not wait for it
+            // the recheck was the last reader of prev's set on `st`; the aux
+            // stream already holds prev's join and digest: the mark completes
+            // after all three, and `st` goes on to cur's decode without waiting
+            RBC_HIP(hipEventRecord(w.ev_rel, st));
             RBC_HIP(hipStreamWaitEvent(w.aux, w.ev_rel, 0));
             RBC_HIP(hipEventRecord((hipEvent_t)marks->prev_released, w.aux));
         }
     }
+    w.rx_count = 0;  // prev is complete once this call's work on `st` is; cur is pending only on success
     if (hc) {
+        if (marks && marks->decode_begin) RBC_HIP(hipEventRecord((hipEvent_t)marks->decode_begin, st));
+        bool joined = false;
+        rc = stage_regenerate(c, w, st, cur->count, cur->shards, cur->shard_pitch, cur->shard_lens,
+                              cur->uniform_shard_len, cur->valid, cur->status, 1, r_cnt, cur->values_out,
+                              cur->value_pitch, &joined);
+        if (rc) return rc;
+        if (marks && marks->decoded) RBC_HIP(hipEventRecord((hipEvent_t)marks->decoded, st));
         if (cur->values_out && !joined) {  // the row view (values_out NULL) has no join; the FFT decode joins
             RBC_HIP(hipEventRecord(w.ev_fork, st));
             RBC_HIP(hipStreamWaitEvent(w.aux, w.ev_fork, 0));
