@@ -611,8 +611,10 @@ void rbc_batcher::v_run() {
                 O->seen = cnt;
                 O->t_seen = now;
             }
-            // idle lane: max_wait from the first message; busy: also max_wait of quiet, or kVTarget bytes
-            wake = queued == 0 ? O->t0 + mw : std::max(O->t0, O->t_seen) + mw;
+            // idle lane: max_wait from the first message; busy: at least max_wait old and
+            // max_wait / 4 without an arrival (a full max_wait of quiet cost 1 k outstanding
+            // validates 11 -> 14 GB/s, tools/gpu_runs/gpu_r05v.sh), or kVTarget bytes
+            wake = queued == 0 ? O->t0 + mw : std::max(O->t0 + mw, O->t_seen + mw / 4);
             const bool big = bytes >= kVTarget && O->t0 + mw <= now;
             if (v_stop || (slot_free && (wake <= now || big))) {
                 lk.unlock();
