@@ -67,3 +67,35 @@ def test_frac_is_achieved_over_peak(path, line):
         ach = r["algorithmic_bytes_per_launch"] / (r["avg_ms"] / 1e3) / 1e9
         assert abs(ach - r["achieved"]) <= 0.002 * ach + 0.1, (path, key)
         assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3, (path, key)
+
+
+def _profiled_pairs():
+    """(line, trace roles) pairs: a bench line of a run made under rocprofv3
+    and the per-role trace summary of that same run (tools/trace_summary.py)."""
+    out = []
+    for tr in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "trace_roles.json"))):
+        m = re.match(r"r(\d+)", os.path.basename(os.path.dirname(tr)))
+        line = os.path.join(os.path.dirname(tr), "prof_default.json")
+        if m and int(m.group(1)) >= 5 and os.path.exists(line):
+            out.append((os.path.relpath(line, ROOT), json.load(open(line)), json.load(open(tr))["roles"]))
+    return out
+
+
+PAIRS = _profiled_pairs()
+
+
+def test_a_profiled_round5_run_is_committed():
+    assert PAIRS, "no profiles/r05*/prof_default.json + trace_roles.json pair"
+
+
+@pytest.mark.parametrize("path,line,roles", PAIRS, ids=[p for p, _, _ in PAIRS])
+def test_live_span_agrees_with_the_rocprof_average(path, line, roles):
+    """The contract's check: the dominant kernel's live span (HIP events in
+    bench.py) and rocprofv3's average duration of the same kernel over the
+    same timed launches agree -- within 5 % (the event span also holds the
+    launch's own enqueue and, under the pipeline, nothing else on its stream)."""
+    for key in ("roofline", "roofline_encode"):
+        r = line[key]
+        tr = roles.get(r["kernel"])
+        assert tr and tr["timed_launches"] >= 20, (path, key, r["kernel"])
+        assert abs(tr["avg_ms"] - r["avg_ms"]) <= 0.05 * r["avg_ms"], (path, key, tr["avg_ms"], r["avg_ms"])
