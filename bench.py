@@ -19,8 +19,15 @@ while the receiver stream runs rbc_dev_receive_step(cur = t-1, prev = t-2);
 --pipeline 0 runs the stages in order on one stream, and is what the bench
 falls back to when the pipeline's shard sets do not fit the HBM this rank
 may use (free device memory / ranks sharing the device).  Interpolate's
-value is the row view (the k data rows of the shard set, no join) unless
---join asks for the assembled k*S-byte value.
+value is the joined form rbc/rbc.go:88 returns (k*S contiguous bytes per
+instance); --row-view times the row view instead (the k data rows of the
+shard set, no join), and a shorter second run reports the other form.
+
+Host-fed leg (every rank, after the device-resident timing; key
+pcie_inclusive, never `value`): one epoch of the rank's instances through the
+C ABI from pinned NUMA-local host memory -- rbc_shard_commit,
+rbc_validate_packed_leaves of every received ECHO and
+rbc_interpolate_batch_verified -- all ranks at once (tools/host_bench.epoch).
 
 Scaling: by default every GPU owns `instances` (weak scaling, as the driver
 runs N = 1, 2, 4, 8).  --total-instances T partitions T instances over the
@@ -88,10 +95,10 @@ def parse_args(argv):
     ap.add_argument("--pipeline", type=int, default=7, choices=(0, 7),
                     help="7: proposer stream commit(t) || receiver stream rbc_dev_receive_step(t-1, t-2); "
                          "0: one stream, stages in order")
-    ap.add_argument("--join", action="store_true",
-                    help="assemble interpolate's value (k*S bytes per instance) instead of the row view")
-    ap.add_argument("--no-joined-leg", action="store_true",
-                    help="skip the secondary timed run in the joined value form (key value_joined)")
+    ap.add_argument("--row-view", action="store_true",
+                    help="time interpolate's row view (the k data rows, no join) instead of the joined value")
+    ap.add_argument("--no-second-form", "--no-joined-leg", dest="no_second_form", action="store_true",
+                    help="skip the secondary timed run in the other value form (key value_row_view / value_joined)")
     ap.add_argument("--faults-on", default="receiver", choices=("receiver", "proposer"),
                     help="stream that injects the corrupted ECHO shards (synthetic input)")
     ap.add_argument("--wave-prio", default="",
@@ -111,7 +118,9 @@ def parse_args(argv):
     ap.add_argument("--cpu-configs", default="c1,c2,c3,c4",
                     help="configs the CPU port is also timed on (the bench config always is)")
     ap.add_argument("--no-pcie", action="store_true",
-                    help="skip the PCIe-inclusive host-path measurement (a secondary key, never `value`)")
+                    help="skip the host-fed (PCIe-inclusive) epoch leg on every rank (secondary key, never `value`)")
+    ap.add_argument("--host-instances", type=int, default=0,
+                    help="instances per rank in the host-fed epoch (default: the rank's, at most 2 GiB of values)")
     ap.add_argument("--no-batcher", action="store_true",
                     help="skip the per-message validate lane sweep (secondary key `batcher`, C2 only, never `value`)")
     ap.add_argument("--rehearse-on-one-gpu", action="store_true",
@@ -121,6 +130,7 @@ def parse_args(argv):
                     help="instances whose root and digest are checked against the C oracle after timing")
     ap.add_argument("--watchdog-scale", type=float, default=1.0, help="multiplies every stage deadline")
     args = ap.parse_args(argv)
+    args.join = not args.row_view
     # checked before any rank starts or touches a GPU
     if args.wave_prio and not _levels_ok(args.wave_prio, ()):
         ap.error("--wave-prio takes two levels 0..3, e.g. 0,2")
@@ -408,16 +418,18 @@ def run(args, world, rank, local_rank, wd, out):
     poisoned = check_batch(args, ca, dev, stream, I, n, k, B, S, spitch, vpitch, opitch, d_values, pset, prb, d_count)
     checks = fold_guard(args, synth, rdz, first, I, total, n, f, k, B, vpitch, checks, timed, poisoned)
 
-    def joined_leg():
-        """The same pipelined step with interpolate's value assembled (k*S
-        contiguous bytes per instance, as rbc/rbc.go:88 returns it) instead of
-        the row view: a shorter second timed run, reported beside `value`."""
-        extra = 2 * I * opitch
-        if need["pipelined"] + extra > plan["budget_bytes"]:
-            return {"skipped": "the joined values do not fit the HBM plan"}
-        for rb in rxb:
-            rb["out"] = mb(I * opitch)
-        form.update(join=True, start=100000)
+    def second_form_leg():
+        """The same pipelined step in the other value form: the row view (the
+        k data rows of the shard set, no join) beside a joined `value`, or
+        the joined value (k*S contiguous bytes per instance, as rbc/rbc.go:88
+        returns it) beside a row-view `value`: a shorter second timed run."""
+        join2 = not args.join
+        if join2:
+            if need["pipelined"] + 2 * I * opitch > plan["budget_bytes"]:
+                return {"skipped": "the joined values do not fit the HBM plan"}
+            for rb in rxb:
+                rb["out"] = mb(I * opitch)
+        form.update(join=join2, start=100000)
         stream.sync()
         rstream.sync()
         steps_j = max(20, args.steps // 3)
@@ -433,19 +445,21 @@ def run(args, world, rank, local_rank, wd, out):
         ctx.dev_receive_step(rstream.ptr, None, cur_j)
         rstream.sync()
         res = check_batch(args, ca, dev, stream, I, n, k, B, S, spitch, vpitch, opitch, d_values, sets[x_j % nsets],
-                          rxb[x_j % 2], d_count, join=True)
+                          rxb[x_j % 2], d_count, join=join2)
         sm = spans(ev_sets[:steps_j], args.faults_on)
         return {"value": round(total * n * S * steps_j / el / 1e9, 3), "unit": "GB/s", "steps": steps_j,
                 "ms_per_step": round(el * 1000.0 / steps_j, 4),
                 "decoded_ok": int((res["status"] == 0).sum()), "values_ok": res["mism"] == 0,
                 "stage_ms": {kk: round(v, 4) for kk, v in sm.items()},
-                "value_form": "joined (k*S contiguous bytes per instance, join_kernel on the aux stream)",
-                "note": "secondary run after the guard, same pipelined schedule; `value` is the row view"}
+                "value_form": "joined (k*S contiguous bytes per instance, assembled by the FFT re-encode)" if join2
+                else "row view (the k data rows of the shard set, no join)",
+                "note": "secondary run after the guard, same pipelined schedule; `value` is the "
+                        + ("row view" if join2 else "joined form")}
 
-    joined = None
-    if pipe and world == 1 and not args.join and not args.no_joined_leg:
-        wd.enter("joined-value leg", 300)
-        joined = joined_leg()
+    second = None
+    if pipe and world == 1 and not args.no_second_form:
+        wd.enter("second value-form leg", 300)
+        second = second_form_leg()
 
     ms_per_step = elapsed_max * 1000.0 / args.steps
     value = total * n * S * args.steps / elapsed_max / 1e9
@@ -460,13 +474,27 @@ def run(args, world, rank, local_rank, wd, out):
             rep["phases"][ph]["cpu_gbs"] = cpu["phases"][ph]
             rep["phases"][ph]["gpu_over_cpu"] = round(rep["phases"][ph]["gpu_gbs"] / cpu["phases"][ph], 1)
     pcie = None
-    if rank == 0 and world == 1 and not args.no_pcie:
-        # what a Go batcher sees with host buffers in and out (pinned rings,
-        # two submissions in flight): PCIe-bound, reported beside `value`
+    if not args.no_pcie:
+        # host feeding is the scaling risk -- every rank runs one
+        # epoch from pinned NUMA-local host memory at once (barrier-bracketed),
+        # after the device-resident timing
+        wd.enter("host-fed epoch", 600)
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         import host_bench
-        pcie = host_bench.measure(ca, n, f, B, batch=64, batches=8, inflight=2, pinned=True, device=dev)
-        pcie["unit"] = "GB/s of committed shard bytes (N*S per instance), host memory in and out"
+        hi = args.host_instances or min(I, max(1, (2 * GiB) // B))
+        sub = max(1, min(hi, int(400e6 // (n * S))))
+        h = host_bench.epoch(ca, n, f, B, instances=hi, sub=sub, device=dev, seed=SEED + 7 + rank,
+                             barrier=rdz.barrier)
+        me["host_fed"] = {kk: h[kk] for kk in ("GBps", "seconds", "instances", "pcie_GBps", "ok")}
+        pcie = host_fed_aggregate(rdz.allgather(h), n, S)
+        pcie.update({
+                "unit": "GB/s of committed shard bytes (N*S per instance), host memory in and out",
+                "path": "one epoch per rank through the C ABI from pinned host memory, all ranks at once: "
+                        "rbc_shard_commit (values in; shards, roots, branches out) || "
+                        "rbc_validate_packed_leaves of every received ECHO (N-f per instance, 10% of instances "
+                        "with one corrupted ECHO; only the received rows cross PCIe) -> "
+                        "rbc_interpolate_batch_verified of the valid ECHOs reusing their leaves (values out)",
+                "aggregate_note": "sum of the ranks' instances x N x S / the slowest rank's epoch seconds"})
     batcher = None
     if rank == 0 and world == 1 and args.config == "c2" and not args.no_batcher:
         wd.enter("batcher sweep", 600)
@@ -488,8 +516,8 @@ def run(args, world, rank, local_rank, wd, out):
                                   + (", RCCL all-gather of {root,digest} records" if gather else ""),
                    "gf_codec": ctx.codec,
                    "wave_priority": {"commit": tx, "receive": rx, "decode_gemv": gv, "decode_reencode": rv},
-                   "value_form": "joined (k*S bytes per instance)" if args.join else
-                                 "row view (the k data rows of the shard set, no join)",
+                   "value_form": "joined (k*S contiguous bytes per instance, the []byte rbc/rbc.go:88 returns)"
+                                 if args.join else "row view (the k data rows of the shard set, no join)",
                    "faults_on": args.faults_on, "hbm_plan": plan,
                    **({"rehearsal": "all ranks on device 0, no RCCL (not a multi-GPU measurement)"}
                       if args.rehearse_on_one_gpu else {}),
@@ -497,12 +525,15 @@ def run(args, world, rank, local_rank, wd, out):
                                 f"recheck(t-2), decode(t-1) (rbc_dev_receive_step), two streams, {nsets} shard "
                                 "sets") if pipe else "serial"},
         **rep, **checks, "cpu_baseline": cpu, "pcie_inclusive": pcie, "rccl": rccl, "ranks": ranks,
-        "rank_skew": skew, "library": ca.rbc.library_path(), "value_joined": joined, "batcher": batcher,
+        "rank_skew": skew, "library": ca.rbc.library_path(), **({"value_row_view": second} if args.join else {"value_joined": second}),
+        "batcher": batcher,
         "host": {kk: host[kk] for kk in ("cpu_model", "nproc", "cgroup_cpu_quota", "affinity_cpus")},
     }
     ok = all(checks[c] for c in ("values_ok", "oracle_sample_ok", "gather_ok")) and checks["decoded_ok"] == total
-    if joined and "value" in joined:  # the joined leg's last batch passes the same value check
-        ok = ok and joined["values_ok"] and joined["decoded_ok"] == I
+    if pcie is not None:  # every rank's host-fed verdicts, values and roots
+        ok = ok and pcie["ok"]
+    if second and "value" in second:  # the second leg's last batch passes the same value check
+        ok = ok and second["values_ok"] and second["decoded_ok"] == I
     wd.leave()
     if not ok:
         print(json.dumps({"error": "correctness check failed", **checks, "library": line["library"]}),
@@ -514,6 +545,20 @@ def run(args, world, rank, local_rank, wd, out):
     rdz.barrier()
     rdz.close()
     return 0
+
+
+def host_fed_aggregate(per, n, S):
+    """The ranks' host-fed epochs (tools/host_bench.epoch results, rank
+    order) -> the job's figure: every rank's committed shard bytes over the
+    slowest rank's epoch (the ranks start together behind a barrier), the
+    per-rank rates, the spread, and whether every rank's checks passed."""
+    el_max = max(x["seconds"] for x in per)
+    rates = [x["GBps"] for x in per]
+    return {"aggregate_GBps": round(sum(x["instances"] for x in per) * n * S / el_max / 1e9, 3),
+            "ranks": len(per), "per_rank_GBps": rates,
+            "slowest_rank": int(np.argmax([x["seconds"] for x in per])),
+            "min_over_max": round(min(rates) / max(rates), 4) if max(rates) > 0 else None,
+            "ok": all(x["ok"] for x in per), "rank0": per[0]}
 
 
 BATCHER_LEVELS = (1024, 8192, 32768, 88064)  # outstanding validates; 88,064 = one C2 epoch (1,024 x 86 ECHOs)
@@ -627,20 +672,23 @@ def report(args, ctx, I, n, k, d, S, present_h, corrupt_h, stage_ms, iso, elapse
     else:
         kern["sha_rows_kernel<verify>"] = ("verify", R * (S + 32 * d + 32 + 1) + I * 32, R * (bps + 2 * d))
     if pipe:
+        # + the joined value the FFT re-encode writes from the data rows it loads (k*S per instance)
         kern["decode: prepare + gf_regen_kernel + rs_fft_kernel<decode>"] = (
-            "decode", decode_bytes(n, k, S, present_h, corrupt_h), 0)
+            "decode", decode_bytes(n, k, S, present_h, corrupt_h) + (I * k * S if args.join else 0), 0)
     pm, pmc_path = {}, None
+    want_form = "joined" if args.join else "row view"
+    cands = []
     for cand in sorted((x for x in os.listdir(os.path.join(ROOT, "profiles")) if x.startswith("pmc_traffic_r")),
                        reverse=True):
         try:
-            pm = json.load(open(os.path.join(ROOT, "profiles", cand)))
+            c = json.load(open(os.path.join(ROOT, "profiles", cand)))
         except (OSError, ValueError):
             continue
-        if pm.get("config") == args.config and pm.get("instances", 1024) == I and \
-                pm.get("value_form", "joined") == ("joined" if args.join else "row view"):
-            pmc_path = os.path.join("profiles", cand)
-            break
-        pm = {}
+        if c.get("config") == args.config and c.get("instances", 1024) == I:
+            cands.append((c.get("value_form", "joined") != want_form, cand, c))
+    if cands:  # the newest file of the timed value form, else of the other form (same SHA / encode kernels)
+        _, cand, pm = min(cands, key=lambda x: x[0])
+        pmc_path = os.path.join("profiles", cand)
     # the loaded clock per kernel, each kernel alone (serial schedule; tools/clock_summary.py)
     clk, clk_path = {}, None
     for cand in sorted((x for x in os.listdir(os.path.join(ROOT, "profiles")) if x.startswith("valu_clock_r")),

@@ -39,7 +39,7 @@ class RxBatch(ctypes.Structure):
     _fields_ = [("count", c_int), ("shards", c_void_p), ("shard_pitch", c_uint32), ("shard_lens", c_void_p),
                 ("uniform_shard_len", c_uint32), ("branches", c_void_p), ("roots", c_void_p),
                 ("present", c_void_p), ("valid", c_void_p), ("leaves", c_void_p), ("values_out", c_void_p),
-                ("value_pitch", c_uint32), ("digests", c_void_p), ("status", c_void_p)]
+                ("value_pitch", c_uint32), ("digests", c_void_p), ("status", c_void_p), ("verified", c_int)]
 
 
 class RxMarks(ctypes.Structure):
@@ -119,6 +119,14 @@ _SIGS = {
     "rbc_batcher_set_validate": (c_int, [c_void_p, c_int, c_size_t]),
     "rbc_validate_packed": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_void_p, POINTER(c_uint64)]),
+    "rbc_validate_packed_leaves": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p,
+                                           c_void_p, c_void_p, c_void_p, c_void_p, POINTER(c_uint64)]),
+    "rbc_interpolate_batch_verified": (c_int, [c_void_p, c_int, c_void_p, c_size_t, szp, c_void_p, c_void_p,
+                                               c_void_p, c_void_p, c_size_t, c_void_p, i32p, POINTER(c_uint64)]),
+    "rbc_batcher_validate_leaf": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_uint32,
+                                          POINTER(c_int), c_void_p, POINTER(c_uint64)]),
+    "rbc_batcher_interpolate_verified": (c_int, [c_void_p, c_void_p, c_void_p, szp, c_void_p, c_void_p, c_size_t,
+                                                 szp, c_void_p, POINTER(c_uint64)]),
     "rbc_rs_new": (c_int, [c_int, c_int, c_int, POINTER(c_void_p)]),
     "rbc_rs_free": (None, [c_void_p]),
     "rbc_rs_encode": (c_int, [c_void_p, c_void_p, szp, c_int]),

@@ -44,7 +44,9 @@
 
 namespace {
 
-enum Kind { K_SHARD = 0, K_VALIDATE = 1, K_INTERP = 2 };
+// K_INTERPV: interpolate with the validate lane's leaves (rbc_batcher_interpolate_verified)
+enum Kind { K_SHARD = 0, K_VALIDATE = 1, K_INTERP = 2, K_INTERPV = 3 };
+constexpr int kKinds = 4;
 
 struct Req {
     uint64_t ticket;
@@ -66,6 +68,7 @@ struct Req {
     size_t value_cap = 0;
     size_t *value_len = nullptr;
     uint8_t *digest_out = nullptr;
+    const uint8_t *leaves = nullptr;  // K_INTERPV: n x 32, the leaves of the present shards
 };
 
 // Per-request copies between the callers' buffers and a launch's pinned
@@ -112,7 +115,7 @@ struct Pinned {
 
 // The pinned buffers of one launch: shards, roots, branches / values.
 struct PinnedSet {
-    Pinned shards, roots, br, values;
+    Pinned shards, roots, br, values, leaves;
 };
 
 // One arena of the validate lane: the messages of one launch in the layout
@@ -123,8 +126,10 @@ struct VBuf {
     Pinned arena, meta;
     uint64_t *offs = nullptr;
     uint32_t *lens = nullptr;
-    uint8_t *roots = nullptr, *br = nullptr, *idx = nullptr, *ok = nullptr, *shape = nullptr;
+    uint8_t *roots = nullptr, *br = nullptr, *idx = nullptr, *ok = nullptr, *shape = nullptr, *lv = nullptr;
     std::vector<int *> out;
+    std::vector<uint8_t *> lout;     // callers' leaf_out (rbc_batcher_validate_leaf), nullable
+    std::atomic<bool> any_leaf{false};  // some slot asked for its leaf (set before the caller's pend add)
     int cap = 0;                     // messages the meta block holds
     // Copies done, then at seal time + (kSealed - count): == kSealed exactly
     // when the arena is sealed and every reserved slot copied.  One atomic
@@ -150,7 +155,7 @@ struct VBuf {
     uint64_t ticket = 0;
     int rc = RBC_OK;
     bool layout(int msgs, int bslot) {  // the meta block for `msgs` messages
-        const size_t per = 8 + 4 + 32 + (size_t)bslot + 3;
+        const size_t per = 8 + 4 + 32 + (size_t)bslot + 3 + 32;
         if (!meta.ensure((size_t)msgs * per)) return false;
         uint8_t *p = meta.p;
         offs = reinterpret_cast<uint64_t *>(p);
@@ -160,8 +165,10 @@ struct VBuf {
         idx = br + (size_t)msgs * bslot;
         ok = idx + msgs;
         shape = ok + msgs;
+        lv = shape + msgs;  // [msgs][32] leaves (only when a slot asked for one)
         cap = msgs;
         out.assign(msgs, nullptr);
+        lout.assign(msgs, nullptr);
         return true;
     }
 };
@@ -177,7 +184,7 @@ struct rbc_batcher {
     int max_wait_us = 200;
     std::mutex mu;
     std::condition_variable cv_work;
-    std::deque<Req> q[3];
+    std::deque<Req> q[kKinds];
     // Completed tickets -> status, sharded by ticket so that the callers'
     // waits and polls (one per request, from many threads) and the worker's
     // completions contend per shard, not on the queue lock, and a finished
@@ -235,6 +242,19 @@ struct rbc_batcher {
 };
 
 namespace {
+
+inline size_t round_up64(size_t x) { return (x + 63) / 64 * 64; }
+
+// spin-wait hint of v_reserve's retry (host code a cgo build links on any ISA)
+inline void cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_ia32_pause();
+#elif defined(__aarch64__)
+    asm volatile("yield");
+#else
+    std::this_thread::yield();
+#endif
+}
 
 int check_shards_sizes(const std::vector<size_t> &lens, size_t *S) {
     size_t size = 0;
@@ -319,11 +339,12 @@ std::unique_ptr<Pending> rbc_batcher::submit(Kind kind, std::vector<Req> &&batch
             P->shards = P->pin->shards.ensure((size_t)m * n * Smax);
             P->roots = P->pin->roots.ensure((size_t)m * 32);
             P->values = P->pin->values.ensure((size_t)m * k * Smax);
+            uint8_t *lv = kind == K_INTERPV ? P->pin->leaves.ensure((size_t)m * n * 32) : nullptr;
             P->present.assign((size_t)m * n, 0);
             P->digests.resize((size_t)m * 32);
             P->lens.resize(m);
             P->status.assign(m, 0);
-            if (!P->shards || !P->roots || !P->values) {
+            if (!P->shards || !P->roots || !P->values || (kind == K_INTERPV && !lv)) {
                 P->rc = RBC_ERR_DEVICE;
                 return P;
             }
@@ -336,12 +357,13 @@ std::unique_ptr<Pending> rbc_batcher::submit(Kind kind, std::vector<Req> &&batch
                         memcpy(row, r.in_shards[j], P->lens[t]);
                         if (P->lens[t] < Smax) memset(row + P->lens[t], 0, Smax - P->lens[t]);
                         P->present[(size_t)t * n + j] = 1;
+                        if (lv) memcpy(lv + ((size_t)t * n + j) * 32, r.leaves + (size_t)j * 32, 32);
                     }
                 memcpy(P->roots + (size_t)t * 32, r.root, 32);
             });
-            P->rc = rbc_interpolate_batch(ctx, m, P->shards, Smax, P->lens.data(), P->present.data(), P->roots,
-                                          P->values, (size_t)k * Smax, P->digests.data(), P->status.data(),
-                                          &P->ticket);
+            P->rc = rbc_interpolate_batch_verified(ctx, m, P->shards, Smax, P->lens.data(), P->present.data(), lv,
+                                                   P->roots, P->values, (size_t)k * Smax, P->digests.data(),
+                                                   P->status.data(), &P->ticket);
         }
     }
     return P;
@@ -408,7 +430,7 @@ void rbc_batcher::run() {
         const auto now = std::chrono::steady_clock::now();
         int pick = -1;
         auto earliest = now + std::chrono::hours(1);
-        for (int kd = 0; kd < 3; ++kd) {
+        for (int kd = 0; kd < kKinds; ++kd) {
             if (q[kd].empty()) continue;
             const auto due = q[kd].front().t0 + std::chrono::microseconds(max_wait_us);
             if ((int)q[kd].size() >= max_batch || due <= now || stop) { pick = kd; break; }
@@ -486,7 +508,7 @@ int rbc_batcher::v_reserve(size_t need, VBuf **out, int *slot, size_t *off) {
             const uint64_t w = B->word.fetch_add(VBuf::kCountOne | need);
             const uint64_t oc = w >> 40, ob = w & VBuf::kBytesMask;
             if (oc >= (uint64_t)B->cap) {  // sealed, or full and being sealed: the next arena
-                __builtin_ia32_pause();
+                cpu_relax();
                 continue;
             }
             if (ob + need <= B->arena.cap) {
@@ -499,6 +521,7 @@ int rbc_batcher::v_reserve(size_t need, VBuf **out, int *slot, size_t *off) {
             }
             // no room for these bytes: slot oc is launched as an empty message
             B->out[oc] = nullptr;
+            B->lout[oc] = nullptr;
             B->offs[oc] = 0;
             B->lens[oc] = 1;
             B->idx[oc] = 0;
@@ -538,6 +561,7 @@ int rbc_batcher::v_reserve(size_t need, VBuf **out, int *slot, size_t *off) {
         f->word.store(VBuf::kCountOne | need);
         f->rc = RBC_OK;
         f->ticket = 0;
+        f->any_leaf.store(false);
         f->t0 = f->t_seen = std::chrono::steady_clock::now();  // max_wait runs from the first message
         f->seen = 1;
         *out = f;
@@ -557,8 +581,8 @@ int rbc_batcher::v_reserve(size_t need, VBuf **out, int *slot, size_t *off) {
 }
 
 void rbc_batcher::v_launch(VBuf *B) {
-    B->rc = B->count ? rbc_validate_packed(ctx, B->count, B->arena.p, B->bytes, B->offs, B->lens, B->idx, B->br,
-                                           B->roots, B->ok, &B->ticket)
+    B->rc = B->count ? rbc_validate_packed_leaves(ctx, B->count, B->arena.p, B->bytes, B->offs, B->lens, B->idx,
+                                                  B->br, B->roots, B->ok, B->any_leaf.load() ? B->lv : nullptr, &B->ticket)
                      : RBC_OK;
     if (B->rc) B->ticket = 0;
 }
@@ -569,7 +593,9 @@ void rbc_batcher::v_complete(VBuf *B) {
     int real = 0;
     for (int i = 0; i < B->count; ++i)
         if (B->out[i]) {  // holes have no caller
-            *B->out[i] = (!rc && B->shape[i]) ? B->ok[i] : 0;
+            const int ok = (!rc && B->shape[i]) ? B->ok[i] : 0;
+            if (ok && B->lout[i]) memcpy(B->lout[i], B->lv + (size_t)i * 32, 32);
+            *B->out[i] = ok;
             ++real;
         }
     std::lock_guard<std::mutex> lk(vmu);
@@ -748,6 +774,12 @@ int rbc_batcher_shard(rbc_batcher *b, const uint8_t *data, size_t len, uint8_t *
 
 int rbc_batcher_validate(rbc_batcher *b, const uint8_t *root, const uint8_t *branch, size_t branch_len,
                          const uint8_t *shard, size_t shard_len, uint32_t index, int *ok_out, uint64_t *ticket) {
+    return rbc_batcher_validate_leaf(b, root, branch, branch_len, shard, shard_len, index, ok_out, nullptr, ticket);
+}
+
+int rbc_batcher_validate_leaf(rbc_batcher *b, const uint8_t *root, const uint8_t *branch, size_t branch_len,
+                              const uint8_t *shard, size_t shard_len, uint32_t index, int *ok_out, uint8_t *leaf_out,
+                              uint64_t *ticket) {
     if (!b || !ticket || !ok_out || !root) return RBC_ERR_INVALID_ARG;
     *ok_out = 0;
     const int n = b->n, d = b->depth;
@@ -761,6 +793,25 @@ int rbc_batcher_validate(rbc_batcher *b, const uint8_t *root, const uint8_t *bra
         const uint8_t *sh = shard, *bp = branch, *rp = root;
         const int rc = rbc_validate_batch(b->ctx, 1, &sh, &shard_len, &index, &bp, &branch_len, &rp, &ok, nullptr);
         if (rc) return rc;
+        if (ok && leaf_out) {  // the leaf of a message larger than an arena: a packed launch of one
+            uint8_t *tmp = nullptr;
+            void *q = nullptr;
+            if (rbc_host_alloc(round_up64(shard_len) + 64, &q) != RBC_OK) return RBC_ERR_DEVICE;
+            tmp = static_cast<uint8_t *>(q);
+            memcpy(tmp, shard, shard_len);
+            uint8_t brd[32 * 8] = {0}, okp = 0;
+            const int n = b->n, d = b->depth;
+            const bool e0 = d > 0 && (index ^ 1u) >= (uint32_t)n;
+            for (int l = 0, o = 0; l < d; ++l)
+                if (!(l == 0 && e0)) { memcpy(brd + 32 * l, branch + o, 32); o += 32; }
+            const uint64_t off0 = 0;
+            const uint32_t ln = (uint32_t)shard_len;
+            const uint8_t ix = (uint8_t)index;
+            int rc2 = rbc_validate_packed_leaves(b->ctx, 1, tmp, round_up64(shard_len), &off0, &ln, &ix, brd, root,
+                                                 &okp, leaf_out, nullptr);
+            rbc_host_free(tmp);
+            if (rc2) return rc2;
+        }
         *ok_out = ok;
         *ticket = kVTicket | 1;  // generation 0: already complete
         std::lock_guard<std::mutex> lk(b->vmu);
@@ -776,6 +827,9 @@ int rbc_batcher_validate(rbc_batcher *b, const uint8_t *root, const uint8_t *bra
     // the copy runs on the calling thread, outside the lock
     uint8_t *row = B->arena.p + off, *br = B->br + (size_t)slot * b->bslot;
     B->out[slot] = ok_out;
+    B->lout[slot] = leaf_out;
+    if (leaf_out && !B->any_leaf.load(std::memory_order_relaxed))
+        B->any_leaf.store(true);  // before this slot's pend add: the launch sees it
     B->offs[slot] = off;
     B->shape[slot] = shape_ok;
     if (shape_ok) {
@@ -819,6 +873,24 @@ int rbc_batcher_interpolate(rbc_batcher *b, const uint8_t *root, const uint8_t *
     r.root = root;
     r.in_shards.assign(shards, shards + b->n);
     r.in_lens.assign(lens, lens + b->n);
+    r.value_out = value_out;
+    r.value_cap = value_cap;
+    r.value_len = value_len;
+    r.digest_out = digest_out;
+    *ticket = enqueue(b, std::move(r));
+    return RBC_OK;
+}
+
+int rbc_batcher_interpolate_verified(rbc_batcher *b, const uint8_t *root, const uint8_t *const *shards,
+                                     const size_t *lens, const uint8_t *leaves, uint8_t *value_out, size_t value_cap,
+                                     size_t *value_len, uint8_t *digest_out, uint64_t *ticket) {
+    if (!b || !ticket || !root || !shards || !lens || !value_out || !leaves) return RBC_ERR_INVALID_ARG;
+    Req r;
+    r.kind = K_INTERPV;
+    r.root = root;
+    r.in_shards.assign(shards, shards + b->n);
+    r.in_lens.assign(lens, lens + b->n);
+    r.leaves = leaves;
     r.value_out = value_out;
     r.value_cap = value_cap;
     r.value_len = value_len;

@@ -554,8 +554,11 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
             a.counter = pa.counter;
         }
         a.prio = c->reencode_prio();
+        // tile 0's lanes zero the value's tail, 4 B each, and only the lanes
+        // with a column inside the row pitch run (rs_fft.hip): the tail must
+        // fit min(256, shard_pitch) bytes, else the separate join zero-fills it
         if (values_out && joined && !shard_lens && value_pitch >= (uint64_t)c->k * uniform_shard_len &&
-            value_pitch - (uint64_t)c->k * uniform_shard_len <= 256) {
+            value_pitch - (uint64_t)c->k * uniform_shard_len <= std::min<uint64_t>(256, shard_pitch)) {
             a.join = values_out;
             a.join_pitch = value_pitch;
             *joined = true;
@@ -781,7 +784,8 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
     const int cur_vslot = w.rx_vslot ^ (hp ? 1 : 0);
     bool roots_kept = false;
     if (hc && reuse) RBC_HIP(w.vroot[cur_vslot].ensure((size_t)cur->count * 32));
-    if (hc) {
+    const bool hv = hc && !cur->verified;  // cur's ECHOs still to verify in this step
+    if (hv) {
         v.count = cur->count;
         v.rows_per_inst = c->n;
         v.rows = cur->shards;
@@ -831,10 +835,12 @@ int stage_receive_step(rbc_ctx *c, hipStream_t st, const rbc_rx_batch *cur, cons
     if (hc && reuse && !roots_kept)  // no compaction to carry the copy
         RBC_HIP(hipMemcpyAsync(w.vroot[cur_vslot].p, cur->roots, (size_t)cur->count * 32, hipMemcpyDeviceToDevice, st));
     if (marks && marks->hash_begin) RBC_HIP(hipEventRecord((hipEvent_t)marks->hash_begin, st));
+    // (a verified cur leaves only prev's regen rows; with neither side the
+    // launch still zeroes the next users' counters)
     RBC_HIP(rbc_launch_sha_rx(v, r, v_walk, st, reinterpret_cast<uint4 *>(r_cnt), reinterpret_cast<uint4 *>(v_next)));
     w.v_clean[par ^ 1] = true;
     if (marks && marks->rows_hashed) RBC_HIP(hipEventRecord((hipEvent_t)marks->rows_hashed, st));
-    if (hc && v_path) {
+    if (hv && v_path) {
         PathArgs p{};
         p.count = cur->count;
         p.n = c->n;
@@ -1759,18 +1765,32 @@ int rbc_validate_batch(rbc_ctx *c, int count, const uint8_t *const *shards, cons
 int rbc_validate_packed(rbc_ctx *c, int count, const uint8_t *arena, size_t arena_bytes, const uint64_t *offs,
                         const uint32_t *lens, const uint8_t *idx, const uint8_t *branches, const uint8_t *roots,
                         uint8_t *ok_out, uint64_t *ticket) {
+    return rbc_validate_packed_leaves(c, count, arena, arena_bytes, offs, lens, idx, branches, roots, ok_out, nullptr,
+                                      ticket);
+}
+
+int rbc_validate_packed_leaves(rbc_ctx *c, int count, const uint8_t *arena, size_t arena_bytes, const uint64_t *offs,
+                               const uint32_t *lens, const uint8_t *idx, const uint8_t *branches, const uint8_t *roots,
+                               uint8_t *ok_out, uint8_t *leaves_out, uint64_t *ticket) {
     if (!c || count < 0 ||
         (count > 0 && (!arena || !arena_bytes || !offs || !lens || !idx || !branches || !roots || !ok_out)))
         return RBC_ERR_INVALID_ARG;
     if (count == 0) { if (ticket) *ticket = 0; return RBC_OK; }
     // every message's 64-B blocks must lie inside the arena (the kernel reads
     // whole blocks) and its leaf index inside the tree
-    for (int i = 0; i < count; ++i)
+    size_t named = 0;  // arena bytes the messages cover
+    for (int i = 0; i < count; ++i) {
         if (offs[i] % 64 || lens[i] == 0 || offs[i] > arena_bytes ||
             round_up((size_t)lens[i], 64) > arena_bytes - offs[i] || idx[i] >= c->n)  // no wrap-around
             return RBC_ERR_INVALID_ARG;
+        named += round_up((size_t)lens[i], 64);
+    }
     const int d = c->depth;
     const size_t bslot = (size_t)std::max(d, 1) * 32;
+    // a sparse arena in pinned memory (a receiver's [count][N][pitch] ECHO
+    // buffer naming only the received rows): gather the named bytes over PCIe
+    // instead of moving the whole arena
+    const uint8_t *zc = named < arena_bytes / 4 * 3 ? host_zero_copy(arena, arena_bytes) : nullptr;
     std::lock_guard<std::mutex> lk(c->mu);
     RBC_HIP(hipSetDevice(c->device));
     Slot *sp = acquire_slot(c);
@@ -1784,9 +1804,14 @@ int rbc_validate_packed(rbc_ctx *c, int count, const uint8_t *arena, size_t aren
     RBC_HIP(s.d_idx.ensure((size_t)count));
     RBC_HIP(s.d_offs.ensure((size_t)count * 8));
     RBC_HIP(s.d_valid.ensure((size_t)count));
-    RBC_HIP(hipMemcpyAsync(s.d_shards.p, arena, arena_bytes, hipMemcpyHostToDevice, st));
+    if (leaves_out) RBC_HIP(s.d_leaves.ensure((size_t)count * 32));
     RBC_HIP(hipMemcpyAsync(s.d_offs.p, offs, (size_t)count * 8, hipMemcpyHostToDevice, st));
     RBC_HIP(hipMemcpyAsync(s.d_slens.p, lens, (size_t)count * 4, hipMemcpyHostToDevice, st));
+    if (zc)
+        RBC_HIP(rbc_launch_gather_msgs(zc, s.d_offs.as<uint64_t>(), s.d_slens.as<uint32_t>(), (uint32_t)count,
+                                       s.d_shards.as<uint8_t>(), st));
+    else
+        RBC_HIP(hipMemcpyAsync(s.d_shards.p, arena, arena_bytes, hipMemcpyHostToDevice, st));
     RBC_HIP(hipMemcpyAsync(s.d_idx.p, idx, (size_t)count, hipMemcpyHostToDevice, st));
     RBC_HIP(hipMemcpyAsync(s.d_branches.p, branches, (size_t)count * bslot, hipMemcpyHostToDevice, st));
     RBC_HIP(hipMemcpyAsync(s.d_roots.p, roots, (size_t)count * 32, hipMemcpyHostToDevice, st));
@@ -1806,10 +1831,15 @@ int rbc_validate_packed(rbc_ctx *c, int count, const uint8_t *arena, size_t aren
     a.roots = s.d_roots.as<uint8_t>();
     a.valid = s.d_valid.as<uint8_t>();
     a.prio = c->rx_prio;
+    if (leaves_out) {  // the message's SHA-256 leaf, [count][32] (interpolate_batch_verified reuses it)
+        a.leaves = s.d_leaves.as<uint8_t>();
+        a.leaves_inst_pitch = 32;
+    }
     RBC_HIP(rbc_launch_sha_rows(a, true, st));
-    void *d_valid = s.d_valid.p;
+    void *d_valid = s.d_valid.p, *d_lv = s.d_leaves.p;
     auto d2h = [=]() -> int {  // behind the next submission's H2D (Slot::d2h)
         RBC_HIP(hipMemcpyAsync(ok_out, d_valid, (size_t)count, hipMemcpyDeviceToHost, st));
+        if (leaves_out) RBC_HIP(hipMemcpyAsync(leaves_out, d_lv, (size_t)count * 32, hipMemcpyDeviceToHost, st));
         return RBC_OK;
     };
     return submit(c, s, ticket, []() { return RBC_OK; }, d2h);
@@ -1819,6 +1849,18 @@ int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t s
                           const size_t *shard_lens, const uint8_t *present, const uint8_t *roots,
                           uint8_t *values_out, size_t value_pitch, uint8_t *digests_out, int32_t *status_out,
                           uint64_t *ticket) {
+    return rbc_interpolate_batch_verified(c, count, shards, shard_pitch, shard_lens, present, nullptr, roots,
+                                          values_out, value_pitch, digests_out, status_out, ticket);
+}
+
+// leaves != NULL: the present rows were validated (rbc_validate_packed_leaves
+// / the batcher's validate lane) and leaves[i][j] holds their SHA-256, so the
+// device hashes only the rows interpolate regenerates (or finds changed) --
+// as rbc_dev_receive_step does -- instead of all N
+int rbc_interpolate_batch_verified(rbc_ctx *c, int count, const uint8_t *shards, size_t shard_pitch,
+                                   const size_t *shard_lens, const uint8_t *present, const uint8_t *leaves,
+                                   const uint8_t *roots, uint8_t *values_out, size_t value_pitch,
+                                   uint8_t *digests_out, int32_t *status_out, uint64_t *ticket) {
     if (!c || count < 0 ||
         (count > 0 && (!shards || !shard_lens || !present || !roots || !values_out || !status_out)))
         return RBC_ERR_INVALID_ARG;
@@ -1892,10 +1934,13 @@ int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t s
     memcpy(i_rt, roots, (size_t)count * 32);
     RBC_HIP(hipMemcpyAsync(s.d_roots.p, i_rt, (size_t)count * 32, hipMemcpyHostToDevice, st));
     RBC_HIP(hipMemcpyAsync(s.d_slens.p, ln, (size_t)count * 4, hipMemcpyHostToDevice, st));
+    if (leaves)  // 32 B per row (1/744 of a C2 row): the whole [count][n][32] block in one copy
+        RBC_HIP(hipMemcpyAsync(s.d_leaves.p, leaves, (size_t)count * n * 32, hipMemcpyHostToDevice, st));
     // ragged batch: bytes past k*S_i of a value row are returned as zero
     RBC_HIP(hipMemsetAsync(s.d_values.p, 0, (size_t)count * vpitch, st));
     int rc = stage_interpolate(c, s.ws, st, count, s.d_shards.as<uint8_t>(), (uint32_t)dpitch,
-                               s.d_slens.as<uint32_t>(), 0, s.d_valid.as<uint8_t>(), s.d_leaves.as<uint8_t>(), 0,
+                               s.d_slens.as<uint32_t>(), 0, s.d_valid.as<uint8_t>(), s.d_leaves.as<uint8_t>(),
+                               leaves ? 1 : 0,
                                s.d_roots.as<uint8_t>(), s.d_values.as<uint8_t>(), (uint32_t)vpitch,
                                s.d_digests.as<uint8_t>(), s.d_status.as<int32_t>());
     if (rc) return rc;

@@ -246,6 +246,10 @@ hipError_t rbc_launch_fill_random(uint8_t *dst, uint64_t first_row, uint64_t row
 // present rows of a pinned host batch -> device rows (zero-copy reads), absent rows zeroed
 hipError_t rbc_launch_gather_present(const uint8_t *host, uint64_t hpitch, uint32_t S, const uint8_t *present,
                                      uint8_t *dev, uint32_t dpitch, uint32_t rows, hipStream_t st);
+// the messages of a pinned validate arena -> the same offsets of a device arena
+// (zero-copy reads of bytes [offs[i], offs[i] + lens[i]) only; the rest untouched)
+hipError_t rbc_launch_gather_msgs(const uint8_t *host, const uint64_t *offs, const uint32_t *lens, uint32_t count,
+                                  uint8_t *dev, hipStream_t st);
 hipError_t rbc_launch_count_mismatch(const uint8_t *a, uint64_t a_pitch, const uint8_t *b, uint64_t b_pitch,
                                      uint64_t rows, uint64_t len, uint32_t *counter, hipStream_t st);
 hipError_t rbc_launch_count_mismatch_rows(const uint8_t *shards, uint64_t inst_pitch, uint32_t row_pitch, int k,

@@ -1751,9 +1751,42 @@ __global__ __launch_bounds__(256) void gather_present_kernel(const uint8_t *host
     }
 }
 
+// Validate lane over a SPARSE pinned arena (rbc_validate_packed): a receiver
+// whose ECHO rows sit at their leaf positions in a [count][N][pitch] buffer
+// names only the received rows (offs), so only those bytes cross PCIe instead
+// of one DMA of the whole arena.  Same zero-copy read as gather_present; the
+// device copy keeps the host offsets (the SHA kernel reads rows by offs), and
+// bytes past a message's length inside its last 64-B block stay unwritten
+// (sha256_row masks them).  offs / lens are device copies.
+__global__ __launch_bounds__(256) void gather_msgs_kernel(const uint8_t *host, const uint64_t *offs,
+                                                          const uint32_t *lens, uint32_t count, uint8_t *dev) {
+    for (uint32_t m = blockIdx.x; m < count; m += gridDim.x) {
+        const uint64_t off = offs[m];
+        const uint32_t S = lens[m];
+        const uint8_t *row = host + off;
+        uint4 *dst = reinterpret_cast<uint4 *>(dev + off);
+        const rsrc_t src = make_rsrc(row, S);
+        const uint32_t full = S / 16;
+        for (uint32_t c = threadIdx.x; c < full; c += blockDim.x) dst[c] = bload16(src, 16u * c);
+        if (threadIdx.x == 0 && (S & 15u)) {  // the last partial chunk, byte by byte (never past S)
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+            for (uint32_t b = 0; b < (S & 15u); ++b) w[b >> 2] |= (uint32_t)row[16u * full + b] << (8 * (b & 3));
+            dst[full] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+    }
+}
+
 // ============================================================================
 // launchers
 // ============================================================================
+hipError_t rbc_launch_gather_msgs(const uint8_t *host, const uint64_t *offs, const uint32_t *lens, uint32_t count,
+                                  uint8_t *dev, hipStream_t st) {
+    if (count == 0) return hipSuccess;
+    const uint32_t blocks = std::min(count, 64u);  // as gather_present: enough PCIe reads in flight
+    hipLaunchKernelGGL(gather_msgs_kernel, dim3(blocks), dim3(256), 0, st, host, offs, lens, count, dev);
+    return hipGetLastError();
+}
+
 hipError_t rbc_launch_compact_present(const uint8_t *present, int n, int count, uint8_t *valid, uint32_t *list,
                                      uint32_t *counter, hipStream_t st, int prio, const uint8_t *roots_src,
                                      uint8_t *roots_dst) {

@@ -418,35 +418,57 @@ class Context:
         return ok.astype(bool)
 
     def validate_packed(self, arena: np.ndarray, offs, lens, idx, branches: np.ndarray, roots: np.ndarray,
-                        arena_bytes: Optional[int] = None) -> np.ndarray:
+                        arena_bytes: Optional[int] = None, leaves: bool = False):
         """rbc_validate_packed: message i is arena[offs[i] : offs[i] + lens[i]]
         (offs[i] % 64 == 0), its branch branches[i] in the device form
         [depth][32], its root roots[i], its leaf index idx[i]; waits and returns
-        the verdicts."""
+        the verdicts (and, leaves=True, the [count][32] message leaves of
+        rbc_validate_packed_leaves)."""
+        return self.validate_packed_submit(arena, offs, lens, idx, branches, roots, arena_bytes, leaves).wait()
+
+    def validate_packed_submit(self, arena: np.ndarray, offs, lens, idx, branches: np.ndarray, roots: np.ndarray,
+                               arena_bytes: Optional[int] = None, leaves: bool = False,
+                               out: Optional[dict] = None) -> "HostTicket":
+        """Asynchronous rbc_validate_packed_leaves; .wait() returns the verdicts
+        (bool array) or, leaves=True, (verdicts, leaves [count][32]).  `out` may
+        hold preallocated (pinned) "ok" [count] and "leaves" [count][32] arrays."""
         count = len(offs)
-        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        arena = arena if (isinstance(arena, np.ndarray) and arena.dtype == np.uint8 and arena.flags.c_contiguous) \
+            else np.ascontiguousarray(arena, dtype=np.uint8)
         o = np.ascontiguousarray(offs, dtype=np.uint64)
         ln = np.ascontiguousarray(lens, dtype=np.uint32)
         ix = np.ascontiguousarray(idx, dtype=np.uint8)
         br = np.ascontiguousarray(branches, dtype=np.uint8)
         rt = np.ascontiguousarray(roots, dtype=np.uint8)
-        ok = np.zeros(max(count, 1), dtype=np.uint8)
+        ok = out["ok"] if out else np.zeros(max(count, 1), dtype=np.uint8)
+        lv = (out["leaves"] if out else np.zeros((max(count, 1), 32), dtype=np.uint8)) if leaves else None
         t = c_uint64(0)
-        check(lib.rbc_validate_packed(self._p, count, _ptr(arena), arena.nbytes if arena_bytes is None else arena_bytes,
-                                      _ptr(o), _ptr(ln), _ptr(ix), _ptr(br), _ptr(rt), _ptr(ok), byref(t)),
-              "rbc_validate_packed")
-        if t.value:
-            check(lib.rbc_wait(self._p, t.value))
-        return ok[:count].astype(bool)
+        check(lib.rbc_validate_packed_leaves(self._p, count, _ptr(arena),
+                                             arena.nbytes if arena_bytes is None else arena_bytes, _ptr(o), _ptr(ln),
+                                             _ptr(ix), _ptr(br), _ptr(rt), _ptr(ok),
+                                             _ptr(lv) if leaves else None, byref(t)), "rbc_validate_packed_leaves")
+
+        class _V(HostTicket):
+            def wait(self_):
+                if self_.ticket and self_._keep is not None:
+                    check(lib.rbc_wait(self._p, self_.ticket), "rbc_wait")
+                self_._keep = None
+                v = ok[:count].astype(bool)
+                return (v, lv[:count]) if leaves else v
+        return _V(self, t.value, None, keep=(arena, o, ln, ix, br, rt, ok, lv))
 
     def interpolate_batch(self, shards: np.ndarray, shard_lens, present: np.ndarray, roots: np.ndarray,
-                          values_out: Optional[np.ndarray] = None) -> dict:
-        return self.interpolate_submit(shards, shard_lens, present, roots, values_out).wait()
+                          values_out: Optional[np.ndarray] = None, leaves: Optional[np.ndarray] = None) -> dict:
+        return self.interpolate_submit(shards, shard_lens, present, roots, values_out, leaves).wait()
 
     def interpolate_submit(self, shards: np.ndarray, shard_lens, present: np.ndarray, roots: np.ndarray,
-                           values_out: Optional[np.ndarray] = None) -> "HostTicket":
+                           values_out: Optional[np.ndarray] = None, leaves: Optional[np.ndarray] = None,
+                           digests_out: Optional[np.ndarray] = None,
+                           status_out: Optional[np.ndarray] = None) -> "HostTicket":
         """Asynchronous rbc_interpolate_batch: returns at once; .wait()
-        completes it (values, digests, status land in the returned arrays)."""
+        completes it (values, digests, status land in the returned arrays).
+        leaves [count][n][32] (the present rows' SHA-256 from
+        validate_packed(leaves=True)) selects rbc_interpolate_batch_verified."""
         shards = np.ascontiguousarray(shards, dtype=np.uint8)
         count, n, pitch = shards.shape
         assert n == self.n
@@ -460,14 +482,20 @@ class Context:
             assert values.shape == (count, max(vp, 1)) and values.dtype == np.uint8
         else:
             values = np.zeros((count, max(vp, 1)), dtype=np.uint8)
-        digests = np.zeros((count, 32), dtype=np.uint8)
-        status = np.zeros(count, dtype=np.int32)
+        digests = np.zeros((count, 32), dtype=np.uint8) if digests_out is None else digests_out
+        status = np.zeros(count, dtype=np.int32) if status_out is None else status_out
+        lv = None
+        if leaves is not None:
+            lv = leaves if (leaves.dtype == np.uint8 and leaves.flags.c_contiguous) else \
+                np.ascontiguousarray(leaves, dtype=np.uint8)
+            assert lv.size == count * self.n * 32
         t = c_uint64(0)
-        check(lib.rbc_interpolate_batch(self._p, count, _ptr(shards), pitch, sl, _ptr(present), _ptr(roots),
-                                        _ptr(values), values.shape[1], _ptr(digests),
-                                        status.ctypes.data_as(_lib.i32p), byref(t)), "rbc_interpolate_batch")
+        check(lib.rbc_interpolate_batch_verified(self._p, count, _ptr(shards), pitch, sl, _ptr(present),
+                                                 _ptr(lv) if lv is not None else None, _ptr(roots), _ptr(values),
+                                                 values.shape[1], _ptr(digests), status.ctypes.data_as(_lib.i32p),
+                                                 byref(t)), "rbc_interpolate_batch_verified")
         out = {"values": values, "digests": digests, "status": status}
-        return HostTicket(self, t.value, out, keep=(shards, present, roots, sl))
+        return HostTicket(self, t.value, out, keep=(shards, present, roots, sl, lv))
 
     # ---- device-resident stages --------------------------------------------
     def dev_encode(self, stream, count, values, value_pitch, value_lens, uniform_len, shards, shard_pitch):
@@ -503,13 +531,15 @@ class Context:
 
     @staticmethod
     def rx_batch(count, shards, shard_pitch, shard_lens, uniform_len, branches, roots, present, valid, leaves,
-                 values_out, value_pitch, digests, status) -> "_lib.RxBatch":
-        """An rbc_rx_batch of device buffers (DeviceBuffer / int / None)."""
+                 values_out, value_pitch, digests, status, verified=False) -> "_lib.RxBatch":
+        """An rbc_rx_batch of device buffers (DeviceBuffer / int / None);
+        verified=True: valid / leaves already hold rbc_dev_verify's output."""
         def v(x):
             p = _dv(x)
             return p.value if isinstance(p, c_void_p) else p
         return _lib.RxBatch(count, v(shards), shard_pitch, v(shard_lens), uniform_len, v(branches), v(roots),
-                            v(present), v(valid), v(leaves), v(values_out), value_pitch, v(digests), v(status))
+                            v(present), v(valid), v(leaves), v(values_out), value_pitch, v(digests), v(status),
+                            1 if verified else 0)
 
     def dev_receive_step(self, stream, cur=None, prev=None, hashed=None, decode_begin=None, decoded=None,
                          hash_begin=None, rows_hashed=None, prev_released=None) -> None:
@@ -705,15 +735,22 @@ class Batcher:
               "rbc_batcher_shard")
         return h
 
-    def submit_validate(self, root, branch, shard, index) -> dict:
+    def submit_validate(self, root, branch, shard, index, leaf: bool = False) -> dict:
+        """validateMessage through the lane; leaf=True also returns the shard's
+        SHA-256 leaf (rbc_batcher_validate_leaf) for submit_interpolate(leaves=)."""
         r, b, s = _bytes_array(root).copy(), _bytes_array(branch).copy(), _bytes_array(shard).copy()
-        h = {"kind": "validate", "r": r, "b": b, "s": s, "ok": c_int(0), "t": c_uint64(0)}
-        check(lib.rbc_batcher_validate(self._p, _ptr(r), _ptr(b) if len(b) else None, len(b),
-                                       _ptr(s) if len(s) else None, len(s), index, byref(h["ok"]), byref(h["t"])),
-              "rbc_batcher_validate")
+        h = {"kind": "validate", "r": r, "b": b, "s": s, "ok": c_int(0), "t": c_uint64(0),
+             "leaf": np.zeros(32, np.uint8) if leaf else None}
+        check(lib.rbc_batcher_validate_leaf(self._p, _ptr(r), _ptr(b) if len(b) else None, len(b),
+                                            _ptr(s) if len(s) else None, len(s), index, byref(h["ok"]),
+                                            _ptr(h["leaf"]) if leaf else None, byref(h["t"])),
+              "rbc_batcher_validate_leaf")
         return h
 
-    def submit_interpolate(self, root, shards) -> dict:
+    def submit_interpolate(self, root, shards, leaves=None) -> dict:
+        """interpolate through the coalescer; leaves (n x 32, the leaves of the
+        present shards from submit_validate(leaf=True)) selects
+        rbc_batcher_interpolate_verified: only regenerated rows are hashed."""
         n, k = self.ctx.n, self.ctx.k
         arrs = [_bytes_array(x).copy() for x in shards]
         S = max(len(a) for a in arrs)
@@ -723,14 +760,24 @@ class Batcher:
         h = {"kind": "interp", "arrs": arrs, "lens": lens, "ptrs": ptrs, "r": r,
              "value": np.zeros(max(k * S, 1), np.uint8), "vlen": c_size_t(0), "dig": np.zeros(32, np.uint8),
              "t": c_uint64(0)}
-        check(lib.rbc_batcher_interpolate(self._p, _ptr(r), ptrs, lens, _ptr(h["value"]), h["value"].nbytes,
-                                          byref(h["vlen"]), _ptr(h["dig"]), byref(h["t"])), "rbc_batcher_interpolate")
+        if leaves is None:
+            check(lib.rbc_batcher_interpolate(self._p, _ptr(r), ptrs, lens, _ptr(h["value"]), h["value"].nbytes,
+                                              byref(h["vlen"]), _ptr(h["dig"]), byref(h["t"])),
+                  "rbc_batcher_interpolate")
+        else:
+            lv = np.ascontiguousarray(leaves, dtype=np.uint8).reshape(n, 32).copy()
+            h["lv"] = lv
+            check(lib.rbc_batcher_interpolate_verified(self._p, _ptr(r), ptrs, lens, _ptr(lv), _ptr(h["value"]),
+                                                       h["value"].nbytes, byref(h["vlen"]), _ptr(h["dig"]),
+                                                       byref(h["t"])), "rbc_batcher_interpolate_verified")
         return h
 
     def wait(self, h: dict):
         st = lib.rbc_batcher_wait(self._p, h["t"].value)
         if h["kind"] == "validate":
             check(st, "validate")
+            if h["leaf"] is not None:
+                return bool(h["ok"].value), bytes(h["leaf"])
             return bool(h["ok"].value)
         check(st, h["kind"])
         if h["kind"] == "shard":

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define RBC_ABI_VERSION 5
+#define RBC_ABI_VERSION 6
 
 /* ---- status codes ------------------------------------------------------- */
 #define RBC_OK 0
@@ -235,6 +235,12 @@ typedef struct rbc_rx_batch {
     uint32_t value_pitch;
     uint8_t *digests;            /* [count][32] out (nullable) */
     int32_t *status;             /* [count] out */
+    /* ABI 6: != 0 when valid / leaves already hold rbc_dev_verify's output for
+     * this batch's received ECHOs (e.g. run on the proposer's stream right
+     * after the commit it depends on): the step then only decodes it as cur
+     * (no compaction, no row hashing or path walk for it) and rehashes,
+     * rechecks and digests it as prev as usual. */
+    int verified;
 } rbc_rx_batch;
 /* Timing marks (each nullable, rbc_event_create events) recorded on `stream`:
  * hashed after the hashing launch (and cur's shared-path walk), decode_begin
@@ -296,6 +302,17 @@ int rbc_validate_batch(rbc_ctx *ctx, int count, const uint8_t *const *shards, co
 int rbc_validate_packed(rbc_ctx *ctx, int count, const uint8_t *arena, size_t arena_bytes, const uint64_t *offs,
                         const uint32_t *lens, const uint8_t *idx, const uint8_t *branches, const uint8_t *roots,
                         uint8_t *ok_out, uint64_t *ticket);
+/* ABI 6: rbc_validate_packed that also returns each message's leaf,
+ * leaves_out[i] = SHA-256 of message i's shard bytes (32 B, nullable), so an
+ * interpolate of the same shards need not hash them again
+ * (rbc_interpolate_batch_verified).  Either form moves only the named bytes
+ * over PCIe when the arena is pinned and the messages cover less than 3/4 of
+ * it (a receiver's [count][n][pitch] ECHO buffer with offs at the received
+ * rows), else the whole arena in one DMA. */
+int rbc_validate_packed_leaves(rbc_ctx *ctx, int count, const uint8_t *arena, size_t arena_bytes,
+                               const uint64_t *offs, const uint32_t *lens, const uint8_t *idx,
+                               const uint8_t *branches, const uint8_t *roots, uint8_t *ok_out, uint8_t *leaves_out,
+                               uint64_t *ticket);
 /* interpolate() for `count` instances: shards [count][n][shard_pitch] with
  * present [count][n] (0 = missing, the Go `len == 0`), shard_lens [count],
  * roots [count][32] -> values_out [count][value_pitch] (k*S_i bytes),
@@ -304,6 +321,20 @@ int rbc_interpolate_batch(rbc_ctx *ctx, int count, const uint8_t *shards, size_t
                           const size_t *shard_lens, const uint8_t *present, const uint8_t *roots,
                           uint8_t *values_out, size_t value_pitch, uint8_t *digests_out, int32_t *status_out,
                           uint64_t *ticket);
+/* ABI 6: rbc_interpolate_batch over shards that were already validated:
+ * every present row (present[i][j] != 0) passed validateMessage and
+ * leaves [count][n][32] holds its SHA-256 (rbc_validate_packed_leaves /
+ * rbc_batcher_validate_leaf output; the slots of absent rows are ignored).
+ * The device hashes only the rows interpolate regenerates or finds changed
+ * (~2f of N instead of N), as rbc_dev_receive_step does; outputs and statuses
+ * equal rbc_interpolate_batch's on the same shards when the leaves are the
+ * present rows' true hashes (a wrong leaf is trusted: pass only leaves this
+ * library computed for exactly these bytes).  leaves == NULL is
+ * rbc_interpolate_batch. */
+int rbc_interpolate_batch_verified(rbc_ctx *ctx, int count, const uint8_t *shards, size_t shard_pitch,
+                                   const size_t *shard_lens, const uint8_t *present, const uint8_t *leaves,
+                                   const uint8_t *roots, uint8_t *values_out, size_t value_pitch,
+                                   uint8_t *digests_out, int32_t *status_out, uint64_t *ticket);
 int rbc_wait(rbc_ctx *ctx, uint64_t ticket);
 int rbc_poll(rbc_ctx *ctx, uint64_t ticket, int *done);
 
@@ -344,10 +375,24 @@ int rbc_batcher_validate(rbc_batcher *b, const uint8_t *root, const uint8_t *bra
  * shards, six arenas, four in flight); before the first validate only.
  * max_msgs < 2^20, 64 <= max_bytes <= 4 GiB - 64. */
 int rbc_batcher_set_validate(rbc_batcher *b, int max_msgs, size_t max_bytes);
+/* ABI 6: rbc_batcher_validate that also returns the shard's leaf
+ * (leaf_out, 32 B, written when *ok_out == 1) for a later
+ * rbc_batcher_interpolate_verified of the same shard.  rbc/rbc.go:88,93 are
+ * both package-internal, so a cgo shim can keep the leaves per RBC instance
+ * and the handlers stay unchanged. */
+int rbc_batcher_validate_leaf(rbc_batcher *b, const uint8_t *root, const uint8_t *branch, size_t branch_len,
+                              const uint8_t *shard, size_t shard_len, uint32_t index, int *ok_out, uint8_t *leaf_out,
+                              uint64_t *ticket);
 /* interpolate(): shards/lens are n entries (lens[j] == 0: missing) */
 int rbc_batcher_interpolate(rbc_batcher *b, const uint8_t *root, const uint8_t *const *shards, const size_t *lens,
                             uint8_t *value_out, size_t value_cap, size_t *value_len, uint8_t *digest_out,
                             uint64_t *ticket);
+/* ABI 6: interpolate() of shards that passed rbc_batcher_validate_leaf:
+ * leaves n*32 bytes, leaves[32j..] the leaf of shard j for every lens[j] != 0
+ * (rbc_interpolate_batch_verified semantics: only regenerated rows are hashed). */
+int rbc_batcher_interpolate_verified(rbc_batcher *b, const uint8_t *root, const uint8_t *const *shards,
+                                     const size_t *lens, const uint8_t *leaves, uint8_t *value_out, size_t value_cap,
+                                     size_t *value_len, uint8_t *digest_out, uint64_t *ticket);
 int rbc_batcher_wait(rbc_batcher *b, uint64_t ticket);
 int rbc_batcher_poll(rbc_batcher *b, uint64_t ticket, int *done);
 int rbc_batcher_stats(rbc_batcher *b, uint64_t *batches, uint64_t *requests);

@@ -43,8 +43,17 @@ int rbcref_interpolate(int n, int f, const uint8_t *shards, size_t pitch, size_t
                        const uint8_t *root, uint8_t *value_out, uint8_t *digest_out);
 int rbcref_merkle_verify(int n, const uint8_t *shard, size_t S, uint32_t index, const uint8_t *branch,
                          const uint8_t *root);
+int rbcref_interpolate_leaves(int n, int f, const uint8_t *shards, size_t pitch, size_t S, const uint8_t *valid,
+                              const uint8_t *leaves, const uint8_t *root, uint8_t *value_out, uint8_t *digest_out);
 int rbcref_tree_depth(int n);
+void rbcref_sha256(const uint8_t *p, size_t n, uint8_t out[32]);
 }
+
+// Failure injection of the validate lane's launches: when
+// g_fail_mod > 0, the packed launch number q (1-based, launch order) fails
+// at completion when q % g_fail_mod == 0 -- the arena of generation q, since
+// the lane launches one arena per generation in order.
+static std::atomic<int> g_fail_mod{0}, g_packed_calls{0};
 
 // ------------------------------------------------ stand-in context (oracle)
 struct rbc_ctx {
@@ -141,35 +150,50 @@ int rbc_validate_batch(rbc_ctx *c, int count, const uint8_t *const *shards, cons
     return RBC_OK;
 }
 
-int rbc_validate_packed(rbc_ctx *c, int count, const uint8_t *arena, size_t arena_bytes, const uint64_t *offs,
-                        const uint32_t *lens, const uint8_t *idx, const uint8_t *branches, const uint8_t *roots,
-                        uint8_t *ok_out, uint64_t *ticket) {
+int rbc_validate_packed_leaves(rbc_ctx *c, int count, const uint8_t *arena, size_t arena_bytes, const uint64_t *offs,
+                               const uint32_t *lens, const uint8_t *idx, const uint8_t *branches, const uint8_t *roots,
+                               uint8_t *ok_out, uint8_t *leaves_out, uint64_t *ticket) {
     // the real API's argument checks, then the arena read at some point before completion
     for (int i = 0; i < count; ++i)
         if (offs[i] % 64 || !lens[i] || offs[i] + (lens[i] + 63) / 64 * 64 > arena_bytes || idx[i] >= c->n)
             return RBC_ERR_INVALID_ARG;
     const size_t bslot = (size_t)std::max(c->d, 1) * 32;
-    *ticket = launch(c, [=] {
-        for (int i = 0; i < count; ++i)
+    const int q = ticket ? ++g_packed_calls : 0, mod = g_fail_mod.load();  // (a synchronous call is no lane launch)
+    const bool fail = mod > 0 && q > 0 && q % mod == 0;
+    auto work = [=] {
+        if (fail) {  // a failed launch writes nothing (a device error before the D2H)
+            return RBC_ERR_DEVICE;
+        }
+        for (int i = 0; i < count; ++i) {
             ok_out[i] = rbcref_merkle_verify(c->n, arena + offs[i], lens[i], idx[i], branches + i * bslot,
                                              roots + 32 * i);
+            if (leaves_out) rbcref_sha256(arena + offs[i], lens[i], leaves_out + 32 * (size_t)i);
+        }
         return RBC_OK;
-    });
+    };
+    if (!ticket) return work();  // a NULL ticket: synchronous, as the real API
+    *ticket = launch(c, work);
     return RBC_OK;
 }
 
-int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t pitch, const size_t *shard_lens,
-                          const uint8_t *present, const uint8_t *roots, uint8_t *values_out, size_t value_pitch,
-                          uint8_t *digests_out, int32_t *status_out, uint64_t *ticket) {
+int rbc_interpolate_batch_verified(rbc_ctx *c, int count, const uint8_t *shards, size_t pitch,
+                                   const size_t *shard_lens, const uint8_t *present, const uint8_t *leaves,
+                                   const uint8_t *roots, uint8_t *values_out, size_t value_pitch,
+                                   uint8_t *digests_out, int32_t *status_out, uint64_t *ticket) {
     for (int i = 0; i < count; ++i)
         if (shard_lens[i] > pitch || (size_t)c->k * shard_lens[i] > value_pitch) return RBC_ERR_INVALID_ARG;
     std::vector<size_t> sl(shard_lens, shard_lens + count);
     *ticket = launch(c, [=] {
         for (int i = 0; i < count; ++i)
-            status_out[i] = rbcref_interpolate(c->n, c->f, shards + (size_t)i * c->n * pitch, pitch, sl[i],
-                                               present + (size_t)i * c->n, roots + 32 * i,
-                                               values_out + (size_t)i * value_pitch,
-                                               digests_out ? digests_out + 32 * i : nullptr);
+            status_out[i] =
+                leaves ? rbcref_interpolate_leaves(c->n, c->f, shards + (size_t)i * c->n * pitch, pitch, sl[i],
+                                                   present + (size_t)i * c->n, leaves + (size_t)i * c->n * 32,
+                                                   roots + 32 * i, values_out + (size_t)i * value_pitch,
+                                                   digests_out ? digests_out + 32 * i : nullptr)
+                       : rbcref_interpolate(c->n, c->f, shards + (size_t)i * c->n * pitch, pitch, sl[i],
+                                            present + (size_t)i * c->n, roots + 32 * i,
+                                            values_out + (size_t)i * value_pitch,
+                                            digests_out ? digests_out + 32 * i : nullptr);
         return RBC_OK;
     });
     return RBC_OK;
@@ -300,9 +324,22 @@ void client(rbc_batcher *bt, int n, int f, int id, int reqs, const std::vector<C
             if (tamper == 2) O.root[rnd(0, 31)] ^= 0x01;
             const bool expect = tamper >= 3 || (tamper == 1 && O.brflat.empty());
             O.want_status = RBC_OK;
-            EXPECT(rbc_batcher_validate(bt, O.root.data(), O.brflat.data(), O.brflat.size(), O.shard.data(),
-                                        O.shard.size(), j, &O.ok, &t) == RBC_OK, "validate submit");
-            O.check = [&O, expect] { EXPECT(O.ok == (int)expect, "validate ok=%d want %d", O.ok, (int)expect); };
+            if (rnd(0, 1)) {  // with the leaf (ABI 6)
+                O.digest.assign(32, 0);
+                EXPECT(rbc_batcher_validate_leaf(bt, O.root.data(), O.brflat.data(), O.brflat.size(), O.shard.data(),
+                                                 O.shard.size(), j, &O.ok, O.digest.data(), &t) == RBC_OK,
+                       "validate_leaf submit");
+                O.check = [&O, expect] {
+                    EXPECT(O.ok == (int)expect, "validate ok=%d want %d", O.ok, (int)expect);
+                    uint8_t want[32];
+                    rbcref_sha256(O.shard.data(), O.shard.size(), want);
+                    if (O.ok == 1) EXPECT(!memcmp(want, O.digest.data(), 32), "validate leaf differs");
+                };
+            } else {
+                EXPECT(rbc_batcher_validate(bt, O.root.data(), O.brflat.data(), O.brflat.size(), O.shard.data(),
+                                            O.shard.size(), j, &O.ok, &t) == RBC_OK, "validate submit");
+                O.check = [&O, expect] { EXPECT(O.ok == (int)expect, "validate ok=%d want %d", O.ok, (int)expect); };
+            }
         } else {  // interpolate from a random present subset, maybe one shard corrupted
             O.rows.resize(n);
             O.ptrs.assign(n, nullptr);
@@ -330,15 +367,26 @@ void client(rbc_batcher *bt, int n, int f, int id, int reqs, const std::vector<C
             O.value.resize((size_t)k * cm.S - (small ? 1 : 0));
             O.digest.resize(32);
             std::vector<uint8_t> want_value((size_t)k * cm.S), want_digest(32);
+            const bool verified = rnd(0, 1) != 0;  // the present rows' leaves handed in (ABI 6)
+            O.in.assign((size_t)n * 32, 0);
+            for (int j = 0; j < n; ++j)
+                if (valid[j]) rbcref_sha256(flat.data() + (size_t)j * cm.S, cm.S, O.in.data() + (size_t)j * 32);
             int want = have < k ? RBC_ERR_TOO_FEW_SHARDS
-                                : rbcref_interpolate(n, f, flat.data(), cm.S, cm.S, valid.data(), cm.root,
-                                                     want_value.data(), want_digest.data());
+                       : verified ? rbcref_interpolate_leaves(n, f, flat.data(), cm.S, cm.S, valid.data(), O.in.data(),
+                                                              cm.root, want_value.data(), want_digest.data())
+                                  : rbcref_interpolate(n, f, flat.data(), cm.S, cm.S, valid.data(), cm.root,
+                                                       want_value.data(), want_digest.data());
             if (ragged) want = RBC_ERR_SHARD_SIZE;
             else if (small && have >= k) want = RBC_ERR_INVALID_ARG;
             O.want_status = want;
-            EXPECT(rbc_batcher_interpolate(bt, O.root.data(), O.ptrs.data(), O.lens.data(), O.value.data(),
-                                           O.value.size(), &O.out_len, O.digest.data(), &t) == RBC_OK,
-                   "interpolate submit");
+            if (verified)
+                EXPECT(rbc_batcher_interpolate_verified(bt, O.root.data(), O.ptrs.data(), O.lens.data(), O.in.data(),
+                                                        O.value.data(), O.value.size(), &O.out_len, O.digest.data(),
+                                                        &t) == RBC_OK, "interpolate_verified submit");
+            else
+                EXPECT(rbc_batcher_interpolate(bt, O.root.data(), O.ptrs.data(), O.lens.data(), O.value.data(),
+                                               O.value.size(), &O.out_len, O.digest.data(), &t) == RBC_OK,
+                       "interpolate submit");
             O.check = [&O, want_value, want_digest] {
                 EXPECT(O.out_len == want_value.size() && O.value == want_value && O.digest == want_digest,
                        "interpolate result differs from the oracle");
@@ -355,6 +403,147 @@ void client(rbc_batcher *bt, int n, int f, int id, int reqs, const std::vector<C
     }
     std::shuffle(live.begin(), live.end(), rng);
     for (auto &o : live) complete(*o);
+}
+
+// failed validate launches.  Every 3rd packed launch fails in the
+// stand-in: rbc_batcher_wait must return the error for exactly the tickets of
+// that launch's arena (generation g: ticket = 1 << 63 | g << 20 | slot),
+// ok_out must stay 0 for them, and rbc_batcher_poll must report them done.
+// Leaves are requested for every other message and must be the oracle's
+// SHA-256 of the shard wherever the verdict is 1.
+void failed_launches(int n, int f, const std::vector<Commit> &pool, int T, int R) {
+    const int d = rbcref_tree_depth(n);
+    rbc_ctx ctx;
+    ctx.n = n;
+    ctx.f = f;
+    ctx.k = n - 2 * f;
+    ctx.d = d;
+    g_fail_mod = 3;
+    g_packed_calls = 0;
+    rbc_batcher *bt = nullptr;
+    if (rbc_batcher_create(&ctx, 8, 200, &bt) != RBC_OK || rbc_batcher_set_validate(bt, 7, 1 << 16) != RBC_OK) abort();
+    std::atomic<int> failed_seen{0}, ok_seen{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            std::mt19937_64 rng(77 + t);
+            for (int r = 0; r < R; ++r) {
+                const Commit &cm = pool[rng() % pool.size()];
+                const uint32_t j = (uint32_t)(rng() % n);
+                std::vector<uint8_t> shard(cm.shards.begin() + (size_t)j * cm.S,
+                                           cm.shards.begin() + (size_t)(j + 1) * cm.S);
+                std::vector<uint8_t> br = flat_branch(n, d, cm, j), leaf(32, 0xEE);
+                int ok = -1;
+                uint64_t tk = 0;
+                const bool want_leaf = (r & 1) != 0;
+                EXPECT(rbc_batcher_validate_leaf(bt, cm.root, br.data(), br.size(), shard.data(), shard.size(), j, &ok,
+                                                 want_leaf ? leaf.data() : nullptr, &tk) == RBC_OK, "submit");
+                const uint64_t gen = (tk & ~(1ull << 63)) >> 20;
+                const int rc = rbc_batcher_wait(bt, tk);
+                int done = 0;
+                EXPECT(rbc_batcher_poll(bt, tk, &done) == RBC_OK && done == 1, "poll after wait");
+                const bool fails = gen > 0 && gen % 3 == 0;
+                EXPECT(rc == (fails ? RBC_ERR_DEVICE : RBC_OK), "gen %llu rc %d", (unsigned long long)gen, rc);
+                EXPECT(ok == (fails ? 0 : 1), "gen %llu ok %d", (unsigned long long)gen, ok);
+                if (want_leaf && ok == 1) {
+                    uint8_t want[32];
+                    rbcref_sha256(shard.data(), shard.size(), want);
+                    EXPECT(!memcmp(want, leaf.data(), 32), "leaf differs from the oracle's SHA-256");
+                }
+                (fails ? failed_seen : ok_seen)++;
+            }
+        });
+    for (auto &x : th) x.join();
+    rbc_batcher_destroy(bt);
+    g_fail_mod = 0;
+    EXPECT(failed_seen > 0 && ok_seen > 0, "failure injection: %d failed, %d ok", failed_seen.load(), ok_seen.load());
+    printf("n=%d f=%d failed launches: %d requests failed, %d ok\n", n, f, failed_seen.load(), ok_seen.load());
+}
+
+// rbc_batcher_destroy with requests still outstanding (open,
+// sealed and in-flight arenas; queued shard / interpolate requests) drains
+// them: after it returns every request's outputs are final.
+void destroy_outstanding(int n, int f, const std::vector<Commit> &pool, int T, int R) {
+    const int k = n - 2 * f, d = rbcref_tree_depth(n);
+    rbc_ctx ctx;
+    ctx.n = n;
+    ctx.f = f;
+    ctx.k = k;
+    ctx.d = d;
+    rbc_batcher *bt = nullptr;
+    if (rbc_batcher_create(&ctx, 16, 5000, &bt) != RBC_OK || rbc_batcher_set_validate(bt, 11, 1 << 16) != RBC_OK)
+        abort();
+    struct Item {
+        int kind;
+        const Commit *cm;
+        uint32_t j;
+        int ok = -1;
+        std::vector<uint8_t> shard, br, leaf, value, digest, out, root, brs;
+        std::vector<const uint8_t *> ptrs;
+        std::vector<size_t> lens;
+        size_t out_len = 0;
+    };
+    std::vector<std::vector<std::unique_ptr<Item>>> items(T);
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            std::mt19937_64 rng(991 + t);
+            for (int r = 0; r < R; ++r) {
+                auto it = std::make_unique<Item>();
+                Item &I = *it;
+                I.kind = (int)(rng() % 3);
+                I.cm = &pool[rng() % pool.size()];
+                uint64_t tk = 0;
+                if (I.kind == 0) {
+                    I.j = (uint32_t)(rng() % n);
+                    I.shard.assign(I.cm->shards.begin() + (size_t)I.j * I.cm->S,
+                                   I.cm->shards.begin() + (size_t)(I.j + 1) * I.cm->S);
+                    I.br = flat_branch(n, d, *I.cm, I.j);
+                    I.leaf.assign(32, 0);
+                    EXPECT(rbc_batcher_validate_leaf(bt, I.cm->root, I.br.data(), I.br.size(), I.shard.data(),
+                                                     I.shard.size(), I.j, &I.ok, I.leaf.data(), &tk) == RBC_OK, "v");
+                } else if (I.kind == 1) {
+                    I.out.resize((size_t)n * I.cm->S);
+                    I.root.resize(32);
+                    I.brs.resize((size_t)n * d * 32);
+                    EXPECT(rbc_batcher_shard(bt, I.cm->value.data(), I.cm->value.size(), I.out.data(), I.out.size(),
+                                             &I.out_len, I.root.data(), I.brs.data(), &tk) == RBC_OK, "s");
+                } else {
+                    I.ptrs.assign(n, nullptr);
+                    I.lens.assign(n, 0);
+                    for (int j = 0; j < n; ++j)
+                        if (j % 3 != 1 || j < k) {  // at least k present
+                            I.ptrs[j] = I.cm->shards.data() + (size_t)j * I.cm->S;
+                            I.lens[j] = I.cm->S;
+                        }
+                    I.value.resize((size_t)k * I.cm->S);
+                    I.digest.resize(32);
+                    EXPECT(rbc_batcher_interpolate(bt, I.cm->root, I.ptrs.data(), I.lens.data(), I.value.data(),
+                                                   I.value.size(), &I.out_len, I.digest.data(), &tk) == RBC_OK, "i");
+                }
+                items[t].push_back(std::move(it));  // never waited: destroy must drain it
+            }
+        });
+    for (auto &x : th) x.join();
+    rbc_batcher_destroy(bt);
+    int n_checked = 0;
+    for (auto &v : items)
+        for (auto &it : v) {
+            Item &I = *it;
+            if (I.kind == 0) {
+                uint8_t want[32];
+                rbcref_sha256(I.shard.data(), I.shard.size(), want);
+                EXPECT(I.ok == 1 && !memcmp(want, I.leaf.data(), 32), "validate not drained: ok=%d", I.ok);
+            } else if (I.kind == 1) {
+                EXPECT(I.out_len == I.cm->S && I.out == I.cm->shards && !memcmp(I.root.data(), I.cm->root, 32),
+                       "shard not drained");
+            } else {
+                EXPECT(I.out_len == (size_t)k * I.cm->S && !memcmp(I.value.data(), I.cm->value.data(),
+                                                                    I.cm->value.size()), "interpolate not drained");
+            }
+            ++n_checked;
+        }
+    printf("n=%d f=%d destroy with %d requests outstanding: all drained\n", n, f, n_checked);
 }
 
 }  // namespace
@@ -396,6 +585,8 @@ int main(int argc, char **argv) {
             fprintf(stderr, "FAIL: %zu launches never waited\n", ctx.inflight.size());
             ++failures;
         }
+        failed_launches(n, f, pool, std::min(T, 6), R);
+        destroy_outstanding(n, f, pool, std::min(T, 6), std::max(R / 2, 8));
     }
     if (failures) {
         printf("FAILED %d\n", failures.load());

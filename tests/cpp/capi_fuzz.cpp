@@ -126,9 +126,12 @@ static void fuzz_interpolate_batch(Geo &g) {
     std::vector<int32_t> status(count + 1);
     uint64_t t = 0;
     const bool async = coin(50);
-    const int rc = rbc_interpolate_batch(g.ctx, count, shards.data(), pitch, sl.data(), present.data(), roots.data(),
-                                         values.data(), vpitch, coin(30) ? nullptr : digests.data(), status.data(),
-                                         async ? &t : nullptr);
+    // ABI 6: half the calls hand in the present rows' leaves [count][n][32]
+    std::vector<uint8_t> leaves = bytes((size_t)count * g.n * 32 + 1);
+    const int rc = rbc_interpolate_batch_verified(g.ctx, count, shards.data(), pitch, sl.data(), present.data(),
+                                                  coin(50) ? leaves.data() : nullptr, roots.data(), values.data(),
+                                                  vpitch, coin(30) ? nullptr : digests.data(), status.data(),
+                                                  async ? &t : nullptr);
     bool bad = vpitch < (size_t)g.k * Smax;
     for (int i = 0; i < count; ++i) bad |= sl[i] > pitch;
     if (count > 0 && bad) EXPECT(rc == RBC_ERR_INVALID_ARG);
@@ -137,6 +140,49 @@ static void fuzz_interpolate_batch(Geo &g) {
         EXPECT(rbc_poll(g.ctx, t, &done) == RBC_OK);
         EXPECT(rbc_wait(g.ctx, t) == RBC_OK);
     }
+}
+
+// rbc_validate_packed_leaves: offsets / lengths / indices in and out of
+// range, dense and sparse arenas, pageable and pinned (the sparse pinned
+// case takes the gather path); leaves_out sized for exactly `count` messages.
+static void fuzz_validate_packed(Geo &g) {
+    const int count = (int)rnd(6);
+    const size_t arena_bytes = 64 * (1 + rnd(64));
+    const bool pinned = coin(50);
+    uint8_t *arena = nullptr;
+    std::vector<uint8_t> pageable;
+    if (pinned) {
+        void *q = nullptr;
+        EXPECT(rbc_host_alloc(arena_bytes, &q) == RBC_OK);
+        arena = (uint8_t *)q;
+    } else {
+        pageable = bytes(arena_bytes);
+        arena = pageable.data();
+    }
+    std::vector<uint64_t> offs(count + 1);
+    std::vector<uint32_t> lens(count + 1);
+    std::vector<uint8_t> idx(count + 1);
+    bool bad = false;
+    for (int i = 0; i < count; ++i) {
+        offs[i] = coin(90) ? 64 * rnd(arena_bytes / 64) : rnd(arena_bytes + 128);
+        lens[i] = coin(90) ? (uint32_t)(1 + rnd(std::min<size_t>(arena_bytes - std::min<size_t>(offs[i], arena_bytes), 200) + 1))
+                           : (uint32_t)rnd(2);
+        idx[i] = coin(95) ? (uint8_t)rnd(g.n) : (uint8_t)rng();
+        bad |= offs[i] % 64 || lens[i] == 0 || offs[i] > arena_bytes ||
+               (lens[i] + 63) / 64 * 64 > arena_bytes - offs[i] || idx[i] >= g.n;
+    }
+    const size_t bslot = (size_t)std::max(g.d, 1) * 32;
+    std::vector<uint8_t> br = bytes((size_t)count * bslot + 1), roots = bytes((size_t)count * 32 + 1);
+    std::vector<uint8_t> ok(count + 1), leaves((size_t)count * 32 + 1);
+    uint64_t t = 0;
+    const bool async = coin(50);
+    const int rc = rbc_validate_packed_leaves(g.ctx, count, arena, arena_bytes, offs.data(), lens.data(), idx.data(),
+                                              br.data(), roots.data(), ok.data(), coin(50) ? leaves.data() : nullptr,
+                                              async ? &t : nullptr);
+    if (count > 0 && bad) EXPECT(rc == RBC_ERR_INVALID_ARG);
+    else EXPECT(rc == RBC_OK);
+    if (rc == RBC_OK && async && t) EXPECT(rbc_wait(g.ctx, t) == RBC_OK);
+    if (pinned) rbc_host_free(arena);
 }
 
 static void fuzz_single_calls(Geo &g) {
@@ -344,7 +390,7 @@ int main(int argc, char **argv) {
                 fuzz_rs(encs[e], kp[e].first, kp[e].second);
                 break;
             }
-            case 5: fuzz_acs(); break;
+            case 5: coin(50) ? fuzz_acs() : fuzz_validate_packed(g); break;
             default: fuzz_receive_step(g); break;
         }
         EXPECT(rbc_strerror((int)rnd(40) - 30) != nullptr);

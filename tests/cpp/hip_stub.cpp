@@ -312,6 +312,14 @@ hipError_t rbc_launch_gather_present(const uint8_t *host, uint64_t hpitch, uint3
     }
     return hipSuccess;
 }
+hipError_t rbc_launch_gather_msgs(const uint8_t *host, const uint64_t *offs, const uint32_t *lens, uint32_t count,
+                                  uint8_t *dev, hipStream_t) {
+    for (uint32_t m = 0; m < count; ++m) {  // the kernel stores whole 16-B chunks up to round_up(len, 16)
+        touch(dev + offs[m], (lens[m] + 15) / 16 * 16);
+        memcpy(dev + offs[m], host + offs[m], lens[m]);
+    }
+    return hipSuccess;
+}
 hipError_t rbc_launch_count_mismatch(const uint8_t *, uint64_t, const uint8_t *, uint64_t, uint64_t, uint64_t,
                                      uint32_t *counter, hipStream_t) {
     touch(counter, 4);

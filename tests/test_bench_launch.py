@@ -259,3 +259,30 @@ def test_report_prices_the_step_per_opcode_not_at_four_clocks():
     assert 0 < v["issue_priced_ms"] < v["chain_priced_ms"]
     assert not v["unpriced_kernels"], v["unpriced_kernels"]
     assert "priced" in out["roofline_verify"]["valu"] and "measured" not in out["roofline_verify"]["valu"]
+
+
+def test_host_fed_aggregate_over_ranks():
+    """the host-fed epoch runs on every rank at once; the
+    job figure is every rank's committed shard bytes over the slowest rank's
+    seconds, never a sum of per-rank rates, and one failing rank fails it."""
+    import bench
+    n, S = 128, 23832
+    per = [{"GBps": round(1024 * n * S / t / 1e9, 3), "seconds": t, "instances": 1024, "ok": True}
+           for t in (0.20, 0.25, 0.40, 0.22)]
+    agg = bench.host_fed_aggregate(per, n, S)
+    assert agg["ranks"] == 4 and agg["slowest_rank"] == 2
+    assert agg["aggregate_GBps"] == round(4 * 1024 * n * S / 0.40 / 1e9, 3)
+    assert agg["aggregate_GBps"] < sum(agg["per_rank_GBps"])
+    assert agg["min_over_max"] == round(min(agg["per_rank_GBps"]) / max(agg["per_rank_GBps"]), 4)
+    assert agg["ok"] and agg["rank0"] is per[0]
+    per[3]["ok"] = False
+    assert not bench.host_fed_aggregate(per, n, S)["ok"]
+
+
+def test_value_form_defaults_to_the_joined_value():
+    """`value` is timed on the joined form interpolate
+    returns (rbc/rbc.go:88); --row-view selects the row view."""
+    import bench
+    assert bench.parse_args([]).join is True
+    assert bench.parse_args(["--row-view"]).join is False
+    assert bench.parse_args(["--no-joined-leg"]).no_second_form is True

@@ -138,3 +138,42 @@ def test_validate_packed_matches_oracle_and_checks_its_layout(gpu, n, f):
         with pytest.raises(gpu.RBCError):
             ctx.validate_packed(small, [o], [ln], [ix], **one)
     assert ctx.validate_packed(small, [], [], [], br[:0], roots[:0]).size == 0
+
+
+def test_batcher_epoch_all_three_kinds_with_reused_leaves(tmp_path):
+    """one node's C2 epoch through the batcher as the Go
+    handlers drive it -- 1,024 shard, 88,064 validateMessage and 1,024
+    interpolate requests from 16 client threads at once, 10 % of the
+    instances with a corrupted ECHO.  tools/batcher_bench checks every
+    verdict, value, shard row and root itself, and that interpolate with the
+    validate lane's leaves (only regenerated rows hashed) equals the full
+    rehash bit for bit; the sampled digests and roots are checked here against
+    the C oracle."""
+    import json
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "tools", "batcher_bench")
+    assert os.path.exists(exe), "build() makes tools/batcher_bench"
+    dump = tmp_path / "epoch.bin"
+    r = subprocess.run([exe, "epoch", "1024", "16", "8", "200", str(dump)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    rows = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    ep = [x for x in rows if x["phase"] == "epoch"]
+    assert [x["interpolate"].split()[0] for x in ep] == ["verified", "full"]
+    for x in ep:
+        assert x["instances"] == 1024 and x["echo_messages"] == 1024 * 86 and x["requests"] == 1024 * 88
+        assert x["value_failures"] == 0 and x["shard_failures"] == 0 and x["client_failures"] == 0 and x["GBps"] > 0
+    chk = rows[-1]
+    assert chk["phase"] == "check" and chk["failures"] == 0 and chk["verified_equals_full"]
+    n, f, B = 128, 42, 1 << 20
+    k = n - 2 * f
+    raw = dump.read_bytes()
+    rec = 4 + B + 64
+    assert len(raw) == 8 * rec
+    for q in range(8):
+        o = q * rec
+        value = np.frombuffer(raw[o + 4:o + 4 + B], np.uint8)
+        _, root, _, leaves = rbc_ref.encode_commit(n, f, value)
+        assert raw[o + 4 + B:o + 4 + B + 32] == root
+        assert raw[o + 4 + B + 32:o + rec] == rbc_ref.sha256(np.ascontiguousarray(leaves[:k]).tobytes())

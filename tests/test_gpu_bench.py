@@ -31,7 +31,7 @@ def _run(args, timeout=300, env=None):
 @pytest.mark.parametrize("pipeline,join", [(0, False), (7, False), (7, True)])
 def test_bench_schedules_pass_their_guard(pipeline, join):
     d = _run(["--steps", "3", "--warmup", "3", "--instances", "96", "--pipeline", str(pipeline)]
-             + (["--join"] if join else []) + QUICK)
+             + ([] if join else ["--row-view"]) + QUICK)
     for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
                 "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "ranks"):
         assert key in d, key
@@ -140,6 +140,33 @@ def test_bench_falls_back_to_serial_when_the_shard_sets_do_not_fit():
     assert d["decoded_ok"] == 64 and d["values_ok"] and d["oracle_sample_ok"]
 
 
+def _host_fed_ok(h, n, S):
+    assert h["ok"] and h["checks"]["verdict_mismatches"] == 0 and h["checks"]["values_ok"] and h["checks"]["roots_ok"]
+    assert h["checks"]["decoded"] == h["instances"] and h["echo_messages"] == h["instances"] * (n - 42)
+    assert h["GBps"] > 0 and h["pcie_GBps"]["h2d"] > 0 and h["pcie_GBps"]["d2h"] > 0
+
+
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_bench_host_fed_leg_on_every_rank(gpus):
+    """the host-fed epoch (rbc_shard_commit ||
+    rbc_validate_packed_leaves of every received ECHO -> rbc_interpolate_batch_verified,
+    pinned host memory both ways) runs on EVERY rank at once -- here 1 rank and
+    2 ranks rehearsed on this GPU -- and every rank's verdicts (10 % of the
+    instances carry a corrupted ECHO), values and proposer roots are checked;
+    each rank's record carries its own rate and the line the job aggregate."""
+    extra = ["--gpus", "2", "--rehearse-on-one-gpu"] if gpus == 2 else []
+    d = _run(["--instances", "256", "--steps", "3", "--warmup", "3", "--no-isolated", "--no-cpu-baseline",
+              "--oracle-samples", "4", "--host-instances", "256"] + extra, timeout=600)
+    p = d["pcie_inclusive"]
+    n, S = 128, d["config"]["shard_bytes"]
+    assert p["ok"] and p["ranks"] == gpus and len(p["per_rank_GBps"]) == gpus
+    _host_fed_ok(p["rank0"], n, S)
+    assert p["rank0"]["alone_GBps"]["validate+interpolate"] > 0
+    for r in d["ranks"]:
+        assert r["host_fed"]["ok"] and r["host_fed"]["instances"] == 256 and r["host_fed"]["GBps"] > 0
+    assert p["aggregate_GBps"] <= sum(p["per_rank_GBps"]) * 1.001
+
+
 MUTANT = os.path.join(ROOT, "tests", "mutants", "librbc_gpu_skip_regen.so")
 
 
@@ -152,7 +179,7 @@ def test_bench_guard_fails_a_build_that_never_regenerates(config, join):
     3 with values_ok and decoded_ok false -- and names the mutant it mapped."""
     assert os.path.exists(MUTANT), "build() makes tests/mutants"
     args = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", config, "--instances", "64", "--steps", "3",
-            "--warmup", "3", "--no-isolated"] + QUICK + (["--join"] if join else [])
+            "--warmup", "3", "--no-isolated"] + QUICK + ([] if join else ["--row-view"])
     r = subprocess.run(args, capture_output=True, text=True, timeout=300, env=dict(os.environ, RBC_GPU_LIB=MUTANT))
     assert r.returncode == 3, (r.returncode, r.stderr[-3000:])
     err = [ln for ln in r.stderr.splitlines() if ln.startswith('{"error"')]

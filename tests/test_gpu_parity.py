@@ -1913,3 +1913,35 @@ def test_verify_form_matches_the_profiling_tools_rule(gpu):
         form = gpu.Context(n, f).verify_form(S)
         assert (form == "shared_path") == ts.shared_path(cfg), (cfg, form)
         assert form == ("shared_path" if cfg == "c4" else "walk")
+
+
+@pytest.mark.parametrize("B,tail", [(44 * 40 - 3, 48), (44 * 40 - 3, 176), (44 * 300, 240)])
+def test_fused_join_zeroes_the_whole_padded_value_tail(gpu, B, tail):
+    """the FFT re-encode's fused join zeroes a value's tail from
+    tile 0, whose lanes past the shard row pitch have already returned.  With
+    a short row (S = 40, pitch 64) and a value pitch padded past k*S by more
+    than the pitch, the tail beyond the pitch would stay unwritten; the fused
+    join is then not used and the separate join zero-fills it.  Every byte of
+    every value row (data, then zero tail) is checked, the buffer having been
+    filled with garbage first."""
+    n, f, I = 128, 42, 32
+    pl = Pipeline(gpu, n, f, B, I, seed=B + tail, corrupt_frac=0.2)
+    k, S = pl.k, pl.S
+    vp = rup(k * S, 16) + rup(tail, 16)
+    out = gpu.DeviceBuffer(I * vp)
+    out.upload(np.full(I * vp, 0xA5, np.uint8))
+    pl.commit()
+    pl.poison()
+    b, c = pl.b, pl.ctx
+    c.dev_inject_faults(None, I, b["shards"], pl.spitch, b["corrupt"])
+    c.dev_verify(None, I, b["shards"], pl.spitch, None, S, b["branches"], b["roots"], b["present"], b["valid"],
+                 b["leaves_r"])
+    c.dev_interpolate(None, I, b["shards"], pl.spitch, None, S, b["valid"], b["leaves_r"], 1, b["roots"], out, vp,
+                      b["digests"], b["status"])
+    gpu.rbc.lib.rbc_device_sync(0)
+    assert (pl.arr("status", np.int32) == 0).all()
+    got = out.download(I * vp).reshape(I, vp)
+    for i in range(I):
+        want = np.zeros(vp, np.uint8)
+        want[:B] = pl.values[i, :B]
+        assert np.array_equal(got[i], want), (i, np.flatnonzero(got[i] != want)[:8])

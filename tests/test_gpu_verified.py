@@ -1,0 +1,195 @@
+"""The host-fed receive path with the validate lane's leaves reused (ABI 6,
+VERDICT r05 item 2): validateMessage (rbc/rbc.go:92-95) establishes the
+SHA-256 leaf of every received ECHO, so interpolate (rbc/rbc.go:86-90) needs
+to hash only the rows it regenerates -- as the device pipeline
+(rbc_dev_receive_step) already does.
+
+* rbc_validate_packed_leaves over a receiver's [count][N][pitch] pinned ECHO
+  buffer that names only the received rows (the sparse zero-copy gather) and
+  over the same messages in pageable memory (one DMA): verdicts equal the C
+  oracle's, leaves equal oracle SHA-256 of every message's bytes;
+* rbc_interpolate_batch_verified with those leaves: values, digests and
+  statuses bit-identical to rbc_interpolate_batch (full rehash) and to the
+  oracle, with tampered ECHOs dropped by validate, and a Byzantine
+  non-codeword proposer (every row valid under its root) rejected in both
+  forms;
+* the batcher: rbc_batcher_validate_leaf + rbc_batcher_interpolate_verified
+  from many threads, against the oracle."""
+import threading
+
+import numpy as np
+import pytest
+
+import rbc_oracle as orc
+import rbc_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _epoch(n, f, count, B, seed, tamper=0.1):
+    """count committed values (oracle), each instance's n-f received ECHO
+    rows and, for `tamper` of them, one received row with a flipped byte."""
+    rng = np.random.default_rng(seed)
+    k = n - 2 * f
+    S = (B + k - 1) // k
+    vals, shards, roots, brs = [], [], [], []
+    for i in range(count):
+        v = rng.integers(0, 256, B, dtype=np.uint8)
+        sh, root, br, _ = rbc_ref.encode_commit(n, f, v)
+        vals.append(v)
+        shards.append(sh)
+        roots.append(np.frombuffer(root, np.uint8))
+        brs.append(br)
+    present = np.zeros((count, n), np.uint8)
+    bad = np.full(count, -1)
+    for i in range(count):
+        rec = rng.permutation(n)[: n - f]
+        present[i, rec] = 1
+        if rng.random() < tamper:
+            bad[i] = int(rng.choice(rec))
+    return dict(vals=vals, shards=np.stack(shards), roots=np.stack(roots), br=np.stack(brs), present=present,
+                bad=bad, S=S, k=k)
+
+
+def _receive_buffer(gpu, e, n, pinned):
+    """The receiver's ECHO buffer [count][n][pitch]: received rows at their
+    leaf positions (the tampered one flipped), every other row garbage."""
+    count, S = e["shards"].shape[0], e["S"]
+    pitch = (S + 63) // 64 * 64
+    shape = (count, n, pitch)
+    buf = gpu.pinned_empty(shape) if pinned else np.empty(shape, np.uint8)
+    buf[:] = np.random.default_rng(5).integers(0, 256, shape, dtype=np.uint8)
+    buf[:, :, :S] = np.where(e["present"][:, :, None] == 1, e["shards"], buf[:, :, :S])
+    for i in np.flatnonzero(e["bad"] >= 0):
+        buf[i, e["bad"][i], S // 2] ^= 0x40
+    return buf, pitch
+
+
+def _messages(e, n, pitch):
+    inst, pos = np.nonzero(e["present"])
+    offs = ((inst * n + pos) * pitch).astype(np.uint64)
+    lens = np.full(len(inst), e["S"], np.uint32)
+    br = e["br"][inst, pos].reshape(len(inst), -1)
+    roots = e["roots"][inst]
+    return inst, pos, offs, lens, pos.astype(np.uint8), br, roots
+
+
+@pytest.mark.parametrize("n,f,B", [(128, 42, 44 * 600 + 7), (37, 12, 13 * 70)])
+def test_validate_packed_leaves_sparse_and_dense(gpu, n, f, B):
+    e = _epoch(n, f, 48, B, seed=n)
+    ctx = gpu.Context(n, f)
+    for pinned in (True, False):  # sparse zero-copy gather / whole-arena DMA
+        buf, pitch = _receive_buffer(gpu, e, n, pinned)
+        inst, pos, offs, lens, idx, br, roots = _messages(e, n, pitch)
+        ok, leaves = ctx.validate_packed(buf, offs, lens, idx, br, roots, leaves=True)
+        want = e["bad"][inst] != pos
+        assert np.array_equal(ok, want), np.flatnonzero(ok != want)[:8]
+        flat = buf.reshape(-1)
+        for m in range(0, len(inst), 7):  # every 7th message's leaf vs the oracle's SHA-256
+            o = int(offs[m])
+            assert bytes(leaves[m]) == rbc_ref.sha256(flat[o:o + e["S"]]), m
+        # the same verdicts without leaves (rbc_validate_packed)
+        assert np.array_equal(ctx.validate_packed(buf, offs, lens, idx, br, roots), want)
+    assert (e["bad"] >= 0).any()
+
+
+@pytest.mark.parametrize("n,f,B", [(128, 42, 44 * 600 + 7), (128, 42, 1 << 20), (37, 12, 13 * 70)])
+def test_interpolate_verified_equals_full_and_oracle(gpu, n, f, B):
+    count = 40 if B < (1 << 20) else 12
+    e = _epoch(n, f, count, B, seed=3 * n + B % 7)
+    ctx = gpu.Context(n, f)
+    k, S = e["k"], e["S"]
+    buf, pitch = _receive_buffer(gpu, e, n, pinned=True)
+    inst, pos, offs, lens, idx, br, roots = _messages(e, n, pitch)
+    ok, lv = ctx.validate_packed(buf, offs, lens, idx, br, roots, leaves=True)
+    # what a node passes to interpolate: the ECHOs that validated, with their leaves
+    valid = np.zeros((count, n), np.uint8)
+    valid[inst[ok], pos[ok]] = 1
+    leaves = gpu.pinned_empty((count, n, 32))
+    leaves[:] = 0
+    leaves[inst[ok], pos[ok]] = lv[ok]
+    shards_in = gpu.pinned_empty((count, n, pitch))
+    shards_in[:] = buf
+    v_out = gpu.pinned_empty((count, k * S))
+    got = ctx.interpolate_submit(shards_in, [S] * count, valid, e["roots"], values_out=v_out, leaves=leaves).wait()
+    full = ctx.interpolate_batch(np.array(buf), [S] * count, valid, e["roots"])
+    assert np.array_equal(got["status"], full["status"]) and (got["status"] == 0).all()
+    assert np.array_equal(got["values"], full["values"])
+    assert np.array_equal(got["digests"], full["digests"])
+    for i in range(count):
+        assert got["values"][i, :B].tobytes() == e["vals"][i].tobytes(), i
+    for i in range(0, count, 5):  # digests vs the C restatement (reusing its own verified leaves)
+        sh = np.where(valid[i][:, None] == 1, buf[i, :, :S], 0)
+        st, val, dig = rbc_ref.interpolate(n, f, sh, valid[i], e["roots"][i].tobytes())
+        assert st == 0 and dig == bytes(got["digests"][i]) and val.tobytes() == got["values"][i].tobytes()
+
+
+def test_interpolate_verified_rejects_noncodeword(gpu):
+    """A Byzantine proposer commits rows that are no codeword: every ECHO
+    validates under its root, and interpolate must still fail the root
+    recheck (valid-but-unused rows that disagree with the re-encoding are
+    rehashed) -- with reused leaves exactly as with the full rehash."""
+    n, f, S, count = 128, 42, 333, 16
+    rng = np.random.default_rng(9)
+    rows = rng.integers(0, 256, (count, n, S), dtype=np.uint8)
+    roots, leaves_all = [], []
+    for i in range(count):
+        com = orc.rbc_commit([rows[i, j].tobytes() for j in range(n)])
+        roots.append(np.frombuffer(com["root"], np.uint8))
+        leaves_all.append(np.stack([np.frombuffer(x, np.uint8) for x in com["leaves"]]))
+    roots, leaves_all = np.stack(roots), np.stack(leaves_all)
+    ctx = gpu.Context(n, f)
+    valid = np.zeros((count, n), np.uint8)
+    for i in range(count):
+        valid[i, rng.permutation(n)[: n - f]] = 1
+    lv = np.ascontiguousarray(leaves_all * valid[:, :, None])
+    got = ctx.interpolate_batch(rows, [S] * count, valid, roots, leaves=lv)
+    full = ctx.interpolate_batch(rows, [S] * count, valid, roots)
+    assert (got["status"] == -8).all() and (full["status"] == -8).all()
+
+
+def test_batcher_validate_leaf_then_interpolate_verified(gpu):
+    n, f, B, count = 128, 42, 44 * 900 + 3, 24
+    e = _epoch(n, f, count, B, seed=21)
+    k, S = e["k"], e["S"]
+    ctx = gpu.Context(n, f)
+    bt = gpu.Batcher(ctx, max_batch=8, max_wait_us=500)
+    results, errors = [None] * count, []
+
+    def node(i):  # one RBC instance's goroutine: validate every ECHO, then interpolate the valid ones
+        try:
+            hs = []
+            for j in np.flatnonzero(e["present"][i]):
+                sh = e["shards"][i, j].copy()
+                if e["bad"][i] == j:
+                    sh[S // 2] ^= 0x40
+                hs.append((j, sh, bt.submit_validate(e["roots"][i].tobytes(), e["br"][i, j].tobytes(), sh, int(j),
+                                                     leaf=True)))
+            shards, leaves = [b""] * n, np.zeros((n, 32), np.uint8)
+            for j, sh, h in hs:
+                ok, leaf = bt.wait(h)
+                assert ok == (e["bad"][i] != j)
+                if ok:
+                    assert leaf == rbc_ref.sha256(sh)
+                    shards[j], leaves[j] = sh.tobytes(), np.frombuffer(leaf, np.uint8)
+            r = bt.wait(bt.submit_interpolate(e["roots"][i].tobytes(), shards, leaves=leaves))
+            r0 = bt.wait(bt.submit_interpolate(e["roots"][i].tobytes(), shards))
+            results[i] = (r, r0, shards)
+        except Exception as x:  # noqa: BLE001
+            errors.append(repr(x))
+
+    th = [threading.Thread(target=node, args=(i,)) for i in range(count)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    bt.close()
+    assert not errors, errors[:3]
+    for i, (r, r0, shards) in enumerate(results):
+        assert r == r0
+        assert r["value"][:B] == e["vals"][i].tobytes()
+        if i % 6 == 0:  # vs the C restatement
+            valid = np.array([1 if s else 0 for s in shards], np.uint8)
+            rows = np.stack([np.frombuffer(s, np.uint8) if s else np.zeros(S, np.uint8) for s in shards])
+            st, val, dig = rbc_ref.interpolate(n, f, rows, valid, e["roots"][i].tobytes())
+            assert st == 0 and val.tobytes() == r["value"] and dig == r["digest"]

@@ -17,7 +17,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
+#include <deque>
 #include <chrono>
 #include <thread>
 #include <vector>
@@ -38,9 +40,11 @@ static double now() {
 }
 
 int validate_sweep(int argc, char **argv);
+int epoch(int argc, char **argv);
 
 int main(int argc, char **argv) {
     if (argc > 1 && !strcmp(argv[1], "validate-sweep")) return validate_sweep(argc - 1, argv + 1);
+    if (argc > 1 && !strcmp(argv[1], "epoch")) return epoch(argc - 1, argv + 1);
     const int n = 128, f = 42, k = n - 2 * f, d = 7;
     const size_t B = 1 << 20, S = (B + k - 1) / k;
     const int I = argc > 1 ? atoi(argv[1]) : 256;        // values
@@ -269,5 +273,190 @@ int validate_sweep(int argc, char **argv) {
     }
     rbc_ctx_destroy(ctx);
     printf("{\"phase\": \"check\", \"failures\": %d}\n", fails);
+    return fails ? 1 : 0;
+}
+
+// epoch: one node's whole C2 epoch through the batcher, the way the unchanged
+// Go handlers drive the drop-in (rbc/rbc.go:78, one goroutine per RBC
+// instance): per instance, shard() of the node's own proposal, validateMessage
+// of the N-f ECHOs it receives (10 % of the instances carry one corrupted
+// ECHO), then interpolate() of the ECHOs that validated.  T client threads,
+// each with W instances in flight, so thousands of requests of all three kinds
+// are outstanding together.  Passes: a warm-up, then the epoch timed with the
+// leaves reused (rbc_batcher_validate_leaf + rbc_batcher_interpolate_verified:
+// interpolate hashes only the regenerated rows), then timed again with the
+// plain calls (interpolate rehashes all N rows).  Every verdict, value, shard
+// row and root is checked; the two timed passes must agree bit for bit
+// (values, digests); `dump` receives sampled (value, root, digest) records for
+// the oracle check in tests/test_gpu_batcher.py.
+//   tools/batcher_bench epoch [instances] [threads] [window] [max_wait_us] [dump]
+int epoch(int argc, char **argv) {
+    const int n = 128, f = 42, k = n - 2 * f, d = 7, R = n - f;
+    const size_t B = 1 << 20, S = (B + k - 1) / k;
+    const int I = argc > 1 ? atoi(argv[1]) : 1024;
+    const int T = argc > 2 ? atoi(argv[2]) : 16;
+    const int W = argc > 3 ? atoi(argv[3]) : 8;
+    const int WAIT = argc > 4 ? atoi(argv[4]) : 200;
+    const char *dump = argc > 5 ? argv[5] : nullptr;
+    rbc_ctx *ctx;
+    CK(rbc_ctx_create(n, f, 0, &ctx));
+    std::vector<uint8_t> values((size_t)I * B);
+    uint64_t x = 0x2545F4914F6CDD1Dull;
+    for (size_t w = 0; w < values.size() / 8; ++w) {
+        x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+        memcpy(values.data() + 8 * w, &x, 8);
+    }
+    // the ECHOs this node receives: every instance's committed rows (committed here, before timing)
+    std::vector<uint8_t> shards_c((size_t)I * n * S), roots_c((size_t)I * 32), br_c((size_t)I * n * d * 32);
+    {
+        std::vector<uint32_t> sl(I);
+        std::vector<const uint8_t *> vp(I);
+        std::vector<size_t> vl(I, B);
+        for (int i = 0; i < I; ++i) vp[i] = values.data() + (size_t)i * B;
+        for (int i0 = 0; i0 < I; i0 += 64) {
+            const int c = std::min(64, I - i0);
+            CK(rbc_shard_commit(ctx, c, vp.data() + i0, vl.data() + i0, shards_c.data() + (size_t)i0 * n * S, S,
+                                sl.data() + i0, roots_c.data() + (size_t)i0 * 32, br_c.data() + (size_t)i0 * n * d * 32,
+                                nullptr));
+        }
+    }
+    // received positions (N-f of N) and the corrupted ECHO of 10 % of the instances
+    std::vector<int> recv((size_t)I * R), bad(I, -1);
+    std::vector<std::vector<uint8_t>> badrow(I);
+    uint64_t y = 0x9E3779B97F4A7C15ull;
+    auto rnd = [&](uint64_t m) { y ^= y << 13; y ^= y >> 7; y ^= y << 17; return y % m; };
+    for (int i = 0; i < I; ++i) {
+        std::vector<int> perm(n);
+        for (int j = 0; j < n; ++j) perm[j] = j;
+        for (int j = n - 1; j > 0; --j) std::swap(perm[j], perm[rnd(j + 1)]);
+        std::copy(perm.begin(), perm.begin() + R, recv.begin() + (size_t)i * R);
+        if (rnd(10) == 0) {
+            bad[i] = perm[rnd(R)];
+            badrow[i].assign(shards_c.begin() + ((size_t)i * n + bad[i]) * S,
+                             shards_c.begin() + ((size_t)i * n + bad[i] + 1) * S);
+            badrow[i][S / 2] ^= 0x5A;
+        }
+    }
+    auto echo = [&](int i, int j) -> const uint8_t * {
+        return j == bad[i] ? badrow[i].data() : shards_c.data() + ((size_t)i * n + j) * S;
+    };
+    std::vector<uint8_t> sh_out((size_t)I * n * S), root_out((size_t)I * 32), br_out((size_t)I * n * d * 32);
+    std::vector<size_t> slen(I);
+    std::vector<int> ok((size_t)I * R);
+    std::vector<uint8_t> leaf((size_t)I * n * 32);
+    std::vector<uint8_t> vout[2] = {std::vector<uint8_t>((size_t)I * k * S), std::vector<uint8_t>((size_t)I * k * S)};
+    std::vector<uint8_t> dig[2] = {std::vector<uint8_t>((size_t)I * 32), std::vector<uint8_t>((size_t)I * 32)};
+    std::vector<size_t> vlen(I);
+    int fails = 0;
+    double secs[2] = {0, 0};
+    uint64_t launches[2] = {0, 0}, reqs[2] = {0, 0};
+    // pass 0: warm-up (verified); pass 1: timed, leaves reused; pass 2: timed, full rehash
+    for (int pass = 0; pass < 3; ++pass) {
+        const bool verified = pass < 2;
+        const int o = pass == 2 ? 1 : 0;
+        rbc_batcher *b;
+        CK(rbc_batcher_create(ctx, 64, WAIT, &b));
+        std::atomic<int> next{0}, bad_count{0};
+        std::fill(ok.begin(), ok.end(), -1);
+        const double t0 = now();
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t)
+            th.emplace_back([&] {
+                struct Inst { int i; uint64_t ts, ti; std::vector<uint64_t> tv; };
+                std::deque<Inst> va, ip;  // validates pending / interpolate pending
+                auto finish_validate = [&](Inst &s) {
+                    std::vector<const uint8_t *> ptr(n, nullptr);
+                    std::vector<size_t> len(n, 0);
+                    for (int m = 0; m < R; ++m) {
+                        if (rbc_batcher_wait(b, s.tv[m]) != RBC_OK) ++bad_count;
+                        const int j = recv[(size_t)s.i * R + m];
+                        const int v = ok[(size_t)s.i * R + m];
+                        if (v != (j != bad[s.i])) ++bad_count;
+                        if (v == 1) { ptr[j] = echo(s.i, j); len[j] = S; }
+                    }
+                    const size_t i = s.i;
+                    if (verified)
+                        CK(rbc_batcher_interpolate_verified(b, roots_c.data() + i * 32, ptr.data(), len.data(),
+                                                            leaf.data() + i * n * 32, vout[o].data() + i * k * S,
+                                                            k * S, &vlen[i], dig[o].data() + i * 32, &s.ti));
+                    else
+                        CK(rbc_batcher_interpolate(b, roots_c.data() + i * 32, ptr.data(), len.data(),
+                                                   vout[o].data() + i * k * S, k * S, &vlen[i], dig[o].data() + i * 32,
+                                                   &s.ti));
+                };
+                auto finish_interp = [&](Inst &s) {
+                    if (rbc_batcher_wait(b, s.ti) != RBC_OK) ++bad_count;
+                    if (rbc_batcher_wait(b, s.ts) != RBC_OK) ++bad_count;
+                };
+                for (;;) {
+                    int i = -1;
+                    if ((int)va.size() < W && (i = next.fetch_add(1)) < I) {
+                        Inst s{i, 0, 0, std::vector<uint64_t>(R)};
+                        CK(rbc_batcher_shard(b, values.data() + (size_t)i * B, B, sh_out.data() + (size_t)i * n * S,
+                                             n * S, &slen[i], root_out.data() + (size_t)i * 32,
+                                             br_out.data() + (size_t)i * n * d * 32, &s.ts));
+                        for (int m = 0; m < R; ++m) {
+                            const int j = recv[(size_t)i * R + m];
+                            CK(rbc_batcher_validate_leaf(b, roots_c.data() + (size_t)i * 32,
+                                                         br_c.data() + ((size_t)i * n + j) * d * 32, d * 32, echo(i, j),
+                                                         S, (uint32_t)j, &ok[(size_t)i * R + m],
+                                                         verified ? leaf.data() + ((size_t)i * n + j) * 32 : nullptr,
+                                                         &s.tv[m]));
+                        }
+                        va.push_back(std::move(s));
+                        continue;
+                    }
+                    if (!va.empty()) {  // the oldest instance's ECHOs are all validated: interpolate it
+                        finish_validate(va.front());
+                        ip.push_back(std::move(va.front()));
+                        va.pop_front();
+                        if ((int)ip.size() >= W) { finish_interp(ip.front()); ip.pop_front(); }
+                        continue;
+                    }
+                    while (!ip.empty()) { finish_interp(ip.front()); ip.pop_front(); }
+                    break;
+                }
+            });
+        for (auto &t : th) t.join();
+        const double dt = now() - t0;
+        rbc_batcher_stats(b, &launches[o], &reqs[o]);
+        rbc_batcher_destroy(b);
+        fails += bad_count.load();
+        if (pass == 0) continue;
+        secs[o] = dt;
+        // checks: every value, every proposer shard row / root (the verdicts were checked by the clients)
+        int vbad = 0, sbad = 0;
+        for (int i = 0; i < I; ++i) {
+            vbad += vlen[i] != k * S || memcmp(vout[o].data() + (size_t)i * k * S, values.data() + (size_t)i * B, B) != 0;
+            sbad += slen[i] != S || memcmp(root_out.data() + (size_t)i * 32, roots_c.data() + (size_t)i * 32, 32) != 0 ||
+                    memcmp(sh_out.data() + (size_t)i * n * S, shards_c.data() + (size_t)i * n * S, n * S) != 0;
+        }
+        fails += vbad + sbad;
+        printf("{\"phase\": \"epoch\", \"interpolate\": \"%s\", \"instances\": %d, \"threads\": %d, \"window\": %d, "
+               "\"echo_messages\": %d, \"max_wait_us\": %d, \"seconds\": %.4f, \"GBps\": %.3f, \"requests\": %llu, "
+               "\"launches\": %llu, \"value_failures\": %d, \"shard_failures\": %d, \"client_failures\": %d}\n",
+               verified ? "verified (leaves reused)" : "full rehash", I, T, W, I * R, WAIT, dt,
+               (double)I * n * S / dt / 1e9, (unsigned long long)reqs[o], (unsigned long long)launches[o], vbad, sbad,
+               bad_count.load());
+        fflush(stdout);
+    }
+    // the leaf-reusing and the full-rehash interpolate agree bit for bit
+    const int same = vout[0] == vout[1] && dig[0] == dig[1];
+    fails += !same;
+    if (dump) {  // sampled records for the oracle (tests only read this)
+        FILE *fp = fopen(dump, "wb");
+        if (!fp) { fprintf(stderr, "cannot write %s\n", dump); return 1; }
+        for (int i = 0; i < I; i += std::max(1, I / 8)) {
+            const uint32_t ii = (uint32_t)i;
+            fwrite(&ii, 4, 1, fp);
+            fwrite(values.data() + (size_t)i * B, 1, B, fp);
+            fwrite(roots_c.data() + (size_t)i * 32, 1, 32, fp);
+            fwrite(dig[0].data() + (size_t)i * 32, 1, 32, fp);
+        }
+        fclose(fp);
+    }
+    rbc_ctx_destroy(ctx);
+    printf("{\"phase\": \"check\", \"failures\": %d, \"verified_equals_full\": %s, \"speedup\": %.3f}\n", fails,
+           same ? "true" : "false", secs[0] > 0 ? secs[1] / secs[0] : 0.0);
     return fails ? 1 : 0;
 }

@@ -115,6 +115,168 @@ def measure(ca, n, f, B, batch=64, batches=8, inflight=2, pinned=True, device=0)
             "batch": batch, "batches": batches, "inflight": inflight, "pinned": pinned}
 
 
+def _rx_messages(present, n, pitch):
+    """The received ECHOs of a sub-batch as rbc_validate_packed_leaves names
+    them inside the receiver's [count][n][pitch] buffer."""
+    inst, pos = np.nonzero(present)
+    return inst, pos, ((inst * n + pos) * pitch).astype(np.uint64)
+
+
+def epoch(ca, n, f, B, instances=1024, sub=128, ring=3, inflight=2, device=0, seed=20261018, tamper=0.10,
+          phases=True, barrier=None):
+    """One node's whole RBC epoch through the C ABI from pinned host memory
+    (end-to-end with H2D / D2H).  Per
+    sub-batch of `sub` instances, concurrently (`inflight` of each kind in
+    flight through the context's host slots):
+      proposer  rbc_shard_commit: values in, shards + roots + branches out;
+      receiver  rbc_validate_packed_leaves of every received ECHO (N-f per
+                instance, `tamper` of the instances carry one corrupted ECHO)
+                straight out of the node's [sub][N][pitch] receive buffer
+                (only the received rows cross PCIe), then
+                rbc_interpolate_batch_verified of the ECHOs that validated,
+                reusing their leaves (only the ~2f regenerated rows are
+                hashed), values out.
+    The receive side's inputs are a ring of `ring` committed sub-batches
+    prepared before timing (the ECHOs other proposers would have sent).
+    Every verdict, every decoded value and every proposer root is checked
+    after timing.  `barrier` (callable) brackets the timed region when ranks
+    run the leg together.  GB/s = instances x N x S committed shard bytes
+    per second (the bench's unit); PCIe bytes are counted per direction."""
+    import time as _t
+    ctx = ca.Context(n, f, device=device)
+    k, d = ctx.k, ctx.depth
+    S = (B + k - 1) // k
+    pitch = (S + 63) // 64 * 64
+    rng = np.random.default_rng(seed)
+    nsub = (instances + sub - 1) // sub
+    counts = [min(sub, instances - b * sub) for b in range(nsub)]
+    # ---- inputs (untimed): `ring` distinct value sets, committed once for the receive side
+    vals = []
+    for r in range(ring):
+        v = ca.pinned_empty((sub, B))
+        v[:] = rng.integers(0, 256, (sub, B), dtype=np.uint8)
+        vals.append(v)
+    prop = [{"shards": ca.pinned_empty((sub, n, S)), "roots": ca.pinned_empty((sub, 32)),
+             "branches": ca.pinned_empty((sub, n, max(d, 1), 32))} for _ in range(inflight + 1)]
+    rx = []
+    for r in range(ring):
+        com = ctx.shard_commit_submit(list(vals[r]), out=prop[0]).wait()
+        present = np.zeros((sub, n), np.uint8)
+        bad = np.full(sub, -1)
+        for i in range(sub):
+            rec = rng.permutation(n)[: n - f]
+            present[i, rec] = 1
+            if rng.random() < tamper:
+                bad[i] = int(rng.choice(rec))
+        buf = ca.pinned_empty((sub, n, pitch))
+        buf[:, :, :S] = com["shards"]
+        buf[:, :, S:] = 0
+        for i in np.flatnonzero(bad >= 0):
+            buf[i, bad[i], S // 2] ^= 0x5A
+        inst, pos, offs = _rx_messages(present, n, pitch)
+        m = len(inst)
+        br = ca.pinned_empty((m, max(d, 1) * 32))
+        br[:] = com["branches"][inst, pos].reshape(m, -1)
+        mroots = ca.pinned_empty((m, 32))
+        mroots[:] = com["roots"][inst]
+        meta = {"lens": np.full(m, S, np.uint32), "idx": pos.astype(np.uint8), "offs": offs}
+        rx.append(dict(buf=buf, present=present, bad=bad, inst=inst, pos=pos, br=br, mroots=mroots,
+                       roots=com["roots"].copy(), want=bad[inst] != pos, **meta))
+    vout = ca.pinned_empty((instances, k * S))
+    digests = np.zeros((instances, 32), np.uint8)
+    status = np.full(instances, 99, np.int32)
+    mmax = sub * (n - f)
+    vres = [{"ok": ca.pinned_empty((mmax,)), "leaves": ca.pinned_empty((mmax, 32))} for _ in range(inflight + 1)]
+    lvs = [ca.pinned_empty((sub, n, 32)) for _ in range(inflight + 1)]
+    roots_out = np.zeros((instances, 32), np.uint8)
+    verdict_bad = [0]
+
+    def commit(b, slot):
+        c = counts[b]
+        o = {kk: v[:c] for kk, v in prop[slot].items()}
+        return ctx.shard_commit_submit(list(vals[b % ring][:c]), out=o)
+
+    def validate(b, slot):
+        R = rx[b % ring]
+        m = int(np.searchsorted(R["inst"], counts[b]))
+        return ctx.validate_packed_submit(R["buf"], R["offs"][:m], R["lens"][:m], R["idx"][:m], R["br"][:m],
+                                          R["mroots"][:m], leaves=True,
+                                          out={"ok": vres[slot]["ok"], "leaves": vres[slot]["leaves"]})
+
+    def interpolate(b, slot, ok, leaves):
+        R, c = rx[b % ring], counts[b]
+        m = len(ok)
+        if not np.array_equal(ok, R["want"][:m]):
+            verdict_bad[0] += int((ok != R["want"][:m]).sum())
+        valid = np.zeros((c, n), np.uint8)
+        iv, pv = R["inst"][:m][ok], R["pos"][:m][ok]
+        valid[iv, pv] = 1
+        lv = lvs[slot][:c]
+        lv[iv, pv] = leaves[ok]
+        lo = b * sub
+        return ctx.interpolate_submit(R["buf"][:c], [S] * c, valid, R["roots"][:c], values_out=vout[lo:lo + c],
+                                      leaves=lv, digests_out=digests[lo:lo + c], status_out=status[lo:lo + c])
+
+    def run(kinds):
+        """One epoch, the given sides concurrently; returns wall seconds."""
+        live = {"c": [], "v": [], "i": []}
+        t0 = _t.perf_counter()
+        for b in range(nsub + 1):
+            if b < nsub:
+                if "c" in kinds:
+                    live["c"].append((b, commit(b, b % (inflight + 1))))
+                if "v" in kinds:
+                    live["v"].append((b, validate(b, b % (inflight + 1))))
+            # the receive side: interpolate a sub-batch once its validate is back
+            while live["v"] and (len(live["v"]) > inflight - 1 or b == nsub):
+                bv, tv = live["v"].pop(0)
+                ok, leaves = tv.wait()
+                if "i" in kinds:
+                    live["i"].append((bv, interpolate(bv, bv % (inflight + 1), ok, leaves)))
+                if b < nsub:
+                    break
+            for kd in ("c", "i"):
+                while live[kd] and (len(live[kd]) >= inflight or b == nsub):
+                    bb, tt = live[kd].pop(0)
+                    res = tt.wait()
+                    if kd == "c":
+                        roots_out[bb * sub: bb * sub + counts[bb]] = res["roots"]
+        return _t.perf_counter() - t0
+
+    # warm every slot's buffers, then time the epoch with all three sides together
+    run("cvi")
+    status[:] = 99
+    vout[:] = 0
+    verdict_bad[0] = 0
+    if barrier:
+        barrier()
+    el = run("cvi")
+    if barrier:
+        barrier()
+    # ---- checks (untimed): verdicts, every value, statuses, proposer roots
+    vals_ok = all(np.array_equal(vout[b * sub: b * sub + counts[b], :B], vals[b % ring][:counts[b]])
+                  for b in range(nsub))
+    roots_ok = all(np.array_equal(roots_out[b * sub: b * sub + counts[b]], rx[b % ring]["roots"][:counts[b]])
+                   for b in range(nsub))
+    shard_bytes = instances * n * S
+    echo = sum(int((rx[b % ring]["inst"] < counts[b]).sum()) for b in range(nsub))
+    h2d = instances * B + 2 * echo * S  # values, ECHO rows for validate, the valid ECHO rows for interpolate
+    d2h = shard_bytes + instances * n * d * 32 + instances * k * S
+    out = {"GBps": round(shard_bytes / el / 1e9, 3), "seconds": round(el, 4), "instances": instances,
+           "sub_batch": sub, "inflight": inflight, "echo_messages": echo,
+           "pcie_GBps": {"h2d": round(h2d / el / 1e9, 2), "d2h": round(d2h / el / 1e9, 2)},
+           "checks": {"verdict_mismatches": verdict_bad[0], "values_ok": bool(vals_ok),
+                      "decoded": int((status == 0).sum()), "roots_ok": bool(roots_ok)},
+           "ok": bool(vals_ok and roots_ok and verdict_bad[0] == 0 and (status == 0).all())}
+    if phases:  # each side alone over the same epoch: which one binds
+        alone = {}
+        for name, kinds in (("shard_commit", "c"), ("validate", "v"), ("validate+interpolate", "vi")):
+            alone[name] = round(shard_bytes / run(kinds) / 1e9, 3)
+        out["alone_GBps"] = alone
+    ctx.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2", choices=sorted(CFG))
