@@ -62,6 +62,10 @@ CONFIGS = {
 # the GEMV at r balances the streams at N = 128 and starves C1's one-wave-per-SIMD leaf hashing
 # (tools/gpu_runs/gpu_r03t.sh)
 DECODE_PRIO = {"c1": "c,c", "c2": "r,c", "c3": "r,c", "c4": "r,c"}
+# Stream that verifies each batch's received ECHOs under the pipeline: the receiver's step (one SHA launch
+# with the previous batch's regen rows), or the proposer's stream right after the commit it depends on
+# (rbc_dev_verify, then the receive step takes the batch as verified) -- VERDICT r05 item 4's A/B at C4
+VERIFY_ON = {"c1": "receiver", "c2": "receiver", "c3": "receiver", "c4": "receiver"}
 METRIC = "RBC shard GB/s (RS encode+decode + Merkle verify) per GPU & node, N=128"
 SEED = 20261015
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
@@ -100,7 +104,10 @@ def parse_args(argv):
     ap.add_argument("--no-second-form", "--no-joined-leg", dest="no_second_form", action="store_true",
                     help="skip the secondary timed run in the other value form (key value_row_view / value_joined)")
     ap.add_argument("--faults-on", default="receiver", choices=("receiver", "proposer"),
-                    help="stream that injects the corrupted ECHO shards (synthetic input)")
+                    help="stream that injects the corrupted ECHO shards (synthetic input; the proposer's when "
+                         "it also verifies)")
+    ap.add_argument("--verify-on", default="", choices=("", "receiver", "proposer"),
+                    help="stream that verifies the received ECHOs under the pipeline (default per config, VERIFY_ON)")
     ap.add_argument("--wave-prio", default="",
                     help="commit,receive s_setprio levels (default 0,2 pipelined, 0,0 serial)")
     ap.add_argument("--decode-prio", default="",
@@ -143,13 +150,13 @@ def _levels_ok(text, names):
     return len(text.split(",")) == 2 and all(x in names + ("0", "1", "2", "3") for x in text.split(","))
 
 
-def hbm_plan(I, n, d, spitch, vpitch, opitch, join, world_gather, free, sharing, budget_arg):
+def hbm_plan(I, n, d, spitch, vpitch, opitch, join, world_gather, free, sharing, budget_arg, rx_sets=2):
     """Bytes per shard set / receiver set / the rest, and the schedule that fits."""
     set_b = I * (n * spitch + n * 32 + 32 + n * max(d, 1) * 32)
     rx_b = I * (n + n * 32 + 32 + 4 + (opitch if join else 0))
     other = I * (vpitch + n + 4 + 64) + world_gather + GiB  # + decode workspace, events, slack
     budget = budget_arg or (free / sharing) * 0.97
-    need = {"pipelined": 3 * set_b + 2 * rx_b + other, "serial": set_b + rx_b + other}
+    need = {"pipelined": 3 * set_b + rx_sets * rx_b + other, "serial": set_b + rx_b + other}
     return {"free_bytes": int(free), "ranks_sharing_device": sharing, "budget_bytes": int(budget),
             "need_bytes": {k: int(v) for k, v in need.items()}}, need
 
@@ -209,13 +216,17 @@ def run(args, world, rank, local_rank, wd, out):
     gather = (world > 1 or args.force_gather) and not args.rehearse_on_one_gpu
     slots = acs.max_share(total, world)
     free, _ = ca.rbc.mem_info(dev)
+    pverify = (args.verify_on or VERIFY_ON[args.config]) == "proposer"
     plan, need = hbm_plan(I, n, d, spitch, vpitch, opitch, args.join, world * slots * 64 if gather else 0, free,
-                          world if args.rehearse_on_one_gpu else 1, args.hbm_budget)
+                          world if args.rehearse_on_one_gpu else 1, args.hbm_budget, 3 if pverify else 2)
     pipe = args.pipeline == 7 and need["pipelined"] <= plan["budget_bytes"]
     if need["serial"] > plan["budget_bytes"]:
         raise SystemExit(f"bench: rank {rank} needs {need['serial'] / 1e9:.1f} GB for {I} instances, "
                          f"has {plan['budget_bytes'] / 1e9:.1f} GB: use more ranks or fewer instances")
     plan["schedule"] = "pipelined" if pipe else "serial"
+    pverify = pverify and pipe
+    if pverify:
+        args.faults_on = "proposer"  # the corrupted ECHOs must be in place before the proposer-side verify
     tx, rx = (int(x) for x in (args.wave_prio or ("0,2" if pipe else "0,0")).split(","))
     ctx.set_wave_priority(tx, rx)
     lv = {"c": tx, "r": rx}
@@ -242,7 +253,8 @@ def run(args, world, rank, local_rank, wd, out):
     sets = [dict(shards=mb(I * n * spitch), leaves=mb(I * n * 32), roots=mb(I * 32),
                  branches=mb(I * n * max(d, 1) * 32)) for _ in range(nsets)]
     rxb = [dict(valid=mb(I * n), leaves_r=mb(I * n * 32), digests=mb(I * 32), status=mb(I * 4),
-                out=mb(I * opitch) if args.join else None) for _ in range(2 if pipe else 1)]
+                out=mb(I * opitch) if args.join else None) for _ in range((3 if pverify else 2) if pipe else 1)]
+    nrx = len(rxb)
     d_present = mb(I * n)
     d_present.upload(present_h)
     d_corrupt = mb(I * 4)
@@ -261,7 +273,7 @@ def run(args, world, rank, local_rank, wd, out):
     me["rccl_nranks"] = rccl["nranks"] if rccl else None
 
     rstream = ca.Stream(dev) if pipe else stream
-    names = ("t0", "enc", "leaf", "tree", "pf", "r0", "rf", "hb", "rh", "hashed", "dbeg", "ddone", "rend", "gather")
+    names = ("t0", "enc", "leaf", "tree", "pf", "pv", "r0", "rf", "hb", "rh", "hashed", "dbeg", "ddone", "rend", "gather")
     ev_sets = [{nm: ca.Event() for nm in names} for _ in range(max(args.steps, 20))]  # >= the joined leg's steps
     form = {"join": args.join, "start": 0}  # value form of the receive steps; the first step of a run
     vpo = lambda rb: (rb["out"], opitch) if form["join"] else (None, 0)  # noqa: E731
@@ -313,18 +325,23 @@ def run(args, world, rank, local_rank, wd, out):
         if args.faults_on == "proposer":
             ctx.dev_inject_faults(P.ptr, I, sp["shards"], spitch, d_corrupt)
         rec(ev, "pf", P)
+        if pverify:  # batch t's ECHO verify right behind its commit, on P (rbc_rx_batch.verified)
+            rv = rxb[t % nrx]
+            ctx.dev_verify(P.ptr, I, sp["shards"], spitch, None, S, sp["branches"], sp["roots"], d_present,
+                           rv["valid"], rv["leaves_r"])
+            rec(ev, "pv", P)
         evP[t % nsets].record(P)
         if t == form["start"]:
             return
         x = t - 1
-        sr, rb = sets[x % nsets], rxb[x % 2]
+        sr, rb = sets[x % nsets], rxb[x % nrx]
         R.wait(evP[x % nsets])
         rec(ev, "r0", R)
         if args.faults_on == "receiver":
             ctx.dev_inject_faults(R.ptr, I, sr["shards"], spitch, d_corrupt)
         rec(ev, "rf", R)
         cur = ctx.rx_batch(I, sr["shards"], spitch, None, S, sr["branches"], sr["roots"], d_present, rb["valid"],
-                           rb["leaves_r"], *vpo(rb), rb["digests"], rb["status"])
+                           rb["leaves_r"], *vpo(rb), rb["digests"], rb["status"], verified=pverify)
         prev = pending.pop(x - 1, None)
         marks = {nm: ev[key] for nm, key in (("hashed", "hashed"), ("decode_begin", "dbeg"), ("decoded", "ddone"),
                                              ("hash_begin", "hb"), ("rows_hashed", "rh"))} if ev is not None else {}
@@ -334,7 +351,7 @@ def run(args, world, rank, local_rank, wd, out):
         pending[x] = cur
         rec(ev, "rend", R)
         if gather and prev is not None:
-            pb = rxb[(x - 1) % 2]
+            pb = rxb[(x - 1) % nrx]
             ctx.dev_allgather_records(R.ptr, I, slots, sets[(x - 1) % nsets]["roots"], pb["digests"], pb["status"],
                                       d_gather)
         rec(ev, "gather", R)
@@ -377,14 +394,14 @@ def run(args, world, rank, local_rank, wd, out):
     if pipe:  # complete the batch the last receive step decoded (outside the timed region)
         x_last, cur = pending.popitem()
         ctx.dev_receive_step(rstream.ptr, None, cur)
-        last, rb_last = sets[x_last % nsets], rxb[x_last % 2]
+        last, rb_last = sets[x_last % nsets], rxb[x_last % nrx]
         if gather:  # the guard checks this batch's gathered records
             ctx.dev_allgather_records(rstream.ptr, I, slots, last["roots"], rb_last["digests"], rb_last["status"],
                                       d_gather)
         rstream.sync()
     else:
         last, rb_last = sets[0], rxb[0]
-    stage_ms = spans(ev_sets[: args.steps], args.faults_on if pipe else None)
+    stage_ms = spans(ev_sets[: args.steps], args.faults_on if pipe else None, pverify)
     timed = check_batch(args, ca, dev, stream, I, n, k, B, S, spitch, vpitch, opitch, d_values, last, rb_last,
                         d_count)
 
@@ -445,8 +462,8 @@ def run(args, world, rank, local_rank, wd, out):
         ctx.dev_receive_step(rstream.ptr, None, cur_j)
         rstream.sync()
         res = check_batch(args, ca, dev, stream, I, n, k, B, S, spitch, vpitch, opitch, d_values, sets[x_j % nsets],
-                          rxb[x_j % 2], d_count, join=join2)
-        sm = spans(ev_sets[:steps_j], args.faults_on)
+                          rxb[x_j % nrx], d_count, join=join2)
+        sm = spans(ev_sets[:steps_j], args.faults_on, pverify)
         return {"value": round(total * n * S * steps_j / el / 1e9, 3), "unit": "GB/s", "steps": steps_j,
                 "ms_per_step": round(el * 1000.0 / steps_j, 4),
                 "decoded_ok": int((res["status"] == 0).sum()), "values_ok": res["mism"] == 0,
@@ -486,7 +503,13 @@ def run(args, world, rank, local_rank, wd, out):
         h = host_bench.epoch(ca, n, f, B, instances=hi, sub=sub, device=dev, seed=SEED + 7 + rank,
                              barrier=rdz.barrier)
         me["host_fed"] = {kk: h[kk] for kk in ("GBps", "seconds", "instances", "pcie_GBps", "ok")}
-        pcie = host_fed_aggregate(rdz.allgather(h), n, S)
+        me["host_fed"]["fused_GBps"] = h["fused"]["GBps"]
+        per = rdz.allgather(h)
+        pcie = host_fed_aggregate(per, n, S)
+        fused = host_fed_aggregate([dict(x["fused"], instances=x["instances"]) for x in per], n, S)
+        pcie["fused"] = {kk: fused[kk] for kk in ("aggregate_GBps", "per_rank_GBps", "slowest_rank", "min_over_max",
+                                                  "ok")}
+        pcie["fused"]["path"] = per[0]["fused"]["path"]
         pcie.update({
                 "unit": "GB/s of committed shard bytes (N*S per instance), host memory in and out",
                 "path": "one epoch per rank through the C ABI from pinned host memory, all ranks at once: "
@@ -518,7 +541,8 @@ def run(args, world, rank, local_rank, wd, out):
                    "wave_priority": {"commit": tx, "receive": rx, "decode_gemv": gv, "decode_reencode": rv},
                    "value_form": "joined (k*S contiguous bytes per instance, the []byte rbc/rbc.go:88 returns)"
                                  if args.join else "row view (the k data rows of the shard set, no join)",
-                   "faults_on": args.faults_on, "hbm_plan": plan,
+                   "faults_on": args.faults_on, "verify_on": "proposer" if pverify else "receiver",
+                   "hbm_plan": plan,
                    **({"rehearsal": "all ranks on device 0, no RCCL (not a multi-GPU measurement)"}
                       if args.rehearse_on_one_gpu else {}),
                    "pipeline": (f"commit(t) || receive step: verify(t-1) + rehash(t-2) in one SHA launch, "
@@ -532,6 +556,8 @@ def run(args, world, rank, local_rank, wd, out):
     ok = all(checks[c] for c in ("values_ok", "oracle_sample_ok", "gather_ok")) and checks["decoded_ok"] == total
     if pcie is not None:  # every rank's host-fed verdicts, values and roots
         ok = ok and pcie["ok"]
+    if batcher and "skipped" not in batcher:  # the drop-in path's own checks (verdicts, values, rows, roots)
+        ok = ok and batcher["failures"] == 0 and batcher["epoch"]["failures"] == 0 and batcher["rc"] == 0
     if second and "value" in second:  # the second leg's last batch passes the same value check
         ok = ok and second["values_ok"] and second["decoded_ok"] == I
     wd.leave()
@@ -562,6 +588,7 @@ def host_fed_aggregate(per, n, S):
 
 
 BATCHER_LEVELS = (1024, 8192, 32768, 88064)  # outstanding validates; 88,064 = one C2 epoch (1,024 x 86 ECHOs)
+EPOCH_WINDOW = 8  # instances each of the 16 client threads keeps in flight in the batcher's epoch
 
 
 def batcher_sweep(cpu):
@@ -585,6 +612,22 @@ def batcher_sweep(cpu):
                                             "msgs_per_launch", "failed")} for x in sweep],
            "failures": next((x["failures"] for x in rows if x.get("phase") == "check"), None), "rc": r.returncode,
            "tool": "tools/batcher_bench validate-sweep (C2: N=128, f=42, 1 MiB values, S=23,832; 16 client threads)"}
+    # the whole drop-in epoch: 1,024 shard + 88,064 validate + 1,024 interpolate
+    # requests from 16 client threads at once, timed with the validate lane's leaves reused by
+    # interpolate and again with the full rehash; the tool checks every verdict, value, row and root
+    r = subprocess.run([exe, "epoch", "1024", "16", str(EPOCH_WINDOW), "200"], capture_output=True, text=True,
+                       timeout=300)
+    rows = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    ep = {x["interpolate"].split()[0]: x for x in rows if x.get("phase") == "epoch"}
+    chk = next((x for x in rows if x.get("phase") == "check"), {})
+    out["epoch"] = {"unit": "GB/s of committed shard bytes (N*S per instance), host memory in and out",
+                    "GBps": ep.get("verified", {}).get("GBps"), "GBps_full_rehash": ep.get("full", {}).get("GBps"),
+                    "seconds": ep.get("verified", {}).get("seconds"), "requests": ep.get("verified", {}).get("requests"),
+                    "launches": ep.get("verified", {}).get("launches"), "window_per_thread": EPOCH_WINDOW,
+                    "failures": chk.get("failures"), "verified_equals_full": chk.get("verified_equals_full"),
+                    "rc": r.returncode,
+                    "tool": "tools/batcher_bench epoch (C2, 1,024 instances: shard + 86 validateMessage + interpolate "
+                            "each, 10% with one corrupted ECHO, 16 client threads)"}
     if cpu and cpu.get("validate"):
         out["host_sha_ni"] = cpu["validate"]
         best = max((x["GBps"] for x in sweep), default=0)
@@ -608,7 +651,7 @@ def rank_timing(rdz, me, elapsed, steps, stage_ms):
     return ranks, skew
 
 
-def spans(ev_sets, faults_on):
+def spans(ev_sets, faults_on, pverify=False):
     """Average event spans (ms) per stage over the given steps (faults_on None:
     the serial schedule); each span is taken on the stream its kernels run on
     (under the pipeline it also holds the other stream's concurrent work)."""
@@ -623,6 +666,9 @@ def spans(ev_sets, faults_on):
                      verify_rows=("hb", "rh"), verify_path=("rh", "hashed"),
                      check=("hashed", "dbeg"), decode=("dbeg", "ddone"), interp=("hashed", "rend"),
                      gather=("rend", "gather"))
+        if pverify:  # the verify runs on P after the commit; R's hashing launch is prev's regen rows alone
+            pairs.update(verify=("pf", "pv"), regen_rows=("hb", "rh"))
+            del pairs["verify_rows"], pairs["verify_path"]
     return {nm: sum(ev[a].elapsed_ms(ev[b]) for ev in ev_sets) / len(ev_sets) for nm, (a, b) in pairs.items()}
 
 
@@ -660,7 +706,14 @@ def report(args, ctx, I, n, k, d, S, present_h, corrupt_h, stage_ms, iso, elapse
     # instance's root and writes its valid byte; the shared-path verify reads the leaves and branches
     # of the received rows, the roots and present masks, and writes valid for every row
     path_bytes = R * (32 * d + 32) + I * (32 + 2 * n)
-    if pipe:  # the receive step's row-hashing launch: ECHO rows of t + the regenerated rows of t-1
+    if pipe and "regen_rows" in stage_ms:  # verify on the proposer's stream; R hashes the regen rows alone
+        if path:
+            kern["verify: sha_rows_kernel<leaves> + merkle_path_kernel<4>"] = ("verify", R * (S + 32) + path_bytes,
+                                                                              R * bps)
+        else:
+            kern["sha_rows_kernel<verify>"] = ("verify", R * (S + 32 * d + 32 + 1) + I * 32, R * (bps + 2 * d))
+        kern["sha_rx_kernel<regen>"] = ("regen_rows", regen * (S + 32), regen * bps)
+    elif pipe:  # the receive step's row-hashing launch: ECHO rows of t + the regenerated rows of t-1
         if path:
             kern["sha_rx_kernel<leaves+regen>"] = ("verify_rows", (R + regen) * (S + 32), (R + regen) * bps)
             kern["merkle_path_kernel<4>"] = ("verify_path", path_bytes, 0)
@@ -685,8 +738,11 @@ def report(args, ctx, I, n, k, d, S, present_h, corrupt_h, stage_ms, iso, elapse
         except (OSError, ValueError):
             continue
         if c.get("config") == args.config and c.get("instances", 1024) == I:
-            cands.append((c.get("value_form", "joined") != want_form, cand, c))
-    if cands:  # the newest file of the timed value form, else of the other form (same SHA / encode kernels)
+            # rank: the timed value form stated in the file, then the other form stated (the SHA and
+            # encode kernels are the same in both), then a file from before the form was recorded
+            form = c.get("value_form")
+            cands.append((0 if form == want_form else (1 if form else 2), cand, c))
+    if cands:  # newest first within a rank (the names sort by round)
         _, cand, pm = min(cands, key=lambda x: x[0])
         pmc_path = os.path.join("profiles", cand)
     # the loaded clock per kernel, each kernel alone (serial schedule; tools/clock_summary.py)

@@ -123,6 +123,8 @@ _SIGS = {
                                            c_void_p, c_void_p, c_void_p, c_void_p, POINTER(c_uint64)]),
     "rbc_interpolate_batch_verified": (c_int, [c_void_p, c_int, c_void_p, c_size_t, szp, c_void_p, c_void_p,
                                                c_void_p, c_void_p, c_size_t, c_void_p, i32p, POINTER(c_uint64)]),
+    "rbc_receive_batch": (c_int, [c_void_p, c_int, c_void_p, c_size_t, szp, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_void_p, c_size_t, c_void_p, i32p, POINTER(c_uint64)]),
     "rbc_batcher_validate_leaf": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_uint32,
                                           POINTER(c_int), c_void_p, POINTER(c_uint64)]),
     "rbc_batcher_interpolate_verified": (c_int, [c_void_p, c_void_p, c_void_p, szp, c_void_p, c_void_p, c_size_t,

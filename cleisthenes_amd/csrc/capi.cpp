@@ -130,7 +130,7 @@ struct Ws {
 // buffers at completion (rbc_wait / rbc_poll / slot reuse).
 struct Slot {
     DevBuf d_values, d_shards, d_leaves, d_roots, d_branches, d_valid, d_status, d_digests, d_lens, d_slens, d_idx,
-        d_offs;
+        d_offs, d_present;
     DevBuf h_in{nullptr, 0, true}, h_out{nullptr, 0, true};
     Ws ws;
     hipStream_t stream = nullptr;
@@ -152,7 +152,7 @@ struct Slot {
     int d2h_rc = 0;
     void release() {
         for (DevBuf *b : {&d_values, &d_shards, &d_leaves, &d_roots, &d_branches, &d_valid, &d_status, &d_digests,
-                          &d_lens, &d_slens, &d_idx, &d_offs, &h_in, &h_out})
+                          &d_lens, &d_slens, &d_idx, &d_offs, &d_present, &h_in, &h_out})
             b->release();
         ws.release();
         if (stream) (void)hipStreamDestroy(stream);
@@ -364,9 +364,11 @@ static bool shared_path_verify(const rbc_ctx *c, const uint32_t *shard_lens, uin
     return (shard_lens || 16u * (uint32_t)c->depth >= blocks_per_row) && c->depth >= 1 && c->width <= 256;
 }
 
+// wsp: a host-API slot's own workspace (its submission already holds c->mu);
+// NULL: the context's, guarded by c->mu here (device API)
 int stage_verify(rbc_ctx *c, hipStream_t st, int count, const uint8_t *shards, uint32_t shard_pitch,
                  const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *branches,
-                 const uint8_t *roots, const uint8_t *present, uint8_t *valid, uint8_t *leaves) {
+                 const uint8_t *roots, const uint8_t *present, uint8_t *valid, uint8_t *leaves, Ws *wsp = nullptr) {
     if (count < 0 || (count > 0 && (!shards || !roots || !valid || (c->depth > 0 && !branches))))
         return RBC_ERR_INVALID_ARG;
     if (shard_pitch % kAlign || (!shard_lens && (uniform_shard_len == 0 || uniform_shard_len > shard_pitch)))
@@ -403,9 +405,11 @@ int stage_verify(rbc_ctx *c, hipStream_t st, int count, const uint8_t *shards, u
     if (present && c->n <= 256) {
         uint32_t *vl = nullptr, *vc = nullptr;
         {
-            std::lock_guard<std::mutex> lk(c->mu);
-            RBC_HIP(c->ws.vlist.ensure((size_t)count * c->n * 4 + 64));
-            vl = c->ws.vlist.as<uint32_t>();
+            std::unique_lock<std::mutex> lk(c->mu, std::defer_lock);
+            if (!wsp) lk.lock();
+            Ws &w = wsp ? *wsp : c->ws;
+            RBC_HIP(w.vlist.ensure((size_t)count * c->n * 4 + 64));
+            vl = w.vlist.as<uint32_t>();
             vc = vl + (size_t)count * c->n;
         }
         RBC_HIP(hipMemsetAsync(vc, 0, 4, st));
@@ -416,9 +420,11 @@ int stage_verify(rbc_ctx *c, hipStream_t st, int count, const uint8_t *shards, u
     if (path_pays) {
         uint8_t *lv = leaves;
         if (!lv) {
-            std::lock_guard<std::mutex> lk(c->mu);
-            RBC_HIP(c->ws.vleaves.ensure((size_t)count * c->n * 32));
-            lv = c->ws.vleaves.as<uint8_t>();
+            std::unique_lock<std::mutex> lk(c->mu, std::defer_lock);
+            if (!wsp) lk.lock();
+            Ws &w = wsp ? *wsp : c->ws;
+            RBC_HIP(w.vleaves.ensure((size_t)count * c->n * 32));
+            lv = w.vleaves.as<uint8_t>();
         }
         a.leaves = lv;
         RBC_HIP(rbc_launch_sha_rows(a, false, st));
@@ -1845,6 +1851,11 @@ int rbc_validate_packed_leaves(rbc_ctx *c, int count, const uint8_t *arena, size
     return submit(c, s, ticket, []() { return RBC_OK; }, d2h);
 }
 
+static int host_receive(rbc_ctx *c, int count, const uint8_t *shards, size_t shard_pitch, const size_t *shard_lens,
+                        const uint8_t *present, const uint8_t *leaves, const uint8_t *branches, const uint8_t *roots,
+                        uint8_t *valid_out, uint8_t *values_out, size_t value_pitch, uint8_t *digests_out,
+                        int32_t *status_out, uint64_t *ticket);
+
 int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t shard_pitch,
                           const size_t *shard_lens, const uint8_t *present, const uint8_t *roots,
                           uint8_t *values_out, size_t value_pitch, uint8_t *digests_out, int32_t *status_out,
@@ -1861,6 +1872,28 @@ int rbc_interpolate_batch_verified(rbc_ctx *c, int count, const uint8_t *shards,
                                    const size_t *shard_lens, const uint8_t *present, const uint8_t *leaves,
                                    const uint8_t *roots, uint8_t *values_out, size_t value_pitch,
                                    uint8_t *digests_out, int32_t *status_out, uint64_t *ticket) {
+    return host_receive(c, count, shards, shard_pitch, shard_lens, present, leaves, nullptr, roots, nullptr,
+                        values_out, value_pitch, digests_out, status_out, ticket);
+}
+
+int rbc_receive_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t shard_pitch, const size_t *shard_lens,
+                      const uint8_t *present, const uint8_t *branches, const uint8_t *roots, uint8_t *valid_out,
+                      uint8_t *values_out, size_t value_pitch, uint8_t *digests_out, int32_t *status_out,
+                      uint64_t *ticket) {
+    if (count > 0 && (!branches || !valid_out)) return RBC_ERR_INVALID_ARG;
+    return host_receive(c, count, shards, shard_pitch, shard_lens, present, nullptr, branches, roots, valid_out,
+                        values_out, value_pitch, digests_out, status_out, ticket);
+}
+
+// The host-memory receiver behind rbc_interpolate_batch(_verified) and
+// rbc_receive_batch: the present rows cross PCIe once; with `branches` the
+// ECHO verify (validateMessage of every present row) runs on the device
+// first and interpolate reuses its leaves; with `leaves` the caller verified
+// them; with neither interpolate rehashes all N rows.
+static int host_receive(rbc_ctx *c, int count, const uint8_t *shards, size_t shard_pitch, const size_t *shard_lens,
+                        const uint8_t *present, const uint8_t *leaves, const uint8_t *branches, const uint8_t *roots,
+                        uint8_t *valid_out, uint8_t *values_out, size_t value_pitch, uint8_t *digests_out,
+                        int32_t *status_out, uint64_t *ticket) {
     if (!c || count < 0 ||
         (count > 0 && (!shards || !shard_lens || !present || !roots || !values_out || !status_out)))
         return RBC_ERR_INVALID_ARG;
@@ -1874,8 +1907,9 @@ int rbc_interpolate_batch_verified(rbc_ctx *c, int count, const uint8_t *shards,
     const size_t dpitch = round_up(Smax, 128);
     const size_t vpitch = round_up((size_t)c->k * Smax, 16);
     if ((size_t)c->n * dpitch > 0x7fffffffULL || vpitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
-    const int n = c->n, k = c->k;
+    const int n = c->n, k = c->k, d = c->depth;
     const size_t sh_bytes = (size_t)count * n * dpitch;
+    const size_t br_bytes = (size_t)count * n * std::max(d, 1) * 32;
     std::lock_guard<std::mutex> lk(c->mu);
     RBC_HIP(hipSetDevice(c->device));
     Slot *sp = acquire_slot(c);
@@ -1884,6 +1918,13 @@ int rbc_interpolate_batch_verified(rbc_ctx *c, int count, const uint8_t *shards,
     hipStream_t st = s.stream;
     RBC_HIP(s.d_shards.ensure(sh_bytes));
     RBC_HIP(s.d_valid.ensure((size_t)count * n));
+    if (branches) {
+        RBC_HIP(s.d_present.ensure((size_t)count * n));
+        RBC_HIP(s.d_branches.ensure(br_bytes));
+    }
+    // the present mask on the device: interpolate's valid mask itself, or
+    // (with `branches`) the verify's input, which writes valid
+    uint8_t *d_pres = branches ? s.d_present.as<uint8_t>() : s.d_valid.as<uint8_t>();
     RBC_HIP(s.d_leaves.ensure((size_t)count * n * 32));
     RBC_HIP(s.d_roots.ensure((size_t)count * 32));
     RBC_HIP(s.d_values.ensure((size_t)count * vpitch));
@@ -1906,14 +1947,14 @@ int rbc_interpolate_batch_verified(rbc_ctx *c, int count, const uint8_t *shards,
     uint8_t *i_rt = reinterpret_cast<uint8_t *>(ln + count), *i_pr = i_rt + (size_t)count * 32;
     // present mask first: the zero-copy gather reads it
     memcpy(i_pr, present, (size_t)count * n);
-    RBC_HIP(hipMemcpyAsync(s.d_valid.p, i_pr, (size_t)count * n, hipMemcpyHostToDevice, st));
+    RBC_HIP(hipMemcpyAsync(d_pres, i_pr, (size_t)count * n, hipMemcpyHostToDevice, st));
     const uint8_t *zc = in_direct ? host_zero_copy(shards, ((size_t)count * n - 1) * shard_pitch + Smax)
                                             : nullptr;
     if (zc) {
         // only the received rows cross PCIe (N-f of N at the bench shape)
         for (int i = 0; i < count; ++i) ln[i] = (uint32_t)shard_lens[i];
-        RBC_HIP(rbc_launch_gather_present(zc, shard_pitch, (uint32_t)Smax, s.d_valid.as<uint8_t>(),
-                                          s.d_shards.as<uint8_t>(), (uint32_t)dpitch, (uint32_t)(count * n), st));
+        RBC_HIP(rbc_launch_gather_present(zc, shard_pitch, (uint32_t)Smax, d_pres, s.d_shards.as<uint8_t>(),
+                                          (uint32_t)dpitch, (uint32_t)(count * n), st));
     } else if (in_direct) {
         for (int i = 0; i < count; ++i) ln[i] = (uint32_t)shard_lens[i];
         if (dpitch > Smax) RBC_HIP(hipMemsetAsync(s.d_shards.p, 0, sh_bytes, st));
@@ -1936,18 +1977,27 @@ int rbc_interpolate_batch_verified(rbc_ctx *c, int count, const uint8_t *shards,
     RBC_HIP(hipMemcpyAsync(s.d_slens.p, ln, (size_t)count * 4, hipMemcpyHostToDevice, st));
     if (leaves)  // 32 B per row (1/744 of a C2 row): the whole [count][n][32] block in one copy
         RBC_HIP(hipMemcpyAsync(s.d_leaves.p, leaves, (size_t)count * n * 32, hipMemcpyHostToDevice, st));
+    int rc = RBC_OK;
+    if (branches) {  // validateMessage of every present row on the device, its leaves kept for interpolate
+        RBC_HIP(hipMemcpyAsync(s.d_branches.p, branches, br_bytes, hipMemcpyHostToDevice, st));
+        rc = stage_verify(c, st, count, s.d_shards.as<uint8_t>(), (uint32_t)dpitch, s.d_slens.as<uint32_t>(), 0,
+                          s.d_branches.as<uint8_t>(), s.d_roots.as<uint8_t>(), d_pres, s.d_valid.as<uint8_t>(),
+                          s.d_leaves.as<uint8_t>(), &s.ws);
+        if (rc) return rc;
+    }
     // ragged batch: bytes past k*S_i of a value row are returned as zero
     RBC_HIP(hipMemsetAsync(s.d_values.p, 0, (size_t)count * vpitch, st));
-    int rc = stage_interpolate(c, s.ws, st, count, s.d_shards.as<uint8_t>(), (uint32_t)dpitch,
+    rc = stage_interpolate(c, s.ws, st, count, s.d_shards.as<uint8_t>(), (uint32_t)dpitch,
                                s.d_slens.as<uint32_t>(), 0, s.d_valid.as<uint8_t>(), s.d_leaves.as<uint8_t>(),
-                               leaves ? 1 : 0,
+                               (leaves || branches) ? 1 : 0,
                                s.d_roots.as<uint8_t>(), s.d_values.as<uint8_t>(), (uint32_t)vpitch,
                                s.d_digests.as<uint8_t>(), s.d_status.as<int32_t>());
     if (rc) return rc;
     uint8_t *o_val = s.h_out.as<uint8_t>(), *o_dig = o_val + out_stage;
     int32_t *o_st = reinterpret_cast<int32_t *>(o_dig + (size_t)count * 32);
-    void *d_val = s.d_values.p, *d_dig = s.d_digests.p, *d_st = s.d_status.p;
+    void *d_val = s.d_values.p, *d_dig = s.d_digests.p, *d_st = s.d_status.p, *d_vd = s.d_valid.p;
     auto d2h = [=]() -> int {
+        if (valid_out) RBC_HIP(hipMemcpyAsync(valid_out, d_vd, (size_t)count * n, hipMemcpyDeviceToHost, st));
         if (out_direct && value_pitch == vpitch)  // one contiguous DMA (a 2-D copy runs as a blit kernel)
             RBC_HIP(hipMemcpyAsync(values_out, d_val, (size_t)(count - 1) * vpitch + (size_t)k * Smax,
                                    hipMemcpyDeviceToHost, st));

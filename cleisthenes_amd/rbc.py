@@ -497,6 +497,40 @@ class Context:
         out = {"values": values, "digests": digests, "status": status}
         return HostTicket(self, t.value, out, keep=(shards, present, roots, sl, lv))
 
+    def receive_batch(self, shards, shard_lens, present, branches, roots, **kw) -> dict:
+        return self.receive_submit(shards, shard_lens, present, branches, roots, **kw).wait()
+
+    def receive_submit(self, shards: np.ndarray, shard_lens, present: np.ndarray, branches: np.ndarray,
+                       roots: np.ndarray, values_out: Optional[np.ndarray] = None,
+                       valid_out: Optional[np.ndarray] = None, digests_out: Optional[np.ndarray] = None,
+                       status_out: Optional[np.ndarray] = None) -> "HostTicket":
+        """Asynchronous rbc_receive_batch: ECHO verify of every present row
+        (branches [count][n][depth][32], device form) and interpolate of the
+        valid ones, the present rows crossing PCIe once; .wait() gives
+        {"valid", "values", "digests", "status"}."""
+        shards = shards if (shards.dtype == np.uint8 and shards.flags.c_contiguous) else \
+            np.ascontiguousarray(shards, dtype=np.uint8)
+        count, n, pitch = shards.shape
+        assert n == self.n
+        present = np.ascontiguousarray(present, dtype=np.uint8)
+        br = branches if (branches.dtype == np.uint8 and branches.flags.c_contiguous) else \
+            np.ascontiguousarray(branches, dtype=np.uint8)
+        assert br.size == count * n * max(self.depth, 1) * 32
+        roots = np.ascontiguousarray(roots, dtype=np.uint8)
+        sl = (c_size_t * count)(*[int(x) for x in shard_lens])
+        vp = self.k * int(max(shard_lens))
+        values = np.zeros((count, max(vp, 1)), np.uint8) if values_out is None else values_out
+        assert values.shape == (count, max(vp, 1))
+        valid = np.zeros((count, n), np.uint8) if valid_out is None else valid_out
+        digests = np.zeros((count, 32), np.uint8) if digests_out is None else digests_out
+        status = np.zeros(count, np.int32) if status_out is None else status_out
+        t = c_uint64(0)
+        check(lib.rbc_receive_batch(self._p, count, _ptr(shards), pitch, sl, _ptr(present), _ptr(br), _ptr(roots),
+                                    _ptr(valid), _ptr(values), values.shape[1], _ptr(digests),
+                                    status.ctypes.data_as(_lib.i32p), byref(t)), "rbc_receive_batch")
+        out = {"valid": valid, "values": values, "digests": digests, "status": status}
+        return HostTicket(self, t.value, out, keep=(shards, present, br, roots, sl))
+
     # ---- device-resident stages --------------------------------------------
     def dev_encode(self, stream, count, values, value_pitch, value_lens, uniform_len, shards, shard_pitch):
         check(lib.rbc_dev_encode(self._p, _dv(stream), count, _dv(values), value_pitch, _dv(value_lens),

@@ -335,6 +335,20 @@ int rbc_interpolate_batch_verified(rbc_ctx *ctx, int count, const uint8_t *shard
                                    const size_t *shard_lens, const uint8_t *present, const uint8_t *leaves,
                                    const uint8_t *roots, uint8_t *values_out, size_t value_pitch,
                                    uint8_t *digests_out, int32_t *status_out, uint64_t *ticket);
+/* ABI 6: the receiver's whole batch in one submission, for a batching host
+ * that holds each instance's received ECHOs together (validateMessage of
+ * every present row, rbc/rbc.go:92-95, then interpolate of the ones that
+ * validated, rbc/rbc.go:86-90): the present rows cross PCIe ONCE (from a
+ * pinned, uniform-length buffer only those rows are read), are verified on
+ * the device against branches [count][n][depth][32] (device form: a zero
+ * slot for an empty level-0 sibling) and roots [count][32], and interpolate
+ * reuses the leaves the verify computed.  valid_out [count][n] = present &&
+ * the branch proves the row (the validateMessage verdicts); values_out /
+ * digests_out / status_out as rbc_interpolate_batch over the valid rows. */
+int rbc_receive_batch(rbc_ctx *ctx, int count, const uint8_t *shards, size_t shard_pitch, const size_t *shard_lens,
+                      const uint8_t *present, const uint8_t *branches, const uint8_t *roots, uint8_t *valid_out,
+                      uint8_t *values_out, size_t value_pitch, uint8_t *digests_out, int32_t *status_out,
+                      uint64_t *ticket);
 int rbc_wait(rbc_ctx *ctx, uint64_t ticket);
 int rbc_poll(rbc_ctx *ctx, uint64_t ticket, int *done);
 

@@ -193,3 +193,35 @@ def test_batcher_validate_leaf_then_interpolate_verified(gpu):
             rows = np.stack([np.frombuffer(s, np.uint8) if s else np.zeros(S, np.uint8) for s in shards])
             st, val, dig = rbc_ref.interpolate(n, f, rows, valid, e["roots"][i].tobytes())
             assert st == 0 and val.tobytes() == r["value"] and dig == r["digest"]
+
+
+@pytest.mark.parametrize("n,f,B,pinned", [(128, 42, 44 * 600 + 7, True), (128, 42, 44 * 600 + 7, False),
+                                          (256, 85, 86 * 380, True), (37, 12, 13 * 70, True)])
+def test_receive_batch_fused_equals_validate_then_interpolate(gpu, n, f, B, pinned):
+    """rbc_receive_batch: the present rows cross PCIe once, are verified on
+    the device (the walk at N <= 128, leaves + merkle_path_kernel at N = 256)
+    and interpolate reuses the verify's leaves.  Its verdicts equal the
+    oracle's validateMessage of every present row (tampered ECHOs rejected),
+    and values / digests / statuses equal the full-rehash interpolate over the
+    rows that validated, and the input values."""
+    count = 24
+    e = _epoch(n, f, count, B, seed=7 * n + B % 11)
+    ctx = gpu.Context(n, f)
+    S = e["S"]
+    buf, pitch = _receive_buffer(gpu, e, n, pinned)
+    d = e["br"].shape[2]
+    br = gpu.pinned_empty((count, n, max(d, 1), 32)) if pinned else np.zeros((count, n, max(d, 1), 32), np.uint8)
+    br[:] = e["br"].reshape(count, n, max(d, 1), 32)
+    got = ctx.receive_batch(buf, [S] * count, e["present"], br, e["roots"])
+    want_valid = e["present"].copy()
+    for i in np.flatnonzero(e["bad"] >= 0):
+        want_valid[i, e["bad"][i]] = 0
+    assert np.array_equal(got["valid"], want_valid)
+    for i in range(0, count, 6):  # the verdicts vs the oracle's validateMessage
+        for j in np.flatnonzero(e["present"][i])[::9]:
+            assert bool(got["valid"][i, j]) == rbc_ref.verify(n, buf[i, j, :S], int(j), e["br"][i, j], e["roots"][i].tobytes())
+    full = ctx.interpolate_batch(np.array(buf), [S] * count, want_valid, e["roots"])
+    assert (got["status"] == 0).all() and np.array_equal(got["status"], full["status"])
+    assert np.array_equal(got["values"], full["values"]) and np.array_equal(got["digests"], full["digests"])
+    for i in range(count):
+        assert got["values"][i, :B].tobytes() == e["vals"][i].tobytes(), i

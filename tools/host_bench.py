@@ -180,14 +180,19 @@ def epoch(ca, n, f, B, instances=1024, sub=128, ring=3, inflight=2, device=0, se
         mroots = ca.pinned_empty((m, 32))
         mroots[:] = com["roots"][inst]
         meta = {"lens": np.full(m, S, np.uint32), "idx": pos.astype(np.uint8), "offs": offs}
-        rx.append(dict(buf=buf, present=present, bad=bad, inst=inst, pos=pos, br=br, mroots=mroots,
-                       roots=com["roots"].copy(), want=bad[inst] != pos, **meta))
+        brall = ca.pinned_empty((sub, n, max(d, 1), 32))
+        brall[:] = com["branches"].reshape(sub, n, max(d, 1), 32)
+        want_valid = present.copy()
+        want_valid[np.flatnonzero(bad >= 0), bad[bad >= 0]] = 0
+        rx.append(dict(buf=buf, present=present, bad=bad, inst=inst, pos=pos, br=br, mroots=mroots, brall=brall,
+                       roots=com["roots"].copy(), want=bad[inst] != pos, want_valid=want_valid, **meta))
     vout = ca.pinned_empty((instances, k * S))
     digests = np.zeros((instances, 32), np.uint8)
     status = np.full(instances, 99, np.int32)
     mmax = sub * (n - f)
     vres = [{"ok": ca.pinned_empty((mmax,)), "leaves": ca.pinned_empty((mmax, 32))} for _ in range(inflight + 1)]
     lvs = [ca.pinned_empty((sub, n, 32)) for _ in range(inflight + 1)]
+    vmask = [np.zeros((sub, n), np.uint8) for _ in range(inflight + 1)]
     roots_out = np.zeros((instances, 32), np.uint8)
     verdict_bad = [0]
 
@@ -217,9 +222,17 @@ def epoch(ca, n, f, B, instances=1024, sub=128, ring=3, inflight=2, device=0, se
         return ctx.interpolate_submit(R["buf"][:c], [S] * c, valid, R["roots"][:c], values_out=vout[lo:lo + c],
                                       leaves=lv, digests_out=digests[lo:lo + c], status_out=status[lo:lo + c])
 
+    def receive(b, slot):
+        """rbc_receive_batch: verify + interpolate in one submission, the ECHO rows crossing PCIe once."""
+        R, c = rx[b % ring], counts[b]
+        lo = b * sub
+        return ctx.receive_submit(R["buf"][:c], [S] * c, R["present"][:c], R["brall"][:c], R["roots"][:c],
+                                  values_out=vout[lo:lo + c], valid_out=vmask[slot][:c],
+                                  digests_out=digests[lo:lo + c], status_out=status[lo:lo + c])
+
     def run(kinds):
         """One epoch, the given sides concurrently; returns wall seconds."""
-        live = {"c": [], "v": [], "i": []}
+        live = {"c": [], "v": [], "i": [], "r": []}
         t0 = _t.perf_counter()
         for b in range(nsub + 1):
             if b < nsub:
@@ -227,6 +240,8 @@ def epoch(ca, n, f, B, instances=1024, sub=128, ring=3, inflight=2, device=0, se
                     live["c"].append((b, commit(b, b % (inflight + 1))))
                 if "v" in kinds:
                     live["v"].append((b, validate(b, b % (inflight + 1))))
+                if "r" in kinds:
+                    live["r"].append((b, receive(b, b % (inflight + 1))))
             # the receive side: interpolate a sub-batch once its validate is back
             while live["v"] and (len(live["v"]) > inflight - 1 or b == nsub):
                 bv, tv = live["v"].pop(0)
@@ -235,42 +250,57 @@ def epoch(ca, n, f, B, instances=1024, sub=128, ring=3, inflight=2, device=0, se
                     live["i"].append((bv, interpolate(bv, bv % (inflight + 1), ok, leaves)))
                 if b < nsub:
                     break
-            for kd in ("c", "i"):
+            for kd in ("c", "i", "r"):
                 while live[kd] and (len(live[kd]) >= inflight or b == nsub):
                     bb, tt = live[kd].pop(0)
                     res = tt.wait()
                     if kd == "c":
                         roots_out[bb * sub: bb * sub + counts[bb]] = res["roots"]
+                    elif kd == "r":  # the fused receive's verdicts
+                        R, c = rx[bb % ring], counts[bb]
+                        verdict_bad[0] += int((res["valid"] != R["want_valid"][:c]).sum())
         return _t.perf_counter() - t0
 
-    # warm every slot's buffers, then time the epoch with all three sides together
-    run("cvi")
-    status[:] = 99
-    vout[:] = 0
-    verdict_bad[0] = 0
-    if barrier:
-        barrier()
-    el = run("cvi")
-    if barrier:
-        barrier()
-    # ---- checks (untimed): verdicts, every value, statuses, proposer roots
-    vals_ok = all(np.array_equal(vout[b * sub: b * sub + counts[b], :B], vals[b % ring][:counts[b]])
-                  for b in range(nsub))
-    roots_ok = all(np.array_equal(roots_out[b * sub: b * sub + counts[b]], rx[b % ring]["roots"][:counts[b]])
-                   for b in range(nsub))
+    def timed(kinds):
+        """warm every slot's buffers, then time one epoch of `kinds` (all ranks together) and check it:
+        verdicts, every value, statuses, proposer roots"""
+        run(kinds)
+        status[:] = 99
+        vout[:] = 0
+        roots_out[:] = 0
+        verdict_bad[0] = 0
+        if barrier:
+            barrier()
+        el = run(kinds)
+        if barrier:
+            barrier()
+        vals_ok = all(np.array_equal(vout[b * sub: b * sub + counts[b], :B], vals[b % ring][:counts[b]])
+                      for b in range(nsub))
+        roots_ok = all(np.array_equal(roots_out[b * sub: b * sub + counts[b]], rx[b % ring]["roots"][:counts[b]])
+                       for b in range(nsub))
+        chk = {"verdict_mismatches": verdict_bad[0], "values_ok": bool(vals_ok), "decoded": int((status == 0).sum()),
+               "roots_ok": bool(roots_ok)}
+        return el, chk, bool(vals_ok and roots_ok and verdict_bad[0] == 0 and (status == 0).all())
+
+    el, checks, ok = timed("cvi")  # the drop-in's calls: shard_commit || validate -> interpolate
+    el_f, checks_f, ok_f = timed("cr")  # shard_commit || the fused receive
     shard_bytes = instances * n * S
     echo = sum(int((rx[b % ring]["inst"] < counts[b]).sum()) for b in range(nsub))
     h2d = instances * B + 2 * echo * S  # values, ECHO rows for validate, the valid ECHO rows for interpolate
     d2h = shard_bytes + instances * n * d * 32 + instances * k * S
+    h2d_f = instances * B + echo * S  # the fused receive moves the ECHO rows once
     out = {"GBps": round(shard_bytes / el / 1e9, 3), "seconds": round(el, 4), "instances": instances,
            "sub_batch": sub, "inflight": inflight, "echo_messages": echo,
            "pcie_GBps": {"h2d": round(h2d / el / 1e9, 2), "d2h": round(d2h / el / 1e9, 2)},
-           "checks": {"verdict_mismatches": verdict_bad[0], "values_ok": bool(vals_ok),
-                      "decoded": int((status == 0).sum()), "roots_ok": bool(roots_ok)},
-           "ok": bool(vals_ok and roots_ok and verdict_bad[0] == 0 and (status == 0).all())}
+           "checks": checks, "ok": ok and ok_f,
+           "fused": {"GBps": round(shard_bytes / el_f / 1e9, 3), "seconds": round(el_f, 4), "checks": checks_f,
+                     "ok": ok_f, "pcie_GBps": {"h2d": round(h2d_f / el_f / 1e9, 2), "d2h": round(d2h / el_f / 1e9, 2)},
+                     "path": "rbc_shard_commit || rbc_receive_batch (ECHO rows cross PCIe once, verified on the "
+                             "device, interpolate reusing the leaves)"}}
     if phases:  # each side alone over the same epoch: which one binds
         alone = {}
-        for name, kinds in (("shard_commit", "c"), ("validate", "v"), ("validate+interpolate", "vi")):
+        for name, kinds in (("shard_commit", "c"), ("validate", "v"), ("validate+interpolate", "vi"),
+                            ("receive_fused", "r")):
             alone[name] = round(shard_bytes / run(kinds) / 1e9, 3)
         out["alone_GBps"] = alone
     ctx.close()
