@@ -795,6 +795,8 @@ def report(args, ctx, I, n, k, d, S, present_h, corrupt_h, stage_ms, iso, elapse
              "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "algorithmic_bytes_per_launch": int(nbytes),
              "avg_ms": round(ms, 4), "span": span or f"HIP events around the launch on its stream ({stage})"}
         pk = pm.get("kernels", {}).get(name)
+        if pk and name.startswith("decode") and pm.get("value_form") != ("joined" if args.join else "row view"):
+            pk = None  # the decode writes the joined value in one form and not the other: other traffic
         if pk:
             r["traffic"], r["traffic_source"] = pk["hbm_bytes_per_launch"], pmc_path
         if ncomp:

@@ -1,6 +1,12 @@
-"""Oracle tests (CPU).  Pins the restatement of klauspost/reedsolomon v1.9.1
-to klauspost's own unit-test vectors, SHA-256 to FIPS 180-4, and checks the
-C restatement (oracle/librbc_ref.so) against the Python one and against the
+"""Oracle tests (CPU).  Checks the restatement of klauspost/reedsolomon
+v1.9.1 against known answers from klauspost's unit tests (galois_test.go,
+matrix_test.go, TestOneEncode) -- answers RECALLED from that published test
+suite and re-derived here by hand, NOT vectors held in /root/reference
+(klauspost is not vendored there and the reference's own RBC tests are
+empty, rbc/rbc_internal_test.go:21-31), so the RS layer's parity stays
+"unpinned" in the task's sense, as does the Merkle layer (a convention frozen
+here).  Also SHA-256 against FIPS 180-4, and the C
+restatement (oracle/librbc_ref.so) against the Python one and against the
 committed golden fixtures."""
 import hashlib
 
@@ -11,8 +17,9 @@ from hypothesis import strategies as st
 
 import rbc_oracle as orc
 
-# ---- klauspost/reedsolomon known answers (galois_test.go, matrix_test.go,
-#      reedsolomon_test.go TestOneEncode; Backblaze JavaReedSolomon shares them)
+# ---- klauspost/reedsolomon known answers, recalled from its published tests
+#      (galois_test.go, matrix_test.go, reedsolomon_test.go TestOneEncode;
+#      Backblaze JavaReedSolomon shares them) -- not files in /root/reference
 
 
 def test_galois_known_answers():
