@@ -166,7 +166,10 @@ struct Slot {
 
 // host-API submissions in flight per context: the batcher keeps 4 launches
 // in flight (tools/batcher_bench.cpp), and the box has 4 hardware queues
-constexpr int kHostSlots = 4;
+#ifndef RBC_HOST_SLOTS
+#define RBC_HOST_SLOTS 4
+#endif
+constexpr int kHostSlots = RBC_HOST_SLOTS;
 
 }  // namespace
 

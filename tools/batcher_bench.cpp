@@ -289,7 +289,9 @@ int validate_sweep(int argc, char **argv) {
 // row and root is checked; the two timed passes must agree bit for bit
 // (values, digests); `dump` receives sampled (value, root, digest) records for
 // the oracle check in tests/test_gpu_batcher.py.
-//   tools/batcher_bench epoch [instances] [threads] [window] [max_wait_us] [dump]
+// `kinds` (default svi) drops request kinds for a breakdown: s = shard, v =
+// validate, i = interpolate (with v: of the ECHOs that validated).
+//   tools/batcher_bench epoch [instances] [threads] [window] [max_wait_us] [dump|-] [kinds]
 int epoch(int argc, char **argv) {
     const int n = 128, f = 42, k = n - 2 * f, d = 7, R = n - f;
     const size_t B = 1 << 20, S = (B + k - 1) / k;
@@ -297,7 +299,10 @@ int epoch(int argc, char **argv) {
     const int T = argc > 2 ? atoi(argv[2]) : 16;
     const int W = argc > 3 ? atoi(argv[3]) : 8;
     const int WAIT = argc > 4 ? atoi(argv[4]) : 200;
-    const char *dump = argc > 5 ? argv[5] : nullptr;
+    const char *dump = argc > 5 && strcmp(argv[5], "-") ? argv[5] : nullptr;
+    const char *kinds = argc > 6 ? argv[6] : "svi";
+    const bool ks = strchr(kinds, 's') != nullptr, kv = strchr(kinds, 'v') != nullptr,
+               ki = strchr(kinds, 'i') != nullptr;
     rbc_ctx *ctx;
     CK(rbc_ctx_create(n, f, 0, &ctx));
     std::vector<uint8_t> values((size_t)I * B);
@@ -351,8 +356,8 @@ int epoch(int argc, char **argv) {
     double secs[2] = {0, 0};
     uint64_t launches[2] = {0, 0}, reqs[2] = {0, 0};
     // pass 0: warm-up (verified); pass 1: timed, leaves reused; pass 2: timed, full rehash
-    for (int pass = 0; pass < 3; ++pass) {
-        const bool verified = pass < 2;
+    for (int pass = 0; pass < (ki && kv ? 3 : 2); ++pass) {
+        const bool verified = pass < 2 && kv;
         const int o = pass == 2 ? 1 : 0;
         rbc_batcher *b;
         CK(rbc_batcher_create(ctx, 64, WAIT, &b));
@@ -368,13 +373,17 @@ int epoch(int argc, char **argv) {
                     std::vector<const uint8_t *> ptr(n, nullptr);
                     std::vector<size_t> len(n, 0);
                     for (int m = 0; m < R; ++m) {
-                        if (rbc_batcher_wait(b, s.tv[m]) != RBC_OK) ++bad_count;
                         const int j = recv[(size_t)s.i * R + m];
-                        const int v = ok[(size_t)s.i * R + m];
-                        if (v != (j != bad[s.i])) ++bad_count;
+                        int v = j != bad[s.i];  // without validates: the rows a validate would pass
+                        if (kv) {
+                            if (rbc_batcher_wait(b, s.tv[m]) != RBC_OK) ++bad_count;
+                            if (ok[(size_t)s.i * R + m] != v) ++bad_count;
+                            v = ok[(size_t)s.i * R + m];
+                        }
                         if (v == 1) { ptr[j] = echo(s.i, j); len[j] = S; }
                     }
                     const size_t i = s.i;
+                    if (!ki) return;
                     if (verified)
                         CK(rbc_batcher_interpolate_verified(b, roots_c.data() + i * 32, ptr.data(), len.data(),
                                                             leaf.data() + i * n * 32, vout[o].data() + i * k * S,
@@ -385,17 +394,19 @@ int epoch(int argc, char **argv) {
                                                    &s.ti));
                 };
                 auto finish_interp = [&](Inst &s) {
-                    if (rbc_batcher_wait(b, s.ti) != RBC_OK) ++bad_count;
-                    if (rbc_batcher_wait(b, s.ts) != RBC_OK) ++bad_count;
+                    if (ki && rbc_batcher_wait(b, s.ti) != RBC_OK) ++bad_count;
+                    if (ks && rbc_batcher_wait(b, s.ts) != RBC_OK) ++bad_count;
                 };
                 for (;;) {
                     int i = -1;
                     if ((int)va.size() < W && (i = next.fetch_add(1)) < I) {
                         Inst s{i, 0, 0, std::vector<uint64_t>(R)};
-                        CK(rbc_batcher_shard(b, values.data() + (size_t)i * B, B, sh_out.data() + (size_t)i * n * S,
-                                             n * S, &slen[i], root_out.data() + (size_t)i * 32,
-                                             br_out.data() + (size_t)i * n * d * 32, &s.ts));
-                        for (int m = 0; m < R; ++m) {
+                        if (ks)
+                            CK(rbc_batcher_shard(b, values.data() + (size_t)i * B, B,
+                                                 sh_out.data() + (size_t)i * n * S, n * S, &slen[i],
+                                                 root_out.data() + (size_t)i * 32,
+                                                 br_out.data() + (size_t)i * n * d * 32, &s.ts));
+                        for (int m = 0; m < R && kv; ++m) {
                             const int j = recv[(size_t)i * R + m];
                             CK(rbc_batcher_validate_leaf(b, roots_c.data() + (size_t)i * 32,
                                                          br_c.data() + ((size_t)i * n + j) * d * 32, d * 32, echo(i, j),
@@ -427,21 +438,24 @@ int epoch(int argc, char **argv) {
         // checks: every value, every proposer shard row / root (the verdicts were checked by the clients)
         int vbad = 0, sbad = 0;
         for (int i = 0; i < I; ++i) {
-            vbad += vlen[i] != k * S || memcmp(vout[o].data() + (size_t)i * k * S, values.data() + (size_t)i * B, B) != 0;
-            sbad += slen[i] != S || memcmp(root_out.data() + (size_t)i * 32, roots_c.data() + (size_t)i * 32, 32) != 0 ||
-                    memcmp(sh_out.data() + (size_t)i * n * S, shards_c.data() + (size_t)i * n * S, n * S) != 0;
+            if (ki)
+                vbad += vlen[i] != k * S ||
+                        memcmp(vout[o].data() + (size_t)i * k * S, values.data() + (size_t)i * B, B) != 0;
+            if (ks)
+                sbad += slen[i] != S || memcmp(root_out.data() + (size_t)i * 32, roots_c.data() + (size_t)i * 32, 32) != 0 ||
+                        memcmp(sh_out.data() + (size_t)i * n * S, shards_c.data() + (size_t)i * n * S, n * S) != 0;
         }
         fails += vbad + sbad;
-        printf("{\"phase\": \"epoch\", \"interpolate\": \"%s\", \"instances\": %d, \"threads\": %d, \"window\": %d, "
+        printf("{\"phase\": \"epoch\", \"kinds\": \"%s\", \"interpolate\": \"%s\", \"instances\": %d, \"threads\": %d, \"window\": %d, "
                "\"echo_messages\": %d, \"max_wait_us\": %d, \"seconds\": %.4f, \"GBps\": %.3f, \"requests\": %llu, "
                "\"launches\": %llu, \"value_failures\": %d, \"shard_failures\": %d, \"client_failures\": %d}\n",
-               verified ? "verified (leaves reused)" : "full rehash", I, T, W, I * R, WAIT, dt,
+               kinds, verified ? "verified (leaves reused)" : "full rehash", I, T, W, I * R, WAIT, dt,
                (double)I * n * S / dt / 1e9, (unsigned long long)reqs[o], (unsigned long long)launches[o], vbad, sbad,
                bad_count.load());
         fflush(stdout);
     }
     // the leaf-reusing and the full-rehash interpolate agree bit for bit
-    const int same = vout[0] == vout[1] && dig[0] == dig[1];
+    const int same = !(ki && kv) || (vout[0] == vout[1] && dig[0] == dig[1]);
     fails += !same;
     if (dump) {  // sampled records for the oracle (tests only read this)
         FILE *fp = fopen(dump, "wb");

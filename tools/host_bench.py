@@ -313,6 +313,9 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--batches", type=int, default=8)
     ap.add_argument("--inflight", type=int, default=2)
+    ap.add_argument("--epoch", type=int, default=0,
+                    help="instead: one host-fed epoch of this many instances (the bench's pcie_inclusive leg)")
+    ap.add_argument("--sub", type=int, default=0, help="epoch sub-batch (default: ~400 MB of shards)")
     ap.add_argument("--pinned", action="store_true",
                     help="values, shard/root/branch outputs and interpolate buffers in rbc_host_alloc memory "
                          "(the C ABI then copies to and from them directly, no staging memcpy)")
@@ -320,6 +323,13 @@ def main():
     import cleisthenes_amd as ca
 
     n, f, B = CFG[args.config]
+    if args.epoch:
+        k = n - 2 * f
+        S = (B + k - 1) // k
+        sub = args.sub or max(1, min(args.epoch, int(400e6 // (n * S))))
+        r = epoch(ca, n, f, B, instances=args.epoch, sub=sub, inflight=args.inflight)
+        print(json.dumps({"config": args.config, "library": ca.rbc.library_path(), **r}))
+        return
     r = measure(ca, n, f, B, args.batch, args.batches, args.inflight, args.pinned)
     print(json.dumps({
         "metric": "host-path RBC shard GB/s (PCIe-inclusive, host buffers in and out)",
