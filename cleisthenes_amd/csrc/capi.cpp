@@ -1469,8 +1469,12 @@ static bool host_pinned(const void *p, size_t bytes) {
 // The device address of pinned caller memory when it is the host address itself
 // (hipHostMalloc / rbc_host_alloc under unified addressing), else NULL: a
 // kernel may then read it directly over PCIe.
+inline int n_of(const rbc_ctx *c) { return c->n; }
+#ifndef RBC_ZERO_COPY_READS
+#define RBC_ZERO_COPY_READS 1
+#endif
 static const uint8_t *host_zero_copy(const void *p, size_t bytes) {
-    if (!host_pinned(p, bytes)) return nullptr;
+    if (!RBC_ZERO_COPY_READS || !host_pinned(p, bytes)) return nullptr;
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();
@@ -1907,7 +1911,17 @@ static int host_receive(rbc_ctx *c, int count, const uint8_t *shards, size_t sha
         Smax = std::max(Smax, shard_lens[i]);
     }
     if (value_pitch < (size_t)c->k * Smax) return RBC_ERR_INVALID_ARG;
-    const size_t dpitch = round_up(Smax, 128);
+    // direct H2D of a pinned, uniform-length batch; pinned staging only for
+    // what is not already pinned caller memory
+    bool uniform = true;
+    for (int i = 0; i < count && uniform; ++i) uniform = shard_lens[i] == Smax;
+    const bool in_direct = uniform && host_pinned(shards, ((size_t)count * n_of(c) - 1) * shard_pitch + Smax);
+    const uint8_t *zc = in_direct ? host_zero_copy(shards, ((size_t)count * n_of(c) - 1) * shard_pitch + Smax)
+                                  : nullptr;
+    // a pinned batch whose pitch the device rows can take moves in ONE plain
+    // copy (a pitched 2-D copy runs as a blit kernel)
+    const bool flat = in_direct && !zc && shard_pitch % kAlign == 0;
+    const size_t dpitch = flat ? shard_pitch : round_up(Smax, 128);
     const size_t vpitch = round_up((size_t)c->k * Smax, 16);
     if ((size_t)c->n * dpitch > 0x7fffffffULL || vpitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
     const int n = c->n, k = c->k, d = c->depth;
@@ -1934,12 +1948,6 @@ static int host_receive(rbc_ctx *c, int count, const uint8_t *shards, size_t sha
     RBC_HIP(s.d_digests.ensure((size_t)count * 32));
     RBC_HIP(s.d_status.ensure((size_t)count * 4));
     RBC_HIP(s.d_slens.ensure((size_t)count * 4));
-    // direct H2D of a pinned, uniform-length batch (bytes past S must arrive
-    // as zero: the rows are zeroed on the device first); pinned staging only
-    // for what is not already pinned caller memory
-    bool uniform = true;
-    for (int i = 0; i < count && uniform; ++i) uniform = shard_lens[i] == Smax;
-    const bool in_direct = uniform && host_pinned(shards, ((size_t)count * n - 1) * shard_pitch + Smax);
     const bool out_direct = host_pinned(values_out, (size_t)(count - 1) * value_pitch + (size_t)k * Smax);
     const size_t in_stage = in_direct ? 0 : sh_bytes, out_stage = out_direct ? 0 : (size_t)count * vpitch;
     RBC_HIP(s.h_in.ensure(in_stage + (size_t)count * (n + 32 + 4)));
@@ -1951,14 +1959,17 @@ static int host_receive(rbc_ctx *c, int count, const uint8_t *shards, size_t sha
     // present mask first: the zero-copy gather reads it
     memcpy(i_pr, present, (size_t)count * n);
     RBC_HIP(hipMemcpyAsync(d_pres, i_pr, (size_t)count * n, hipMemcpyHostToDevice, st));
-    const uint8_t *zc = in_direct ? host_zero_copy(shards, ((size_t)count * n - 1) * shard_pitch + Smax)
-                                            : nullptr;
     if (zc) {
         // only the received rows cross PCIe (N-f of N at the bench shape)
         for (int i = 0; i < count; ++i) ln[i] = (uint32_t)shard_lens[i];
         RBC_HIP(rbc_launch_gather_present(zc, shard_pitch, (uint32_t)Smax, d_pres, s.d_shards.as<uint8_t>(),
                                           (uint32_t)dpitch, (uint32_t)(count * n), st));
-    } else if (in_direct) {
+    } else if (flat) {  // every row, one copy; bytes past S must be zero on the device
+        for (int i = 0; i < count; ++i) ln[i] = (uint32_t)shard_lens[i];
+        RBC_HIP(hipMemcpyAsync(s.d_shards.p, shards, sh_bytes, hipMemcpyHostToDevice, st));
+        if (dpitch > Smax)
+            RBC_HIP(hipMemset2DAsync(s.d_shards.as<uint8_t>() + Smax, dpitch, 0, dpitch - Smax, (size_t)count * n, st));
+    } else if (in_direct) {  // bytes past S must arrive as zero: the rows are zeroed on the device first
         for (int i = 0; i < count; ++i) ln[i] = (uint32_t)shard_lens[i];
         if (dpitch > Smax) RBC_HIP(hipMemsetAsync(s.d_shards.p, 0, sh_bytes, st));
         RBC_HIP(hipMemcpy2DAsync(s.d_shards.p, dpitch, shards, shard_pitch, Smax, (size_t)count * n,

@@ -261,6 +261,8 @@ def epoch(ca, n, f, B, instances=1024, sub=128, ring=3, inflight=2, device=0, se
                         verdict_bad[0] += int((res["valid"] != R["want_valid"][:c]).sum())
         return _t.perf_counter() - t0
 
+    marks = []
+
     def timed(kinds):
         """warm every slot's buffers, then time one epoch of `kinds` (all ranks together) and check it:
         verdicts, every value, statuses, proposer roots"""
@@ -271,7 +273,9 @@ def epoch(ca, n, f, B, instances=1024, sub=128, ring=3, inflight=2, device=0, se
         verdict_bad[0] = 0
         if barrier:
             barrier()
+        marks.append([kinds, _t.monotonic_ns()])
         el = run(kinds)
+        marks[-1].append(_t.monotonic_ns())  # CLOCK_MONOTONIC, the clock of rocprofv3's timestamps
         if barrier:
             barrier()
         vals_ok = all(np.array_equal(vout[b * sub: b * sub + counts[b], :B], vals[b % ring][:counts[b]])
@@ -293,6 +297,7 @@ def epoch(ca, n, f, B, instances=1024, sub=128, ring=3, inflight=2, device=0, se
            "sub_batch": sub, "inflight": inflight, "echo_messages": echo,
            "pcie_GBps": {"h2d": round(h2d / el / 1e9, 2), "d2h": round(d2h / el / 1e9, 2)},
            "checks": checks, "ok": ok and ok_f,
+           "timed_windows_ns": marks,
            "fused": {"GBps": round(shard_bytes / el_f / 1e9, 3), "seconds": round(el_f, 4), "checks": checks_f,
                      "ok": ok_f, "pcie_GBps": {"h2d": round(h2d_f / el_f / 1e9, 2), "d2h": round(d2h / el_f / 1e9, 2)},
                      "path": "rbc_shard_commit || rbc_receive_batch (ECHO rows cross PCIe once, verified on the "
