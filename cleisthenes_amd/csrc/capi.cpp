@@ -1390,6 +1390,11 @@ int retire(rbc_ctx *c, Slot &s) {
     return st;
 }
 
+#ifndef RBC_BLOCKING_SYNC_EVENTS
+#define RBC_BLOCKING_SYNC_EVENTS 1
+#endif
+constexpr unsigned kSlotEventSync = RBC_BLOCKING_SYNC_EVENTS ? hipEventBlockingSync : 0u;
+
 Slot *acquire_slot(rbc_ctx *c) {
     for (auto &sl : c->slots)
         if (!sl->busy) return sl.get();
@@ -1399,8 +1404,8 @@ Slot *acquire_slot(rbc_ctx *c) {
             // blocking-sync events: a host-API waiter (the batcher's completer, a
             // goroutine's cgo call) sleeps instead of spinning a core the
             // submitting threads need for their staging copies
-            hipEventCreateWithFlags(&sl->done, hipEventDisableTiming | hipEventBlockingSync) != hipSuccess ||
-            hipEventCreateWithFlags(&sl->kdone, hipEventDisableTiming | hipEventBlockingSync) != hipSuccess ||
+            hipEventCreateWithFlags(&sl->done, hipEventDisableTiming | kSlotEventSync) != hipSuccess ||
+            hipEventCreateWithFlags(&sl->kdone, hipEventDisableTiming | kSlotEventSync) != hipSuccess ||
             !sl->ws.init()) {
             sl->release();
             return nullptr;
@@ -1426,7 +1431,10 @@ int submit(rbc_ctx *c, Slot &s, uint64_t *ticket, std::function<int()> finish,
     for (auto &o : c->slots)
         if (o.get() != &s && o->busy) flush_d2h(*o);
     s.d2h_rc = 0;
-    if (d2h && ticket) {
+#ifndef RBC_DEFER_D2H
+#define RBC_DEFER_D2H 1
+#endif
+    if (RBC_DEFER_D2H && d2h && ticket) {
         if (hipEventRecord(s.kdone, s.stream) != hipSuccess) {
             s.finish = nullptr;
             return RBC_ERR_DEVICE;
