@@ -1491,6 +1491,50 @@ static const uint8_t *host_zero_copy(const void *p, size_t bytes) {
     return a.devicePointer == p ? static_cast<const uint8_t *>(p) : nullptr;
 }
 
+// Every value in pinned memory?  *zc: also each readable zero-copy at its own
+// address (two attribute queries per value, as host_pinned).
+static bool values_pinned(const uint8_t *const *values, const size_t *lens, int count, bool *zc) {
+    *zc = RBC_ZERO_COPY_READS != 0;
+    for (int i = 0; i < count; ++i) {
+        for (int e = 0; e < 2; ++e) {
+            const void *q = values[i] + (e ? lens[i] - 1 : 0);
+            hipPointerAttribute_t a;
+            if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+                (void)hipGetLastError();
+                return false;
+            }
+            if (a.type != hipMemoryTypeHost) return false;
+            if (!e && a.devicePointer != q) *zc = false;
+        }
+    }
+    return true;
+}
+
+// The pinned values of a shard_commit submission into the device value rows:
+// one DMA per value, or -- many short values, all readable zero-copy -- one
+// gather launch over their addresses (host time per DMA call dominated C4's
+// 16,384-value epoch).  `lens` ([2*count] u32, pinned staging) is uploaded
+// here when the gather needs it; `ptr_stage` has room for count addresses.
+static int upload_pinned_values(Slot &s, hipStream_t st, int count, const uint8_t *const *values,
+                                const size_t *value_lens, size_t vpitch, bool zc, uint32_t *lens,
+                                uint64_t *ptr_stage) {
+    size_t total = 0;
+    for (int i = 0; i < count; ++i) total += value_lens[i];
+    if (zc && count >= 64 && total / count < ((size_t)256 << 10)) {
+        for (int i = 0; i < count; ++i) ptr_stage[i] = (uint64_t)(uintptr_t)values[i];
+        RBC_HIP(s.d_offs.ensure((size_t)count * 8));
+        RBC_HIP(hipMemcpyAsync(s.d_offs.p, ptr_stage, (size_t)count * 8, hipMemcpyHostToDevice, st));
+        RBC_HIP(hipMemcpyAsync(s.d_lens.p, lens, (size_t)count * 4, hipMemcpyHostToDevice, st));
+        RBC_HIP(rbc_launch_gather_values(s.d_offs.as<uint64_t>(), s.d_lens.as<uint32_t>(), (uint32_t)count,
+                                         s.d_values.as<uint8_t>(), vpitch, st));
+        return RBC_OK;
+    }
+    for (int i = 0; i < count; ++i)
+        RBC_HIP(hipMemcpyAsync(s.d_values.as<uint8_t>() + (size_t)i * vpitch, values[i], value_lens[i],
+                               hipMemcpyHostToDevice, st));
+    return RBC_OK;
+}
+
 int rbc_shard_commit(rbc_ctx *c, int count, const uint8_t *const *values, const size_t *value_lens,
                      uint8_t *shards_out, size_t shard_pitch, uint32_t *shard_lens_out, uint8_t *roots_out,
                      uint8_t *branches_out, uint64_t *ticket) {
@@ -1504,7 +1548,13 @@ int rbc_shard_commit(rbc_ctx *c, int count, const uint8_t *const *values, const 
         Smax = std::max(Smax, (value_lens[i] + c->k - 1) / c->k);
     }
     if (shard_pitch < Smax) return RBC_ERR_INVALID_ARG;
-    const size_t dpitch = round_up(Smax, 128);  // whole HBM lines per row
+    // pinned output whose pitch the device rows can take: the device rows use
+    // it and the shards come back in ONE plain copy (pitch-to-pitch 2-D copies
+    // of many short rows ran at 0.1 GB/s at C4, and odd pitches off the copy
+    // engine's fast path); else whole HBM lines per row
+    const bool sh_direct = host_pinned(shards_out, ((size_t)count * c->n - 1) * shard_pitch + Smax);
+    const bool sh_flat = sh_direct && shard_pitch % kAlign == 0 && shard_pitch <= 0x7fffffffULL / c->n;
+    const size_t dpitch = sh_flat ? shard_pitch : round_up(Smax, 128);
     const size_t vpitch = round_up((size_t)c->k * Smax + 32, kAlign);
     if (vpitch > 0x7fffffffULL || (size_t)c->n * dpitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
     const int d = c->depth, n = c->n;
@@ -1522,14 +1572,13 @@ int rbc_shard_commit(rbc_ctx *c, int count, const uint8_t *const *values, const 
     RBC_HIP(s.d_branches.ensure(br_bytes));
     RBC_HIP(s.d_lens.ensure((size_t)count * 8));
     // pinned staging only for what is not already pinned caller memory
-    bool in_direct = true;
-    for (int i = 0; i < count && in_direct; ++i) in_direct = host_pinned(values[i], value_lens[i]);
+    bool zc = false;
+    const bool in_direct = values_pinned(values, value_lens, count, &zc);
     const size_t in_stage = in_direct ? 0 : (size_t)count * vpitch;
-    const bool sh_direct = host_pinned(shards_out, ((size_t)count * n - 1) * shard_pitch + Smax);
     const bool rt_direct = host_pinned(roots_out, (size_t)count * 32);
     const size_t br_out = (size_t)count * n * d * 32;
     const bool br_direct = branches_out && d > 0 && host_pinned(branches_out, br_out);
-    RBC_HIP(s.h_in.ensure(in_stage + (size_t)count * 8));
+    RBC_HIP(s.h_in.ensure(in_stage + (size_t)count * 8 + (in_direct ? (size_t)count * 8 : 0)));
     RBC_HIP(s.h_out.ensure((sh_direct ? 0 : sh_bytes) + (size_t)count * 32 + br_bytes));
     uint8_t *stage = s.h_in.as<uint8_t>();
     uint32_t *lens = reinterpret_cast<uint32_t *>(stage + in_stage);
@@ -1538,9 +1587,10 @@ int rbc_shard_commit(rbc_ctx *c, int count, const uint8_t *const *values, const 
         for (int i = 0; i < count; ++i) {
             lens[i] = (uint32_t)value_lens[i];
             lens[count + i] = (uint32_t)((value_lens[i] + c->k - 1) / c->k);
-            RBC_HIP(hipMemcpyAsync(s.d_values.as<uint8_t>() + (size_t)i * vpitch, values[i], value_lens[i],
-                                   hipMemcpyHostToDevice, st));
         }
+        const int rc = upload_pinned_values(s, st, count, values, value_lens, vpitch, zc, lens,
+                                            reinterpret_cast<uint64_t *>(stage + in_stage + (size_t)count * 8));
+        if (rc) return rc;
     } else {
         parallel_for(count, vpitch, [&](int i) {
             memcpy(stage + (size_t)i * vpitch, values[i], value_lens[i]);
@@ -1563,7 +1613,9 @@ int rbc_shard_commit(rbc_ctx *c, int count, const uint8_t *const *values, const 
             *o_br = o_rt + (size_t)count * 32;
     void *d_sh = s.d_shards.p, *d_rt = s.d_roots.p, *d_br = s.d_branches.p;
     auto d2h = [=]() -> int {
-        if (sh_direct)  // Smax bytes per row: the device rows are zero past S_i
+        if (sh_direct && dpitch == shard_pitch)  // every row whole: bytes [S_i, pitch) come back zero
+            RBC_HIP(hipMemcpyAsync(shards_out, d_sh, sh_bytes, hipMemcpyDeviceToHost, st));
+        else if (sh_direct)  // Smax bytes per row: the device rows are zero past S_i
             RBC_HIP(hipMemcpy2DAsync(shards_out, shard_pitch, d_sh, dpitch, Smax, (size_t)count * n,
                                      hipMemcpyDeviceToHost, st));
         else
@@ -1624,18 +1676,19 @@ int rbc_shard_commit_val(rbc_ctx *c, int count, const uint8_t *const *values, co
     RBC_HIP(s.d_roots.ensure((size_t)count * 32));
     RBC_HIP(s.d_branches.ensure(br_bytes));
     RBC_HIP(s.d_lens.ensure((size_t)count * 8 + (size_t)count * n * 4));
-    RBC_HIP(s.h_in.ensure((size_t)count * vpitch + (size_t)count * 8));
+    RBC_HIP(s.h_in.ensure((size_t)count * vpitch + (size_t)count * 16));
     uint8_t *stage = s.h_in.as<uint8_t>();
     uint32_t *lens = reinterpret_cast<uint32_t *>(stage + (size_t)count * vpitch);
-    bool in_direct = true;
-    for (int i = 0; i < count && in_direct; ++i) in_direct = host_pinned(values[i], value_lens[i]);
-    if (in_direct) {  // pinned values: one DMA each, the encode kernel masks the Split pad
+    bool zc = false;
+    const bool in_direct = values_pinned(values, value_lens, count, &zc);
+    if (in_direct) {  // pinned values: one DMA each (or one gather), the encode kernel masks the Split pad
         for (int i = 0; i < count; ++i) {
             lens[i] = (uint32_t)value_lens[i];
             lens[count + i] = (uint32_t)((value_lens[i] + c->k - 1) / c->k);
-            RBC_HIP(hipMemcpyAsync(s.d_values.as<uint8_t>() + (size_t)i * vpitch, values[i], value_lens[i],
-                                   hipMemcpyHostToDevice, st));
         }
+        const int rc = upload_pinned_values(s, st, count, values, value_lens, vpitch, zc, lens,
+                                            reinterpret_cast<uint64_t *>(lens + 2 * (size_t)count));
+        if (rc) return rc;
     } else {
         parallel_for(count, vpitch, [&](int i) {
             memcpy(stage + (size_t)i * vpitch, values[i], value_lens[i]);

@@ -250,6 +250,9 @@ hipError_t rbc_launch_gather_present(const uint8_t *host, uint64_t hpitch, uint3
 // (zero-copy reads of bytes [offs[i], offs[i] + lens[i]) only; the rest untouched)
 hipError_t rbc_launch_gather_msgs(const uint8_t *host, const uint64_t *offs, const uint32_t *lens, uint32_t count,
                                   uint8_t *dev, hipStream_t st);
+// pinned host values (device array of their addresses) -> device value rows (zero-copy reads)
+hipError_t rbc_launch_gather_values(const uint64_t *ptrs, const uint32_t *lens, uint32_t count, uint8_t *dev,
+                                    uint64_t vpitch, hipStream_t st);
 hipError_t rbc_launch_count_mismatch(const uint8_t *a, uint64_t a_pitch, const uint8_t *b, uint64_t b_pitch,
                                      uint64_t rows, uint64_t len, uint32_t *counter, hipStream_t st);
 hipError_t rbc_launch_count_mismatch_rows(const uint8_t *shards, uint64_t inst_pitch, uint32_t row_pitch, int k,

@@ -1718,23 +1718,14 @@ __global__ __launch_bounds__(256) void poison_rows_kernel(uint8_t *shards, uint6
 // caller batch into the device rows, reading the host memory directly over
 // PCIe (zero-copy; measured at the DMA engine's rate, tools/probes/
 // zerocopy_probe.hip).  Bytes [S, dpitch) of a present row and every absent
-// row are written as zero.  Blocks stride over the rows (r = instance * N +
-// row): a few blocks per CU keep enough PCIe reads in flight and leave the
-// CUs to the other slot's decode kernels; the host read is bounded to the
-// row's S bytes.
-__global__ __launch_bounds__(256) void gather_present_kernel(const uint8_t *host, uint64_t hpitch, uint32_t S,
-                                                             const uint8_t *present, uint8_t *dev, uint32_t dpitch,
-                                                             uint32_t rows) {
-    for (uint32_t r = blockIdx.x; r < rows; r += gridDim.x) {
-    uint4 *dst = reinterpret_cast<uint4 *>(dev + (size_t)r * dpitch);
-    const uint32_t chunks = dpitch / 16;
-    if (!present[r]) {
-        for (uint32_t c = threadIdx.x; c < chunks; c += blockDim.x) dst[c] = make_uint4(0, 0, 0, 0);
-        continue;
-    }
-    const uint8_t *row = host + (size_t)r * hpitch;
+// row are written as zero.  One WAVE per row (r = instance * N + row), 1 KiB
+// per pass: C4's 384-B rows used to leave 232 of a 256-thread block idle
+// (the C4 host-fed receive ran at 10 GB/s); the 64 four-wave blocks of the
+// grid keep 256 rows' reads in flight and leave the CUs to the other slots'
+// kernels.  The host read is bounded to the row's S bytes.
+RBC_DEV void row_gather16(const uint8_t *row, uint32_t S, uint4 *dst, uint32_t chunks, uint32_t lane) {
     const rsrc_t src = make_rsrc(row, S);
-    for (uint32_t c = threadIdx.x; c < chunks; c += blockDim.x) {
+    for (uint32_t c = lane; c < chunks; c += 64) {
         const int nv = (int)S - (int)(16u * c);
         uint4 v = make_uint4(0, 0, 0, 0);
         if (nv >= 16) {
@@ -1748,41 +1739,69 @@ __global__ __launch_bounds__(256) void gather_present_kernel(const uint8_t *host
         }
         dst[c] = v;
     }
+}
+
+__global__ __launch_bounds__(256) void gather_present_kernel(const uint8_t *host, uint64_t hpitch, uint32_t S,
+                                                             const uint8_t *present, uint8_t *dev, uint32_t dpitch,
+                                                             uint32_t rows) {
+    const uint32_t lane = threadIdx.x & 63u, waves = gridDim.x * (blockDim.x >> 6);
+    const uint32_t chunks = dpitch / 16;
+    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < rows; r += waves) {
+        uint4 *dst = reinterpret_cast<uint4 *>(dev + (size_t)r * dpitch);
+        if (!present[r]) {
+            for (uint32_t c = lane; c < chunks; c += 64) dst[c] = make_uint4(0, 0, 0, 0);
+            continue;
+        }
+        row_gather16(host + (size_t)r * hpitch, S, dst, chunks, lane);
     }
 }
 
 // Validate lane over a SPARSE pinned arena (rbc_validate_packed): a receiver
 // whose ECHO rows sit at their leaf positions in a [count][N][pitch] buffer
 // names only the received rows (offs), so only those bytes cross PCIe instead
-// of one DMA of the whole arena.  Same zero-copy read as gather_present; the
-// device copy keeps the host offsets (the SHA kernel reads rows by offs), and
-// bytes past a message's length inside its last 64-B block stay unwritten
-// (sha256_row masks them).  offs / lens are device copies.
+// of one DMA of the whole arena.  Same zero-copy read as gather_present, one
+// wave per message; the device copy keeps the host offsets (the SHA kernel
+// reads rows by offs), and bytes past a message's length inside its last 64-B
+// block are written as zero (sha256_row masks them anyway).  offs / lens are
+// device copies.
 __global__ __launch_bounds__(256) void gather_msgs_kernel(const uint8_t *host, const uint64_t *offs,
                                                           const uint32_t *lens, uint32_t count, uint8_t *dev) {
-    for (uint32_t m = blockIdx.x; m < count; m += gridDim.x) {
+    const uint32_t lane = threadIdx.x & 63u, waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t m = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); m < count; m += waves) {
         const uint64_t off = offs[m];
         const uint32_t S = lens[m];
-        const uint8_t *row = host + off;
-        uint4 *dst = reinterpret_cast<uint4 *>(dev + off);
-        const rsrc_t src = make_rsrc(row, S);
-        const uint32_t full = S / 16;
-        for (uint32_t c = threadIdx.x; c < full; c += blockDim.x) dst[c] = bload16(src, 16u * c);
-        if (threadIdx.x == 0 && (S & 15u)) {  // the last partial chunk, byte by byte (never past S)
-            uint32_t w[4] = {0u, 0u, 0u, 0u};
-            for (uint32_t b = 0; b < (S & 15u); ++b) w[b >> 2] |= (uint32_t)row[16u * full + b] << (8 * (b & 3));
-            dst[full] = make_uint4(w[0], w[1], w[2], w[3]);
-        }
+        row_gather16(host + off, S, reinterpret_cast<uint4 *>(dev + off), (S + 15) / 16, lane);
     }
+}
+
+// Host batch API, proposer side: many short pinned values (C4: 16,384 x 64 KiB
+// per epoch) gathered into the device value rows by one launch over a device
+// array of their host addresses, instead of one DMA call per value (~4 us of
+// host time each).  One wave per value; bytes past lens[i] are left as they
+// are (the encode masks the Split pad).
+__global__ __launch_bounds__(256) void gather_values_kernel(const uint64_t *ptrs, const uint32_t *lens,
+                                                            uint32_t count, uint8_t *dev, uint64_t vpitch) {
+    const uint32_t lane = threadIdx.x & 63u, waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < count; i += waves)
+        row_gather16(reinterpret_cast<const uint8_t *>(ptrs[i]), lens[i],
+                     reinterpret_cast<uint4 *>(dev + (size_t)i * vpitch), (lens[i] + 15) / 16, lane);
 }
 
 // ============================================================================
 // launchers
 // ============================================================================
+hipError_t rbc_launch_gather_values(const uint64_t *ptrs, const uint32_t *lens, uint32_t count, uint8_t *dev,
+                                    uint64_t vpitch, hipStream_t st) {
+    if (count == 0) return hipSuccess;
+    if (vpitch % 16) return hipErrorInvalidValue;
+    const uint32_t blocks = std::min((count + 3) / 4, 64u);
+    hipLaunchKernelGGL(gather_values_kernel, dim3(blocks), dim3(256), 0, st, ptrs, lens, count, dev, vpitch);
+    return hipGetLastError();
+}
 hipError_t rbc_launch_gather_msgs(const uint8_t *host, const uint64_t *offs, const uint32_t *lens, uint32_t count,
                                   uint8_t *dev, hipStream_t st) {
     if (count == 0) return hipSuccess;
-    const uint32_t blocks = std::min(count, 64u);  // as gather_present: enough PCIe reads in flight
+    const uint32_t blocks = std::min((count + 3) / 4, 64u);  // as gather_present: 256 messages' reads in flight
     hipLaunchKernelGGL(gather_msgs_kernel, dim3(blocks), dim3(256), 0, st, host, offs, lens, count, dev);
     return hipGetLastError();
 }
@@ -1817,7 +1836,7 @@ hipError_t rbc_launch_gather_present(const uint8_t *host, uint64_t hpitch, uint3
                                      uint8_t *dev, uint32_t dpitch, uint32_t rows, hipStream_t st) {
     if (rows == 0) return hipSuccess;
     if (dpitch % 16 || S > dpitch) return hipErrorInvalidValue;
-    const uint32_t blocks = std::min(rows, 64u);  // a few blocks per CU keep enough PCIe reads in flight
+    const uint32_t blocks = std::min((rows + 3) / 4, 64u);  // 256 rows' reads in flight, one wave each
     hipLaunchKernelGGL(gather_present_kernel, dim3(blocks), dim3(256), 0, st, host, hpitch, S, present, dev, dpitch,
                        rows);
     return hipGetLastError();

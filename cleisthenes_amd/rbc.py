@@ -355,9 +355,11 @@ class Context:
         Smax = max((len(a) + self.k - 1) // self.k for a in arrs)
         pitch = Smax
         bshape = (count, self.n, max(self.depth, 1), 32)
-        if out is not None:
+        if out is not None:  # out["shards"] may be [count][N][pitch >= Smax] (a 64-B pitch: one D2H copy)
             shards, roots, br = out["shards"], out["roots"], out["branches"]
-            assert shards.shape == (count, self.n, pitch) and roots.shape == (count, 32) and br.shape == bshape
+            pitch = shards.shape[2]
+            assert shards.shape[:2] == (count, self.n) and pitch >= Smax and shards.flags.c_contiguous
+            assert roots.shape == (count, 32) and br.shape == bshape
         else:
             shards = np.zeros((count, self.n, pitch), dtype=np.uint8)
             roots = np.zeros((count, 32), dtype=np.uint8)
@@ -369,7 +371,8 @@ class Context:
         check(lib.rbc_shard_commit(self._p, count, vptrs, vlens, _ptr(shards), pitch,
                                    slens.ctypes.data_as(_lib.u32p), _ptr(roots), _ptr(br), byref(t)),
               "rbc_shard_commit")
-        out = {"shards": shards, "shard_lens": slens, "roots": roots, "branches": br[:, :, : self.depth]}
+        out = {"shards": shards[:, :, :Smax] if pitch != Smax else shards, "shard_lens": slens, "roots": roots,
+               "branches": br[:, :, : self.depth]}
         return HostTicket(self, t.value, out, keep=(arrs, vlens, vptrs, br))
 
     def shard_commit_val(self, values: Sequence[bytes], ring: Optional[np.ndarray] = None) -> dict:

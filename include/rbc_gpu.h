@@ -276,7 +276,9 @@ int rbc_dev_inject_faults(rbc_ctx *ctx, void *stream, int count, uint8_t *shards
  * returns a ticket; rbc_wait / rbc_poll complete it (no C->Go callbacks).
  * Caller buffers must stay valid until the ticket completes. */
 /* shard() + Merkle commit for `count` proposals: values[i] (value_lens[i] bytes)
- * -> shards_out [count][n][shard_pitch] (S_i bytes per row used),
+ * -> shards_out [count][n][shard_pitch] (S_i bytes per row used; when
+ * shards_out is pinned and shard_pitch % 64 == 0 the rows come back whole in
+ * one copy, bytes [S_i, shard_pitch) as zero),
  * shard_lens_out [count] (S_i), roots_out [count][32],
  * branches_out [count][n][d][32] (nullable). */
 int rbc_shard_commit(rbc_ctx *ctx, int count, const uint8_t *const *values, const size_t *value_lens,

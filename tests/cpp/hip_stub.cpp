@@ -312,6 +312,14 @@ hipError_t rbc_launch_gather_present(const uint8_t *host, uint64_t hpitch, uint3
     }
     return hipSuccess;
 }
+hipError_t rbc_launch_gather_values(const uint64_t *ptrs, const uint32_t *lens, uint32_t count, uint8_t *dev,
+                                    uint64_t vpitch, hipStream_t) {
+    for (uint32_t i = 0; i < count; ++i) {  // whole 16-B chunks up to round_up(len, 16)
+        touch(dev + (size_t)i * vpitch, (lens[i] + 15) / 16 * 16);
+        memcpy(dev + (size_t)i * vpitch, reinterpret_cast<const void *>(ptrs[i]), lens[i]);
+    }
+    return hipSuccess;
+}
 hipError_t rbc_launch_gather_msgs(const uint8_t *host, const uint64_t *offs, const uint32_t *lens, uint32_t count,
                                   uint8_t *dev, hipStream_t) {
     for (uint32_t m = 0; m < count; ++m) {  // the kernel stores whole 16-B chunks up to round_up(len, 16)

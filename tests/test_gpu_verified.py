@@ -225,3 +225,36 @@ def test_receive_batch_fused_equals_validate_then_interpolate(gpu, n, f, B, pinn
     assert np.array_equal(got["values"], full["values"]) and np.array_equal(got["digests"], full["digests"])
     for i in range(count):
         assert got["values"][i, :B].tobytes() == e["vals"][i].tobytes(), i
+
+
+@pytest.mark.parametrize("n,f", [(256, 85), (37, 12)])
+def test_shard_commit_many_short_pinned_values_gathered(gpu, n, f):
+    """rbc_shard_commit over >= 64 short pinned values reads them with one
+    gather launch over their host addresses (not one DMA per value), and a
+    pinned output at a 64-B pitch comes back in one flat copy (bytes past
+    S_i zero): shards, roots and branches equal the oracle's for ragged
+    lengths (1 byte up to 64 KiB) -- and equal the pageable-memory path."""
+    ctx = gpu.Context(n, f)
+    rng = np.random.default_rng(n)
+    lens = [1, 2, 63, 64, 65, 1000] + [int(x) for x in rng.integers(1, 1 << 16, 94)]
+    count = len(lens)
+    block = gpu.pinned_empty((count, 1 << 16))
+    block[:] = rng.integers(0, 256, block.shape, dtype=np.uint8)
+    vals = [block[i, :lens[i]] for i in range(count)]
+    k = ctx.k
+    Smax = max((L + k - 1) // k for L in lens)
+    pitch = (Smax + 63) // 64 * 64
+    d = max(ctx.depth, 1)
+    out = {"shards": gpu.pinned_empty((count, n, pitch)), "roots": gpu.pinned_empty((count, 32)),
+           "branches": gpu.pinned_empty((count, n, d, 32))}
+    out["shards"][:] = 0xEE
+    got = ctx.shard_commit_submit(vals, out=out).wait()
+    ref = ctx.shard_commit_submit([np.array(v) for v in vals]).wait()  # pageable values and outputs
+    for i in range(count):
+        S = (lens[i] + k - 1) // k
+        shards, root, br, _ = rbc_ref.encode_commit(n, f, np.array(vals[i]))
+        assert got["shard_lens"][i] == S
+        assert np.array_equal(out["shards"][i, :, :S], shards), i
+        assert not out["shards"][i, :, S:].any(), i  # the flat copy returns the zero pad
+        assert bytes(got["roots"][i]) == root and np.array_equal(got["branches"][i], br), i
+        assert np.array_equal(ref["shards"][i, :, :S], shards) and bytes(ref["roots"][i]) == root, i

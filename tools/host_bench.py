@@ -156,7 +156,8 @@ def epoch(ca, n, f, B, instances=1024, sub=128, ring=3, inflight=2, device=0, se
         v = ca.pinned_empty((sub, B))
         v[:] = rng.integers(0, 256, (sub, B), dtype=np.uint8)
         vals.append(v)
-    prop = [{"shards": ca.pinned_empty((sub, n, S)), "roots": ca.pinned_empty((sub, 32)),
+    # the proposer's output rings at a 64-B row pitch: the shards come back in one D2H copy
+    prop = [{"shards": ca.pinned_empty((sub, n, pitch)), "roots": ca.pinned_empty((sub, 32)),
              "branches": ca.pinned_empty((sub, n, max(d, 1), 32))} for _ in range(inflight + 1)]
     rx = []
     for r in range(ring):
