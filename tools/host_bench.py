@@ -123,7 +123,7 @@ def _rx_messages(present, n, pitch):
 
 
 def epoch(ca, n, f, B, instances=1024, sub=128, ring=3, inflight=2, device=0, seed=20261018, tamper=0.10,
-          phases=True, barrier=None):
+          phases=True, barrier=None, contexts=1):
     """One node's whole RBC epoch through the C ABI from pinned host memory
     (end-to-end with H2D / D2H).  Per
     sub-batch of `sub` instances, concurrently (`inflight` of each kind in
@@ -141,9 +141,12 @@ def epoch(ca, n, f, B, instances=1024, sub=128, ring=3, inflight=2, device=0, se
     Every verdict, every decoded value and every proposer root is checked
     after timing.  `barrier` (callable) brackets the timed region when ranks
     run the leg together.  GB/s = instances x N x S committed shard bytes
-    per second (the bench's unit); PCIe bytes are counted per direction."""
+    per second (the bench's unit); PCIe bytes are counted per direction.
+    contexts=2: the proposer and the receiver side submit through contexts of
+    their own (own host slots, streams and lock), as a node may."""
     import time as _t
     ctx = ca.Context(n, f, device=device)
+    pctx = ca.Context(n, f, device=device) if contexts == 2 else ctx  # the proposer side's
     k, d = ctx.k, ctx.depth
     S = (B + k - 1) // k
     pitch = (S + 63) // 64 * 64
@@ -200,7 +203,7 @@ def epoch(ca, n, f, B, instances=1024, sub=128, ring=3, inflight=2, device=0, se
     def commit(b, slot):
         c = counts[b]
         o = {kk: v[:c] for kk, v in prop[slot].items()}
-        return ctx.shard_commit_submit(list(vals[b % ring][:c]), out=o)
+        return pctx.shard_commit_submit(list(vals[b % ring][:c]), out=o)
 
     def validate(b, slot):
         R = rx[b % ring]
@@ -309,6 +312,9 @@ def epoch(ca, n, f, B, instances=1024, sub=128, ring=3, inflight=2, device=0, se
                             ("receive_fused", "r")):
             alone[name] = round(shard_bytes / run(kinds) / 1e9, 3)
         out["alone_GBps"] = alone
+    out["contexts"] = contexts
+    if pctx is not ctx:
+        pctx.close()
     ctx.close()
     return out
 
@@ -322,6 +328,8 @@ def main():
     ap.add_argument("--epoch", type=int, default=0,
                     help="instead: one host-fed epoch of this many instances (the bench's pcie_inclusive leg)")
     ap.add_argument("--sub", type=int, default=0, help="epoch sub-batch (default: ~400 MB of shards)")
+    ap.add_argument("--contexts", type=int, default=1, choices=(1, 2),
+                    help="epoch: 2 = the proposer and the receiver side on contexts of their own")
     ap.add_argument("--pinned", action="store_true",
                     help="values, shard/root/branch outputs and interpolate buffers in rbc_host_alloc memory "
                          "(the C ABI then copies to and from them directly, no staging memcpy)")
@@ -333,7 +341,7 @@ def main():
         k = n - 2 * f
         S = (B + k - 1) // k
         sub = args.sub or max(1, min(args.epoch, int(400e6 // (n * S))))
-        r = epoch(ca, n, f, B, instances=args.epoch, sub=sub, inflight=args.inflight)
+        r = epoch(ca, n, f, B, instances=args.epoch, sub=sub, inflight=args.inflight, contexts=args.contexts)
         print(json.dumps({"config": args.config, "library": ca.rbc.library_path(), **r}))
         return
     r = measure(ca, n, f, B, args.batch, args.batches, args.inflight, args.pinned)
