@@ -2,7 +2,7 @@
 # trace + stats of exactly `python bench.py`, the other configs' lines, and a
 # 2-rank rehearsal with the host-fed leg on both ranks.
 set -o pipefail
-O=gpurun_out/r06j; mkdir -p $O
+O=gpurun_out/${RUN:-r06j}; mkdir -p $O
 R=$(pwd)
 for rep in 1 2; do
   timeout -k 10 600 python bench.py > $O/bench_default_$rep.json 2> $O/bench_default_$rep.err || { echo BENCHFAIL; tail -30 $O/bench_default_$rep.err; exit 1; }
