@@ -134,6 +134,7 @@ struct Slot {
     DevBuf h_in{nullptr, 0, true}, h_out{nullptr, 0, true};
     Ws ws;
     hipStream_t stream = nullptr;
+    hipStream_t dstream = nullptr;  // RBC_D2H_STREAM: the submission's D2H copies, gated on kdone
     hipEvent_t done = nullptr;
     // recorded after the submission's kernels, before its deferred D2H: a
     // waiter enqueues the D2H only once the kernels are done, so the copy
@@ -148,7 +149,7 @@ struct Slot {
     // the copy engine serves the streams' copies in enqueue order, so a D2H
     // queued at submit time (it waits on this submission's kernels) would hold
     // the next submission's H2D behind it and serialise the slots.
-    std::function<int()> d2h;
+    std::function<int(hipStream_t)> d2h;  // enqueues the D2H copies on the given stream
     int d2h_rc = 0;
     void release() {
         for (DevBuf *b : {&d_values, &d_shards, &d_leaves, &d_roots, &d_branches, &d_valid, &d_status, &d_digests,
@@ -156,9 +157,11 @@ struct Slot {
             b->release();
         ws.release();
         if (stream) (void)hipStreamDestroy(stream);
+        if (dstream) (void)hipStreamDestroy(dstream);
         if (done) (void)hipEventDestroy(done);
         if (kdone) (void)hipEventDestroy(kdone);
         stream = nullptr;
+        dstream = nullptr;
         done = nullptr;
         kdone = nullptr;
     }
@@ -166,6 +169,9 @@ struct Slot {
 
 // host-API submissions in flight per context: the batcher keeps 4 launches
 // in flight (tools/batcher_bench.cpp), and the box has 4 hardware queues
+#ifndef RBC_D2H_STREAM
+#define RBC_D2H_STREAM 0
+#endif
 #ifndef RBC_HOST_SLOTS
 #define RBC_HOST_SLOTS 4
 #endif
@@ -1089,7 +1095,7 @@ void rbc_ctx_destroy(rbc_ctx *c) {
     if (c->comm) (void)ncclCommDestroy(c->comm);
     for (auto &sl : c->slots) {
         if (sl->busy && sl->d2h) {
-            (void)sl->d2h();
+            (void)sl->d2h(sl->stream);
             sl->d2h = nullptr;
             (void)hipEventRecord(sl->done, sl->stream);
         }
@@ -1370,7 +1376,7 @@ void parallel_for(int count, size_t bytes_per_item, F &&f) {
 // event (see Slot::d2h).
 void flush_d2h(Slot &s) {
     if (!s.d2h) return;
-    s.d2h_rc = s.d2h();
+    s.d2h_rc = s.d2h(s.stream);
     s.d2h = nullptr;
     if (hipEventRecord(s.done, s.stream) != hipSuccess && !s.d2h_rc) s.d2h_rc = RBC_ERR_DEVICE;
 }
@@ -1401,6 +1407,7 @@ Slot *acquire_slot(rbc_ctx *c) {
     if ((int)c->slots.size() < kHostSlots) {
         auto sl = std::make_unique<Slot>();
         if (hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking) != hipSuccess ||
+            (RBC_D2H_STREAM && hipStreamCreateWithFlags(&sl->dstream, hipStreamNonBlocking) != hipSuccess) ||
             // blocking-sync events: a host-API waiter (the batcher's completer, a
             // goroutine's cgo call) sleeps instead of spinning a core the
             // submitting threads need for their staging copies
@@ -1426,7 +1433,7 @@ Slot *acquire_slot(rbc_ctx *c) {
 // device-to-host copies are deferred (Slot::d2h); the other slots' deferred
 // copies are enqueued now, behind this submission's host-to-device copies.
 int submit(rbc_ctx *c, Slot &s, uint64_t *ticket, std::function<int()> finish,
-           std::function<int()> d2h = nullptr) {
+           std::function<int(hipStream_t)> d2h = nullptr) {
     s.finish = std::move(finish);
     for (auto &o : c->slots)
         if (o.get() != &s && o->busy) flush_d2h(*o);
@@ -1434,14 +1441,27 @@ int submit(rbc_ctx *c, Slot &s, uint64_t *ticket, std::function<int()> finish,
 #ifndef RBC_DEFER_D2H
 #define RBC_DEFER_D2H 1
 #endif
-    if (RBC_DEFER_D2H && d2h && ticket) {
+    if (RBC_D2H_STREAM && d2h) {
+        // the D2H copies go on the slot's own copy stream at once, behind an
+        // event wait on its kernels: nothing waits in front of the next
+        // submission's H2D on the compute stream, and no host call has to
+        // enqueue them later
+        const int rc = hipEventRecord(s.kdone, s.stream) != hipSuccess ||
+                               hipStreamWaitEvent(s.dstream, s.kdone, 0) != hipSuccess
+                           ? RBC_ERR_DEVICE
+                           : d2h(s.dstream);
+        if (rc || hipEventRecord(s.done, s.dstream) != hipSuccess) {
+            s.finish = nullptr;
+            return rc ? rc : RBC_ERR_DEVICE;
+        }
+    } else if (RBC_DEFER_D2H && d2h && ticket) {
         if (hipEventRecord(s.kdone, s.stream) != hipSuccess) {
             s.finish = nullptr;
             return RBC_ERR_DEVICE;
         }
         s.d2h = std::move(d2h);
     } else {
-        const int rc = d2h ? d2h() : RBC_OK;
+        const int rc = d2h ? d2h(s.stream) : RBC_OK;
         if (rc || hipEventRecord(s.done, s.stream) != hipSuccess) {
             s.finish = nullptr;
             return rc ? rc : RBC_ERR_DEVICE;
@@ -1612,17 +1632,17 @@ int rbc_shard_commit(rbc_ctx *c, int count, const uint8_t *const *values, const 
     uint8_t *o_sh = s.h_out.as<uint8_t>(), *o_rt = o_sh + (sh_direct ? 0 : sh_bytes),
             *o_br = o_rt + (size_t)count * 32;
     void *d_sh = s.d_shards.p, *d_rt = s.d_roots.p, *d_br = s.d_branches.p;
-    auto d2h = [=]() -> int {
+    auto d2h = [=](hipStream_t cs) -> int {
         if (sh_direct && dpitch == shard_pitch)  // every row whole: bytes [S_i, pitch) come back zero
-            RBC_HIP(hipMemcpyAsync(shards_out, d_sh, sh_bytes, hipMemcpyDeviceToHost, st));
+            RBC_HIP(hipMemcpyAsync(shards_out, d_sh, sh_bytes, hipMemcpyDeviceToHost, cs));
         else if (sh_direct)  // Smax bytes per row: the device rows are zero past S_i
             RBC_HIP(hipMemcpy2DAsync(shards_out, shard_pitch, d_sh, dpitch, Smax, (size_t)count * n,
-                                     hipMemcpyDeviceToHost, st));
+                                     hipMemcpyDeviceToHost, cs));
         else
-            RBC_HIP(hipMemcpyAsync(o_sh, d_sh, sh_bytes, hipMemcpyDeviceToHost, st));
-        RBC_HIP(hipMemcpyAsync(rt_direct ? roots_out : o_rt, d_rt, (size_t)count * 32, hipMemcpyDeviceToHost, st));
+            RBC_HIP(hipMemcpyAsync(o_sh, d_sh, sh_bytes, hipMemcpyDeviceToHost, cs));
+        RBC_HIP(hipMemcpyAsync(rt_direct ? roots_out : o_rt, d_rt, (size_t)count * 32, hipMemcpyDeviceToHost, cs));
         if (branches_out && d > 0)
-            RBC_HIP(hipMemcpyAsync(br_direct ? branches_out : o_br, d_br, br_bytes, hipMemcpyDeviceToHost, st));
+            RBC_HIP(hipMemcpyAsync(br_direct ? branches_out : o_br, d_br, br_bytes, hipMemcpyDeviceToHost, cs));
         return RBC_OK;
     };
     return submit(c, s, ticket, [=]() {
@@ -1725,10 +1745,10 @@ int rbc_shard_commit_val(rbc_ctx *c, int count, const uint8_t *const *values, co
     // one D2H of the finished messages: straight into a pinned ring, else
     // through HIP's staging (pageable); deferred behind the next submission's H2D
     void *d_rt = s.d_roots.p;
-    auto d2h = [=]() -> int {
-        RBC_HIP(hipMemcpyAsync(msgs, d_msgs, msg_bytes, hipMemcpyDeviceToHost, st));
-        RBC_HIP(hipMemcpyAsync(msg_lens, d_mlens, (size_t)count * n * 4, hipMemcpyDeviceToHost, st));
-        if (roots_out) RBC_HIP(hipMemcpyAsync(roots_out, d_rt, (size_t)count * 32, hipMemcpyDeviceToHost, st));
+    auto d2h = [=](hipStream_t cs) -> int {
+        RBC_HIP(hipMemcpyAsync(msgs, d_msgs, msg_bytes, hipMemcpyDeviceToHost, cs));
+        RBC_HIP(hipMemcpyAsync(msg_lens, d_mlens, (size_t)count * n * 4, hipMemcpyDeviceToHost, cs));
+        if (roots_out) RBC_HIP(hipMemcpyAsync(roots_out, d_rt, (size_t)count * 32, hipMemcpyDeviceToHost, cs));
         return RBC_OK;
     };
     return submit(c, s, ticket, []() { return RBC_OK; }, d2h);
@@ -1911,9 +1931,9 @@ int rbc_validate_packed_leaves(rbc_ctx *c, int count, const uint8_t *arena, size
     }
     RBC_HIP(rbc_launch_sha_rows(a, true, st));
     void *d_valid = s.d_valid.p, *d_lv = s.d_leaves.p;
-    auto d2h = [=]() -> int {  // behind the next submission's H2D (Slot::d2h)
-        RBC_HIP(hipMemcpyAsync(ok_out, d_valid, (size_t)count, hipMemcpyDeviceToHost, st));
-        if (leaves_out) RBC_HIP(hipMemcpyAsync(leaves_out, d_lv, (size_t)count * 32, hipMemcpyDeviceToHost, st));
+    auto d2h = [=](hipStream_t cs) -> int {  // behind the next submission's H2D (Slot::d2h)
+        RBC_HIP(hipMemcpyAsync(ok_out, d_valid, (size_t)count, hipMemcpyDeviceToHost, cs));
+        if (leaves_out) RBC_HIP(hipMemcpyAsync(leaves_out, d_lv, (size_t)count * 32, hipMemcpyDeviceToHost, cs));
         return RBC_OK;
     };
     return submit(c, s, ticket, []() { return RBC_OK; }, d2h);
@@ -2071,18 +2091,18 @@ static int host_receive(rbc_ctx *c, int count, const uint8_t *shards, size_t sha
     uint8_t *o_val = s.h_out.as<uint8_t>(), *o_dig = o_val + out_stage;
     int32_t *o_st = reinterpret_cast<int32_t *>(o_dig + (size_t)count * 32);
     void *d_val = s.d_values.p, *d_dig = s.d_digests.p, *d_st = s.d_status.p, *d_vd = s.d_valid.p;
-    auto d2h = [=]() -> int {
-        if (valid_out) RBC_HIP(hipMemcpyAsync(valid_out, d_vd, (size_t)count * n, hipMemcpyDeviceToHost, st));
+    auto d2h = [=](hipStream_t cs) -> int {
+        if (valid_out) RBC_HIP(hipMemcpyAsync(valid_out, d_vd, (size_t)count * n, hipMemcpyDeviceToHost, cs));
         if (out_direct && value_pitch == vpitch)  // one contiguous DMA (a 2-D copy runs as a blit kernel)
             RBC_HIP(hipMemcpyAsync(values_out, d_val, (size_t)(count - 1) * vpitch + (size_t)k * Smax,
-                                   hipMemcpyDeviceToHost, st));
+                                   hipMemcpyDeviceToHost, cs));
         else if (out_direct)
             RBC_HIP(hipMemcpy2DAsync(values_out, value_pitch, d_val, vpitch, (size_t)k * Smax, (size_t)count,
-                                     hipMemcpyDeviceToHost, st));
+                                     hipMemcpyDeviceToHost, cs));
         else
-            RBC_HIP(hipMemcpyAsync(o_val, d_val, (size_t)count * vpitch, hipMemcpyDeviceToHost, st));
-        RBC_HIP(hipMemcpyAsync(o_dig, d_dig, (size_t)count * 32, hipMemcpyDeviceToHost, st));
-        RBC_HIP(hipMemcpyAsync(o_st, d_st, (size_t)count * 4, hipMemcpyDeviceToHost, st));
+            RBC_HIP(hipMemcpyAsync(o_val, d_val, (size_t)count * vpitch, hipMemcpyDeviceToHost, cs));
+        RBC_HIP(hipMemcpyAsync(o_dig, d_dig, (size_t)count * 32, hipMemcpyDeviceToHost, cs));
+        RBC_HIP(hipMemcpyAsync(o_st, d_st, (size_t)count * 4, hipMemcpyDeviceToHost, cs));
         return RBC_OK;
     };
     return submit(c, s, ticket, [=]() {
