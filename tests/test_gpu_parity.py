@@ -1915,16 +1915,22 @@ def test_verify_form_matches_the_profiling_tools_rule(gpu):
         assert form == ("shared_path" if cfg == "c4" else "walk")
 
 
-@pytest.mark.parametrize("B,tail", [(44 * 40 - 3, 48), (44 * 40 - 3, 176), (44 * 300, 240)])
-def test_fused_join_zeroes_the_whole_padded_value_tail(gpu, B, tail):
+@pytest.mark.parametrize("n,f,B,tail", [
+    (128, 42, 44 * 40 - 3, 48), (128, 42, 44 * 40 - 3, 176), (128, 42, 44 * 300, 240),
+    # rows that start off a 4-byte boundary (S mod 4 != 0): S = 41, 5, 3, 763, 257
+    (128, 42, 44 * 41 - 7, 0), (128, 42, 44 * 41 - 7, 32), (128, 42, 44 * 5 - 1, 16), (128, 42, 44 * 3, 16),
+    (128, 42, 44 * 763, 0), (128, 42, 44 * 257 - 43, 240),
+    (256, 85, 86 * 763 - 5, 0), (256, 85, 86 * 7, 64), (64, 21, 22 * 47663 - 9, 0)])
+def test_fused_join_zeroes_the_whole_padded_value_tail(gpu, n, f, B, tail):
     """the FFT re-encode's fused join zeroes a value's tail from
     tile 0, whose lanes past the shard row pitch have already returned.  With
     a short row (S = 40, pitch 64) and a value pitch padded past k*S by more
     than the pitch, the tail beyond the pitch would stay unwritten; the fused
     join is then not used and the separate join zero-fills it.  Every byte of
     every value row (data, then zero tail) is checked, the buffer having been
-    filled with garbage first."""
-    n, f, I = 128, 42, 32
+    filled with garbage first.  Rows of S bytes with S mod 4 != 0 start off a
+    dword boundary in the value, so neighbouring rows share a dword."""
+    I = 32
     pl = Pipeline(gpu, n, f, B, I, seed=B + tail, corrupt_frac=0.2)
     k, S = pl.k, pl.S
     vp = rup(k * S, 16) + rup(tail, 16)
