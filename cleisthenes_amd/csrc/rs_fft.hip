@@ -260,15 +260,6 @@ RBC_DEV void solve(uint32_t (&v)[R]) {
 
 }  // namespace lch
 
-// build-time A/B switches (tools/build_ab.sh): the XCD-aware tile order for
-// decode too, and the decode join's aligned stores
-#ifndef RBC_FFT_DEC_XCD
-#define RBC_FFT_DEC_XCD 0
-#endif
-#ifndef RBC_FFT_JOIN_ALIGN
-#define RBC_FFT_JOIN_ALIGN 0
-#endif
-
 namespace {
 
 RBC_DEV uint32_t keep_bytes4(int nv) { return nv >= 4 ? 0xffffffffu : (nv <= 0 ? 0u : ((1u << (8 * nv)) - 1u)); }
@@ -288,9 +279,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void rs
     // not line aligned: a 256-B tile touches 3 lines, 2 of them shared with
     // its neighbours.  Remapping linear id L -> (L % 8) * (T8 / 8) + L / 8
     // gives each XCD a contiguous run of tiles, so the shared lines hit in
-    // that XCD's L2 instead of being fetched twice from HBM.
+    // that XCD's L2 instead of being fetched twice from HBM.  Decode too: its
+    // fused join stores row j at j*S, so neighbouring tiles (and row j's end
+    // and row j+1's start) share value lines, merged in one L2 this way
+    // (C1 / C2 / C3 +1-3 %, profiles/r06r/).
     uint32_t tile_x = blockIdx.x, tile_y = blockIdx.y;
-    if constexpr (MODE == GF_MODE_ENCODE || RBC_FFT_DEC_XCD) {
+    {
         const uint32_t gx = gridDim.x, total = gx * gridDim.y, t8 = total & ~7u;
         uint32_t lin = blockIdx.y * gx + blockIdx.x;
         if (lin < t8) lin = (lin & 7u) * (t8 >> 3) + (lin >> 3);
@@ -357,66 +351,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void rs
             // descriptor bounds every store to the instance's value row.
             const auto rj = __builtin_amdgcn_make_buffer_rsrc(a.join + (size_t)inst * a.join_pitch, (short)0,
                                                               (int)a.join_pitch, 0x00020000);
-#if RBC_FFT_JOIN_ALIGN
-            if (S >= 4) {
-                // Aligned form: lane L stores the aligned value dword at
-                // j*S + off - s (s = j*S mod 4), i.e. row bytes [off-s, off+4-s):
-                // the top s bytes of its left neighbour's dword and its own low
-                // 4-s bytes (v_alignbyte).  Lane 0's neighbour is the previous
-                // tile's last dword, or at tile 0 the previous row's last 4
-                // bytes, read by a load the other lanes aim past the buffer
-                // (no memory access).  Each dword is stored by exactly one lane:
-                // a dword that straddles rows j and j+1 belongs to row j+1's
-                // tile-0 lane 0, the one that straddles the value's end to the
-                // tail code below.
-                const uint32_t oob = (uint32_t)a.inst_pitch;
-                lch::sfor<0, K>([&](auto J) {
-                    constexpr int j = decltype(J)::value;
-                    const uint32_t so = (uint32_t)j * S, s = so & 3u;  // wave-uniform
-                    if (s == 0) {
-                        if (off + 4 <= S) __builtin_amdgcn_raw_buffer_store_b32(v[j], rj, (int)(so + off), 0, 0);
-                    } else if constexpr (j > 0) {
-                        const uint32_t po = threadIdx.x != 0 ? oob
-                                            : tile_x != 0 ? (uint32_t)j * pitch + off - 4
-                                                          : (uint32_t)(j - 1) * pitch + S - 4;
-                        const uint32_t pl = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)po, 0, 0);
-                        uint32_t prev = __shfl_up(v[j], 1);
-                        if (threadIdx.x == 0) prev = pl;
-                        if (off + 4 - s <= S)
-                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_alignbyte(v[j], prev, 4 - s), rj,
-                                                                  (int)(so + off - s), 0, 0);
-                    }
-                });
-                if (tile_x == 0) {  // the dword holding the value's last t bytes, then zeros to join_pitch
-                    const uint32_t end = (uint32_t)K * S, t = end & 3u, e0 = end - t;
-                    const uint32_t lo = (threadIdx.x == 0 && t) ? (uint32_t)(K - 1) * pitch + S - 4 : oob;
-                    const uint32_t lw = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)lo, 0, 0);
-                    // tile 0's active lanes: those with a column inside the row pitch
-                    const uint32_t stride = a.row_pitch < 256u ? a.row_pitch : 256u;
-                    for (uint32_t o = e0 + 4u * threadIdx.x; o < a.join_pitch; o += stride)
-                        __builtin_amdgcn_raw_buffer_store_b32((o == e0 && t) ? lw >> (8 * (4 - t)) : 0u, rj, (int)o,
-                                                              0, 0);
+            const int nb = (int)S - (int)off;  // this lane's valid bytes per row
+            lch::sfor<0, K>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                const int so = (int)((uint32_t)j * S);
+                if (nb >= 4) {
+                    __builtin_amdgcn_raw_buffer_store_b32(v[j], rj, (int)off, so, 0);
+                } else if (nb > 0) {
+                    for (int b = 0; b < nb; ++b)
+                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v[j] >> (8 * b)), rj, (int)off + b, so, 0);
                 }
-            } else
-#endif
-            {
-                const int nb = (int)S - (int)off;  // this lane's valid bytes per row
-                lch::sfor<0, K>([&](auto J) {
-                    constexpr int j = decltype(J)::value;
-                    const int so = (int)((uint32_t)j * S);
-                    if (nb >= 4) {
-                        __builtin_amdgcn_raw_buffer_store_b32(v[j], rj, (int)off, so, 0);
-                    } else if (nb > 0) {
-                        for (int b = 0; b < nb; ++b)
-                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v[j] >> (8 * b)), rj, (int)off + b, so, 0);
-                    }
-                });
-                if (tile_x == 0) {
-                    const uint32_t end = (uint32_t)K * S;
-                    for (int b = 0; b < 4; ++b) {
-                        const uint32_t o = end + 4u * threadIdx.x + (uint32_t)b;
-                        if (o < a.join_pitch) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, rj, (int)o, 0, 0);
-                    }
+            });
+            if (tile_x == 0) {
+                const uint32_t end = (uint32_t)K * S;
+                for (int b = 0; b < 4; ++b) {
+                    const uint32_t o = end + 4u * threadIdx.x + (uint32_t)b;
+                    if (o < a.join_pitch) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, rj, (int)o, 0, 0);
                 }
             }
         }
