@@ -1573,7 +1573,8 @@ int rbc_shard_commit(rbc_ctx *c, int count, const uint8_t *const *values, const 
     // of many short rows ran at 0.1 GB/s at C4, and odd pitches off the copy
     // engine's fast path); else whole HBM lines per row
     const bool sh_direct = host_pinned(shards_out, ((size_t)count * c->n - 1) * shard_pitch + Smax);
-    const bool sh_flat = sh_direct && shard_pitch % kAlign == 0 && shard_pitch <= 0x7fffffffULL / c->n;
+    const bool sh_flat = sh_direct && shard_pitch % kAlign == 0 && shard_pitch <= 0x7fffffffULL / c->n &&
+                         host_pinned(shards_out, (size_t)count * c->n * shard_pitch);  // the flat copy's extent
     const size_t dpitch = sh_flat ? shard_pitch : round_up(Smax, 128);
     const size_t vpitch = round_up((size_t)c->k * Smax + 32, kAlign);
     if (vpitch > 0x7fffffffULL || (size_t)c->n * dpitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
@@ -2001,7 +2002,8 @@ static int host_receive(rbc_ctx *c, int count, const uint8_t *shards, size_t sha
                                   : nullptr;
     // a pinned batch whose pitch the device rows can take moves in ONE plain
     // copy (a pitched 2-D copy runs as a blit kernel)
-    const bool flat = in_direct && !zc && shard_pitch % kAlign == 0;
+    const bool flat = in_direct && !zc && shard_pitch % kAlign == 0 &&
+                      host_pinned(shards, (size_t)count * n_of(c) * shard_pitch);  // the flat copy's extent
     const size_t dpitch = flat ? shard_pitch : round_up(Smax, 128);
     const size_t vpitch = round_up((size_t)c->k * Smax, 16);
     if ((size_t)c->n * dpitch > 0x7fffffffULL || vpitch > 0x7fffffffULL) return RBC_ERR_INVALID_ARG;
