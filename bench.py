@@ -510,6 +510,11 @@ def run(args, world, rank, local_rank, wd, out):
         pcie["fused"] = {kk: fused[kk] for kk in ("aggregate_GBps", "per_rank_GBps", "slowest_rank", "min_over_max",
                                                   "ok")}
         pcie["fused"]["path"] = per[0]["fused"]["path"]
+        kept = host_fed_aggregate([dict(x["kept"], instances=x["instances"]) for x in per], n, S)
+        pcie["kept"] = {kk: kept[kk] for kk in ("aggregate_GBps", "per_rank_GBps", "slowest_rank", "min_over_max",
+                                                "ok")}
+        pcie["kept"]["path"] = per[0]["kept"]["path"]
+        me["host_fed"]["kept_GBps"] = h["kept"]["GBps"]
         pcie.update({
                 "unit": "GB/s of committed shard bytes (N*S per instance), host memory in and out",
                 "path": "one epoch per rank through the C ABI from pinned host memory, all ranks at once: "
@@ -614,7 +619,8 @@ def batcher_sweep(cpu):
            "tool": "tools/batcher_bench validate-sweep (C2: N=128, f=42, 1 MiB values, S=23,832; 16 client threads)"}
     # the whole drop-in epoch: 1,024 shard + 88,064 validate + 1,024 interpolate
     # requests from 16 client threads at once, timed with the validate lane's leaves reused by
-    # interpolate and again with the full rehash; the tool checks every verdict, value, row and root
+    # interpolate, again with the full rehash, and with the validated rows kept on the device
+    # (rbc_batcher_set_keep); the tool checks every verdict, value, row and root
     r = subprocess.run([exe, "epoch", "1024", "16", str(EPOCH_WINDOW), "200"], capture_output=True, text=True,
                        timeout=300)
     rows = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
@@ -622,6 +628,10 @@ def batcher_sweep(cpu):
     chk = next((x for x in rows if x.get("phase") == "check"), {})
     out["epoch"] = {"unit": "GB/s of committed shard bytes (N*S per instance), host memory in and out",
                     "GBps": ep.get("verified", {}).get("GBps"), "GBps_full_rehash": ep.get("full", {}).get("GBps"),
+                    # ABI 7: the same calls with rbc_batcher_set_keep (the ECHO rows cross PCIe once)
+                    "GBps_kept": ep.get("kept", {}).get("GBps"),
+                    "keep": next(({kk: v for kk, v in x.items() if kk != "phase"} for x in rows
+                                  if x.get("phase") == "keep"), None),
                     "seconds": ep.get("verified", {}).get("seconds"), "requests": ep.get("verified", {}).get("requests"),
                     "launches": ep.get("verified", {}).get("launches"), "window_per_thread": EPOCH_WINDOW,
                     "failures": chk.get("failures"), "verified_equals_full": chk.get("verified_equals_full"),

@@ -117,10 +117,19 @@ _SIGS = {
     "rbc_batcher_poll": (c_int, [c_void_p, c_uint64, POINTER(c_int)]),
     "rbc_batcher_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
     "rbc_batcher_set_validate": (c_int, [c_void_p, c_int, c_size_t]),
+    "rbc_batcher_set_keep": (c_int, [c_void_p, c_size_t]),
+    "rbc_batcher_keep_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64),
+                                       POINTER(c_uint64)]),
+    "rbc_ctx_device": (c_int, [c_void_p, POINTER(c_int)]),
     "rbc_validate_packed": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_void_p, POINTER(c_uint64)]),
     "rbc_validate_packed_leaves": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p,
                                            c_void_p, c_void_p, c_void_p, c_void_p, POINTER(c_uint64)]),
+    "rbc_validate_packed_keep": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                         POINTER(c_uint64)]),
+    "rbc_interpolate_batch_kept": (c_int, [c_void_p, c_int, c_void_p, szp, c_void_p, c_void_p, c_void_p, c_size_t,
+                                           c_void_p, i32p, POINTER(c_uint64)]),
     "rbc_interpolate_batch_verified": (c_int, [c_void_p, c_int, c_void_p, c_size_t, szp, c_void_p, c_void_p,
                                                c_void_p, c_void_p, c_size_t, c_void_p, i32p, POINTER(c_uint64)]),
     "rbc_receive_batch": (c_int, [c_void_p, c_int, c_void_p, c_size_t, szp, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -44,9 +44,10 @@
 
 namespace {
 
-// K_INTERPV: interpolate with the validate lane's leaves (rbc_batcher_interpolate_verified)
-enum Kind { K_SHARD = 0, K_VALIDATE = 1, K_INTERP = 2, K_INTERPV = 3 };
-constexpr int kKinds = 4;
+// K_INTERPV: interpolate with the validate lane's leaves (rbc_batcher_interpolate_verified);
+// K_INTERPK: interpolate whose every present shard the lane kept on the device (rbc_batcher_set_keep)
+enum Kind { K_SHARD = 0, K_VALIDATE = 1, K_INTERP = 2, K_INTERPV = 3, K_INTERPK = 4 };
+constexpr int kKinds = 5;
 
 struct Req {
     uint64_t ticket;
@@ -69,6 +70,11 @@ struct Req {
     size_t *value_len = nullptr;
     uint8_t *digest_out = nullptr;
     const uint8_t *leaves = nullptr;  // K_INTERPV: n x 32, the leaves of the present shards
+    // K_INTERPK: the kept rows' device addresses (n, NULL = absent), their
+    // leaves (n x 32) and the keep regions they pin until the launch completes
+    std::vector<uint64_t> dev_rows;
+    std::vector<uint8_t> kleaves;
+    std::vector<uint64_t> kgens;
 };
 
 // Per-request copies between the callers' buffers and a launch's pinned
@@ -129,6 +135,9 @@ struct VBuf {
     uint8_t *roots = nullptr, *br = nullptr, *idx = nullptr, *ok = nullptr, *shape = nullptr, *lv = nullptr;
     std::vector<int *> out;
     std::vector<uint8_t *> lout;     // callers' leaf_out (rbc_batcher_validate_leaf), nullable
+    std::vector<const uint8_t *> hostp;  // callers' shard pointers (the keep index's identity check)
+    uint8_t *keep_dev = nullptr;     // this launch's region of the keep ring (NULL: not kept)
+    uint64_t keep_gen = 0;
     std::atomic<bool> any_leaf{false};  // some slot asked for its leaf (set before the caller's pend add)
     int cap = 0;                     // messages the meta block holds
     // Copies done, then at seal time + (kSealed - count): == kSealed exactly
@@ -169,11 +178,102 @@ struct VBuf {
         cap = msgs;
         out.assign(msgs, nullptr);
         lout.assign(msgs, nullptr);
+        hostp.assign(msgs, nullptr);
         return true;
     }
 };
 constexpr uint64_t kVTicket = 1ull << 63;  // validate-lane tickets: kVTicket | gen << 20 | slot
 constexpr int kVSlotBits = 20;
+
+// Device-resident ECHO rows (ABI 7, rbc_batcher_set_keep).  Each validate
+// launch moves its arena into the next region of a device ring instead of a
+// launch buffer (rbc_validate_packed_keep); every message that validated is
+// indexed by (root, leaf index) with the caller's shard pointer and length and
+// its leaf.  An interpolate whose every present shard is indexed -- the same
+// pointer and length the caller validated -- reads the rows on the device
+// (rbc_interpolate_batch_kept): the drop-in's ECHO rows then cross PCIe once.
+// A region is reused only when nothing uses it (its validate has completed
+// and no interpolate that reads it is in flight); when the next region is
+// still in use the launch is simply not kept, and an interpolate that misses
+// any shard takes the host path: keeping never changes a result.
+struct KeepKey {
+    uint8_t root[32];
+    uint32_t idx;
+    bool operator==(const KeepKey &o) const { return idx == o.idx && !memcmp(root, o.root, 32); }
+};
+struct KeepKeyHash {
+    size_t operator()(const KeepKey &k) const {  // roots are SHA-256 digests: 8 of their bytes spread well
+        uint64_t h;
+        memcpy(&h, k.root, 8);
+        return (size_t)(h ^ ((uint64_t)k.idx * 0x9e3779b97f4a7c15ull));
+    }
+};
+struct KeepEntry {
+    uint64_t gen;           // the region's generation when inserted
+    const uint8_t *dev;     // the row on the device
+    const uint8_t *host;    // the caller's shard pointer at validate time
+    size_t len;
+    uint8_t leaf[32];
+};
+struct KeepStore {
+    std::mutex mu;
+    uint8_t *dev = nullptr;
+    size_t cap = 0, head = 0;
+    struct Region {
+        size_t off, len;
+        uint64_t gen;
+        int users;  // the validate writing it (until it completes) + interpolates reading it
+        std::vector<KeepKey> keys;
+    };
+    std::deque<Region> regions;  // allocation order: generations ascending
+    uint64_t next_gen = 1;
+    std::unordered_map<KeepKey, KeepEntry, KeepKeyHash> map;
+    uint64_t kept_interps = 0, host_interps = 0, kept_launches = 0, unkept_launches = 0;
+    Region *find(uint64_t gen) {
+        auto it = std::lower_bound(regions.begin(), regions.end(), gen,
+                                   [](const Region &r, uint64_t g) { return r.gen < g; });
+        return it != regions.end() && it->gen == gen ? &*it : nullptr;
+    }
+    void drop(Region &r) {  // forget the region's rows (those not re-inserted since)
+        for (const KeepKey &k : r.keys) {
+            auto it = map.find(k);
+            if (it != map.end() && it->second.gen == r.gen) map.erase(it);
+        }
+    }
+    // A region of `need` bytes for a launch, or 0 when the ring has no free
+    // room at its head (the launch is then not kept).
+    uint64_t alloc(size_t need, uint8_t **where) {
+        std::lock_guard<std::mutex> lk(mu);
+        need = (need + 255) / 256 * 256;
+        if (!dev) return 0;
+        if (need > cap) {
+            unkept_launches++;
+            return 0;
+        }
+        const size_t pos = head + need <= cap ? head : 0;
+        for (const Region &r : regions)
+            if (r.off < pos + need && pos < r.off + r.len && r.users > 0) {
+                unkept_launches++;
+                return 0;
+            }
+        for (auto it = regions.begin(); it != regions.end();) {
+            if (it->off < pos + need && pos < it->off + it->len) {
+                drop(*it);
+                it = regions.erase(it);
+            } else {
+                ++it;
+            }
+        }
+        regions.push_back(Region{pos, need, next_gen, 1, {}});
+        head = pos + need;
+        *where = dev + pos;
+        kept_launches++;
+        return next_gen++;
+    }
+    void release(uint64_t gen) {  // under mu
+        if (Region *r = find(gen)) r->users--;
+    }
+};
 
 }  // namespace
 
@@ -236,6 +336,10 @@ struct rbc_batcher {
 
     void run();
     std::vector<std::unique_ptr<PinnedSet>> pool;  // worker thread only
+
+    KeepStore keep;                     // rbc_batcher_set_keep
+    std::atomic<bool> keep_on{false};
+    bool keep_lookup(const uint8_t *root, const uint8_t *const *shards, const size_t *lens, Req &r);
 
     std::unique_ptr<struct Pending> submit(Kind kind, std::vector<Req> &&batch);
     void finish(struct Pending &p);
@@ -336,19 +440,33 @@ std::unique_ptr<Pending> rbc_batcher::submit(Kind kind, std::vector<Req> &&batch
             const size_t Smax = P->Smax;
             // absent rows stay as they are (never read: the present mask
             // rules them out); a present row is zero-padded to Smax
-            P->shards = P->pin->shards.ensure((size_t)m * n * Smax);
+            const bool kept = kind == K_INTERPK;
+            P->shards = kept ? nullptr : P->pin->shards.ensure((size_t)m * n * Smax);
             P->roots = P->pin->roots.ensure((size_t)m * 32);
             P->values = P->pin->values.ensure((size_t)m * k * Smax);
-            uint8_t *lv = kind == K_INTERPV ? P->pin->leaves.ensure((size_t)m * n * 32) : nullptr;
+            uint8_t *lv = kind != K_INTERP ? P->pin->leaves.ensure((size_t)m * n * 32) : nullptr;
             P->present.assign((size_t)m * n, 0);
             P->digests.resize((size_t)m * 32);
             P->lens.resize(m);
             P->status.assign(m, 0);
-            if (!P->shards || !P->roots || !P->values || (kind == K_INTERPV && !lv)) {
+            if ((!kept && !P->shards) || !P->roots || !P->values || (kind != K_INTERP && !lv)) {
                 P->rc = RBC_ERR_DEVICE;
                 return P;
             }
             for (int t = 0; t < m; ++t) P->lens[t] = S[P->idx[t]];
+            if (kept) {  // the rows are on the device: their addresses and leaves, no shard bytes
+                std::vector<const uint8_t *> rows((size_t)m * n, nullptr);
+                for (int t = 0; t < m; ++t) {
+                    Req &r = b[P->idx[t]];
+                    for (int j = 0; j < n; ++j)
+                        if (r.in_lens[j]) rows[(size_t)t * n + j] = reinterpret_cast<const uint8_t *>(r.dev_rows[j]);
+                    memcpy(lv + (size_t)t * n * 32, r.kleaves.data(), (size_t)n * 32);
+                    memcpy(P->roots + (size_t)t * 32, r.root, 32);
+                }
+                P->rc = rbc_interpolate_batch_kept(ctx, m, rows.data(), P->lens.data(), lv, P->roots, P->values,
+                                                   (size_t)k * Smax, P->digests.data(), P->status.data(), &P->ticket);
+                return P;
+            }
             parallel_for(m, (size_t)n * Smax, [&](int t) {
                 Req &r = b[P->idx[t]];
                 for (int j = 0; j < n; ++j)
@@ -397,6 +515,11 @@ void rbc_batcher::finish(Pending &P) {
             if (r.value_len) *r.value_len = (size_t)k * P.lens[t];
             if (r.digest_out) memcpy(r.digest_out, P.digests.data() + (size_t)t * 32, 32);
         });
+    }
+    if (P.kind == K_INTERPK) {  // the launch no longer reads its keep regions
+        std::lock_guard<std::mutex> lk(keep.mu);
+        for (const Req &r : b)
+            for (uint64_t g : r.kgens) keep.release(g);
     }
     if (P.pin) pool.push_back(std::move(P.pin));  // the launch is complete: its buffers are free
     {  // count the launch before any of its requests reads as done: a client
@@ -581,9 +704,17 @@ int rbc_batcher::v_reserve(size_t need, VBuf **out, int *slot, size_t *off) {
 }
 
 void rbc_batcher::v_launch(VBuf *B) {
-    B->rc = B->count ? rbc_validate_packed_leaves(ctx, B->count, B->arena.p, B->bytes, B->offs, B->lens, B->idx,
-                                                  B->br, B->roots, B->ok, B->any_leaf.load() ? B->lv : nullptr, &B->ticket)
-                     : RBC_OK;
+    B->keep_dev = nullptr;
+    B->keep_gen = B->count && keep_on.load() ? keep.alloc(B->bytes, &B->keep_dev) : 0;
+    if (B->keep_gen)  // the arena moves into its keep region, the leaves come back for the index
+        B->rc = rbc_validate_packed_keep(ctx, B->count, B->arena.p, B->bytes, B->offs, B->lens, B->idx, B->br,
+                                         B->roots, B->ok, B->lv, B->keep_dev, (B->bytes + 255) / 256 * 256,
+                                         &B->ticket);
+    else
+        B->rc = B->count ? rbc_validate_packed_leaves(ctx, B->count, B->arena.p, B->bytes, B->offs, B->lens, B->idx,
+                                                      B->br, B->roots, B->ok, B->any_leaf.load() ? B->lv : nullptr,
+                                                      &B->ticket)
+                         : RBC_OK;
     if (B->rc) B->ticket = 0;
 }
 
@@ -591,6 +722,24 @@ void rbc_batcher::v_complete(VBuf *B) {
     int rc = B->rc;
     if (!rc && B->ticket) rc = rbc_wait(ctx, B->ticket);
     int real = 0;
+    if (B->keep_gen) {  // index the rows that validated, then the launch no longer uses its region
+        std::lock_guard<std::mutex> lk(keep.mu);
+        KeepStore::Region *R = keep.find(B->keep_gen);
+        for (int i = 0; R && !rc && i < B->count; ++i)
+            if (B->out[i] && B->shape[i] && B->ok[i] && B->hostp[i]) {
+                KeepKey key;
+                memcpy(key.root, B->roots + (size_t)i * 32, 32);
+                key.idx = B->idx[i];
+                KeepEntry &e = keep.map[key];
+                e.gen = B->keep_gen;
+                e.dev = B->keep_dev + B->offs[i];
+                e.host = B->hostp[i];
+                e.len = B->lens[i];
+                memcpy(e.leaf, B->lv + (size_t)i * 32, 32);
+                R->keys.push_back(key);
+            }
+        keep.release(B->keep_gen);
+    }
     for (int i = 0; i < B->count; ++i)
         if (B->out[i]) {  // holes have no caller
             const int ok = (!rc && B->shape[i]) ? B->ok[i] : 0;
@@ -689,6 +838,40 @@ void rbc_batcher::v_finish_run() {
     }
 }
 
+// An interpolate request whose every present shard the lane kept (same
+// caller pointer and length): its rows' device addresses and leaves, and a
+// use of each region they lie in (released when the launch completes) --
+// under the store lock, so no region it names can be reused before then.
+bool rbc_batcher::keep_lookup(const uint8_t *root, const uint8_t *const *shards, const size_t *lens, Req &r) {
+    if (!keep_on.load()) return false;
+    std::lock_guard<std::mutex> lk(keep.mu);
+    r.dev_rows.assign(n, 0);
+    r.kleaves.assign((size_t)n * 32, 0);
+    r.kgens.clear();
+    KeepKey key;
+    memcpy(key.root, root, 32);
+    int present = 0;
+    for (int j = 0; j < n; ++j) {
+        if (!lens[j]) continue;
+        key.idx = (uint32_t)j;
+        const auto it = keep.map.find(key);
+        if (it == keep.map.end() || it->second.host != shards[j] || it->second.len != lens[j]) {
+            keep.host_interps++;
+            return false;
+        }
+        r.dev_rows[j] = (uint64_t)(uintptr_t)it->second.dev;
+        memcpy(r.kleaves.data() + (size_t)j * 32, it->second.leaf, 32);
+        if (std::find(r.kgens.begin(), r.kgens.end(), it->second.gen) == r.kgens.end())
+            r.kgens.push_back(it->second.gen);
+        ++present;
+    }
+    if (!present) return false;
+    for (uint64_t g : r.kgens)
+        if (KeepStore::Region *R = keep.find(g)) R->users++;
+    keep.kept_interps++;
+    return true;
+}
+
 namespace {
 uint64_t enqueue(rbc_batcher *b, Req &&r) {
     std::lock_guard<std::mutex> lk(b->mu);
@@ -735,6 +918,42 @@ int rbc_batcher_set_validate(rbc_batcher *b, int max_msgs, size_t max_bytes) {
     return RBC_OK;
 }
 
+int rbc_batcher_set_keep(rbc_batcher *b, size_t device_bytes) {
+    if (!b) return RBC_ERR_INVALID_ARG;
+    {
+        std::lock_guard<std::mutex> lk(b->vmu);
+        if (b->v_next_gen != 1) return RBC_ERR_INVALID_ARG;  // before the first validate only
+    }
+    std::lock_guard<std::mutex> lk(b->keep.mu);
+    if (b->keep.dev) {
+        rbc_dev_free(b->keep.dev);
+        b->keep.dev = nullptr;
+        b->keep.cap = 0;
+    }
+    b->keep_on.store(false);
+    if (!device_bytes) return RBC_OK;
+    int dev = 0;
+    void *p = nullptr;
+    if (rbc_ctx_device(b->ctx, &dev) != RBC_OK || rbc_dev_malloc(dev, device_bytes, &p) != RBC_OK)
+        return RBC_ERR_DEVICE;
+    b->keep.dev = static_cast<uint8_t *>(p);
+    b->keep.cap = device_bytes;
+    b->keep.head = 0;
+    b->keep_on.store(true);
+    return RBC_OK;
+}
+
+int rbc_batcher_keep_stats(rbc_batcher *b, uint64_t *kept_interps, uint64_t *host_interps, uint64_t *kept_launches,
+                           uint64_t *unkept_launches) {
+    if (!b) return RBC_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(b->keep.mu);
+    if (kept_interps) *kept_interps = b->keep.kept_interps;
+    if (host_interps) *host_interps = b->keep.host_interps;
+    if (kept_launches) *kept_launches = b->keep.kept_launches;
+    if (unkept_launches) *unkept_launches = b->keep.unkept_launches;
+    return RBC_OK;
+}
+
 void rbc_batcher_destroy(rbc_batcher *b) {
     if (!b) return;
     {
@@ -751,6 +970,7 @@ void rbc_batcher_destroy(rbc_batcher *b) {
     b->v_free.notify_all();
     if (b->v_worker.joinable()) b->v_worker.join();
     if (b->v_completer.joinable()) b->v_completer.join();
+    if (b->keep.dev) rbc_dev_free(b->keep.dev);  // every launch that used it has completed
     delete b;
 }
 
@@ -828,6 +1048,7 @@ int rbc_batcher_validate_leaf(rbc_batcher *b, const uint8_t *root, const uint8_t
     uint8_t *row = B->arena.p + off, *br = B->br + (size_t)slot * b->bslot;
     B->out[slot] = ok_out;
     B->lout[slot] = leaf_out;
+    B->hostp[slot] = shape_ok ? shard : nullptr;
     if (leaf_out && !B->any_leaf.load(std::memory_order_relaxed))
         B->any_leaf.store(true);  // before this slot's pend add: the launch sees it
     B->offs[slot] = off;
@@ -869,7 +1090,7 @@ int rbc_batcher_interpolate(rbc_batcher *b, const uint8_t *root, const uint8_t *
                             uint64_t *ticket) {
     if (!b || !ticket || !root || !shards || !lens || !value_out) return RBC_ERR_INVALID_ARG;
     Req r;
-    r.kind = K_INTERP;
+    r.kind = b->keep_lookup(root, shards, lens, r) ? K_INTERPK : K_INTERP;
     r.root = root;
     r.in_shards.assign(shards, shards + b->n);
     r.in_lens.assign(lens, lens + b->n);
@@ -886,7 +1107,7 @@ int rbc_batcher_interpolate_verified(rbc_batcher *b, const uint8_t *root, const 
                                      size_t *value_len, uint8_t *digest_out, uint64_t *ticket) {
     if (!b || !ticket || !root || !shards || !lens || !value_out || !leaves) return RBC_ERR_INVALID_ARG;
     Req r;
-    r.kind = K_INTERPV;
+    r.kind = b->keep_lookup(root, shards, lens, r) ? K_INTERPK : K_INTERPV;
     r.root = root;
     r.in_shards.assign(shards, shards + b->n);
     r.in_lens.assign(lens, lens + b->n);

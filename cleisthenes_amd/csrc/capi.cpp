@@ -1120,6 +1120,12 @@ int rbc_ctx_params(const rbc_ctx *c, int *k, int *p, int *depth) {
     return RBC_OK;
 }
 
+int rbc_ctx_device(const rbc_ctx *c, int *device) {
+    if (!c || !device) return RBC_ERR_INVALID_ARG;
+    *device = c->device;
+    return RBC_OK;
+}
+
 int rbc_ctx_set_wave_priority(rbc_ctx *c, int commit_prio, int receive_prio) {
     if (!c || commit_prio < 0 || commit_prio > 3 || receive_prio < 0 || receive_prio > 3) return RBC_ERR_INVALID_ARG;
     c->tx_prio = commit_prio;
@@ -1864,9 +1870,35 @@ int rbc_validate_packed(rbc_ctx *c, int count, const uint8_t *arena, size_t aren
                                       ticket);
 }
 
+static int validate_packed(rbc_ctx *c, int count, const uint8_t *arena, size_t arena_bytes, const uint64_t *offs,
+                           const uint32_t *lens, const uint8_t *idx, const uint8_t *branches, const uint8_t *roots,
+                           uint8_t *ok_out, uint8_t *leaves_out, uint8_t *keep_dev, size_t keep_bytes,
+                           uint64_t *ticket);
+
 int rbc_validate_packed_leaves(rbc_ctx *c, int count, const uint8_t *arena, size_t arena_bytes, const uint64_t *offs,
                                const uint32_t *lens, const uint8_t *idx, const uint8_t *branches, const uint8_t *roots,
                                uint8_t *ok_out, uint8_t *leaves_out, uint64_t *ticket) {
+    return validate_packed(c, count, arena, arena_bytes, offs, lens, idx, branches, roots, ok_out, leaves_out, nullptr,
+                           0, ticket);
+}
+
+// The messages land in the caller's device buffer instead of the slot's and
+// stay there: an interpolate of the same shards reads them on the device
+// (rbc_interpolate_batch_kept), so the ECHO rows cross PCIe once.
+int rbc_validate_packed_keep(rbc_ctx *c, int count, const uint8_t *arena, size_t arena_bytes, const uint64_t *offs,
+                             const uint32_t *lens, const uint8_t *idx, const uint8_t *branches, const uint8_t *roots,
+                             uint8_t *ok_out, uint8_t *leaves_out, uint8_t *keep_dev, size_t keep_bytes,
+                             uint64_t *ticket) {
+    if (count > 0 && (!keep_dev || keep_bytes < arena_bytes)) return RBC_ERR_INVALID_ARG;
+    return validate_packed(c, count, arena, arena_bytes, offs, lens, idx, branches, roots, ok_out, leaves_out,
+                           keep_dev, keep_bytes, ticket);
+}
+
+static int validate_packed(rbc_ctx *c, int count, const uint8_t *arena, size_t arena_bytes, const uint64_t *offs,
+                           const uint32_t *lens, const uint8_t *idx, const uint8_t *branches, const uint8_t *roots,
+                           uint8_t *ok_out, uint8_t *leaves_out, uint8_t *keep_dev, size_t keep_bytes,
+                           uint64_t *ticket) {
+    (void)keep_bytes;
     if (!c || count < 0 ||
         (count > 0 && (!arena || !arena_bytes || !offs || !lens || !idx || !branches || !roots || !ok_out)))
         return RBC_ERR_INVALID_ARG;
@@ -1892,7 +1924,8 @@ int rbc_validate_packed_leaves(rbc_ctx *c, int count, const uint8_t *arena, size
     if (!sp) return RBC_ERR_DEVICE;
     Slot &s = *sp;
     hipStream_t st = s.stream;
-    RBC_HIP(s.d_shards.ensure(arena_bytes));
+    if (!keep_dev) RBC_HIP(s.d_shards.ensure(arena_bytes));
+    uint8_t *d_arena = keep_dev ? keep_dev : s.d_shards.as<uint8_t>();
     RBC_HIP(s.d_branches.ensure((size_t)count * bslot));
     RBC_HIP(s.d_roots.ensure((size_t)count * 32));
     RBC_HIP(s.d_slens.ensure((size_t)count * 4));
@@ -1904,16 +1937,16 @@ int rbc_validate_packed_leaves(rbc_ctx *c, int count, const uint8_t *arena, size
     RBC_HIP(hipMemcpyAsync(s.d_slens.p, lens, (size_t)count * 4, hipMemcpyHostToDevice, st));
     if (zc)
         RBC_HIP(rbc_launch_gather_msgs(zc, s.d_offs.as<uint64_t>(), s.d_slens.as<uint32_t>(), (uint32_t)count,
-                                       s.d_shards.as<uint8_t>(), st));
+                                       d_arena, st));
     else
-        RBC_HIP(hipMemcpyAsync(s.d_shards.p, arena, arena_bytes, hipMemcpyHostToDevice, st));
+        RBC_HIP(hipMemcpyAsync(d_arena, arena, arena_bytes, hipMemcpyHostToDevice, st));
     RBC_HIP(hipMemcpyAsync(s.d_idx.p, idx, (size_t)count, hipMemcpyHostToDevice, st));
     RBC_HIP(hipMemcpyAsync(s.d_branches.p, branches, (size_t)count * bslot, hipMemcpyHostToDevice, st));
     RBC_HIP(hipMemcpyAsync(s.d_roots.p, roots, (size_t)count * 32, hipMemcpyHostToDevice, st));
     ShaArgs a{};
     a.count = count;
     a.rows_per_inst = 1;
-    a.rows = s.d_shards.as<uint8_t>();
+    a.rows = d_arena;
     a.row_offs = s.d_offs.as<uint64_t>();
     a.lens = s.d_slens.as<uint32_t>();
     a.idx = s.d_idx.as<uint8_t>();
@@ -1943,7 +1976,7 @@ int rbc_validate_packed_leaves(rbc_ctx *c, int count, const uint8_t *arena, size
 static int host_receive(rbc_ctx *c, int count, const uint8_t *shards, size_t shard_pitch, const size_t *shard_lens,
                         const uint8_t *present, const uint8_t *leaves, const uint8_t *branches, const uint8_t *roots,
                         uint8_t *valid_out, uint8_t *values_out, size_t value_pitch, uint8_t *digests_out,
-                        int32_t *status_out, uint64_t *ticket);
+                        int32_t *status_out, uint64_t *ticket, const uint8_t *const *dev_rows = nullptr);
 
 int rbc_interpolate_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t shard_pitch,
                           const size_t *shard_lens, const uint8_t *present, const uint8_t *roots,
@@ -1965,6 +1998,16 @@ int rbc_interpolate_batch_verified(rbc_ctx *c, int count, const uint8_t *shards,
                         values_out, value_pitch, digests_out, status_out, ticket);
 }
 
+// Rows a rbc_validate_packed_keep left on the device: a device gather
+// assembles the batch, nothing of the shards crosses PCIe again.
+int rbc_interpolate_batch_kept(rbc_ctx *c, int count, const uint8_t *const *rows, const size_t *shard_lens,
+                               const uint8_t *leaves, const uint8_t *roots, uint8_t *values_out, size_t value_pitch,
+                               uint8_t *digests_out, int32_t *status_out, uint64_t *ticket) {
+    if (count > 0 && !rows) return RBC_ERR_INVALID_ARG;
+    return host_receive(c, count, nullptr, 0, shard_lens, nullptr, leaves, nullptr, roots, nullptr, values_out,
+                        value_pitch, digests_out, status_out, ticket, rows);
+}
+
 int rbc_receive_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t shard_pitch, const size_t *shard_lens,
                       const uint8_t *present, const uint8_t *branches, const uint8_t *roots, uint8_t *valid_out,
                       uint8_t *values_out, size_t value_pitch, uint8_t *digests_out, int32_t *status_out,
@@ -1982,14 +2025,15 @@ int rbc_receive_batch(rbc_ctx *c, int count, const uint8_t *shards, size_t shard
 static int host_receive(rbc_ctx *c, int count, const uint8_t *shards, size_t shard_pitch, const size_t *shard_lens,
                         const uint8_t *present, const uint8_t *leaves, const uint8_t *branches, const uint8_t *roots,
                         uint8_t *valid_out, uint8_t *values_out, size_t value_pitch, uint8_t *digests_out,
-                        int32_t *status_out, uint64_t *ticket) {
+                        int32_t *status_out, uint64_t *ticket, const uint8_t *const *dev_rows) {
     if (!c || count < 0 ||
-        (count > 0 && (!shards || !shard_lens || !present || !roots || !values_out || !status_out)))
+        (count > 0 && (!shard_lens || !roots || !values_out || !status_out ||
+                       (!dev_rows && (!shards || !present)))))
         return RBC_ERR_INVALID_ARG;
     if (count == 0) { if (ticket) *ticket = 0; return RBC_OK; }
     size_t Smax = 1;
     for (int i = 0; i < count; ++i) {
-        if (shard_lens[i] > shard_pitch) return RBC_ERR_INVALID_ARG;
+        if (shard_lens[i] > (dev_rows ? (size_t)0xffffffffu : shard_pitch)) return RBC_ERR_INVALID_ARG;
         Smax = std::max(Smax, shard_lens[i]);
     }
     if (value_pitch < (size_t)c->k * Smax) return RBC_ERR_INVALID_ARG;
@@ -1997,7 +2041,7 @@ static int host_receive(rbc_ctx *c, int count, const uint8_t *shards, size_t sha
     // what is not already pinned caller memory
     bool uniform = true;
     for (int i = 0; i < count && uniform; ++i) uniform = shard_lens[i] == Smax;
-    const bool in_direct = uniform && host_pinned(shards, ((size_t)count * n_of(c) - 1) * shard_pitch + Smax);
+    const bool in_direct = !dev_rows && uniform && host_pinned(shards, ((size_t)count * n_of(c) - 1) * shard_pitch + Smax);
     const uint8_t *zc = in_direct ? host_zero_copy(shards, ((size_t)count * n_of(c) - 1) * shard_pitch + Smax)
                                   : nullptr;
     // a pinned batch whose pitch the device rows can take moves in ONE plain
@@ -2032,7 +2076,9 @@ static int host_receive(rbc_ctx *c, int count, const uint8_t *shards, size_t sha
     RBC_HIP(s.d_status.ensure((size_t)count * 4));
     RBC_HIP(s.d_slens.ensure((size_t)count * 4));
     const bool out_direct = host_pinned(values_out, (size_t)(count - 1) * value_pitch + (size_t)k * Smax);
-    const size_t in_stage = in_direct ? 0 : sh_bytes, out_stage = out_direct ? 0 : (size_t)count * vpitch;
+    // device rows: the [count][n] table of their addresses instead of a shard staging block
+    const size_t in_stage = dev_rows ? (size_t)count * n * 8 : in_direct ? 0 : sh_bytes,
+                 out_stage = out_direct ? 0 : (size_t)count * vpitch;
     RBC_HIP(s.h_in.ensure(in_stage + (size_t)count * (n + 32 + 4)));
     RBC_HIP(s.h_out.ensure(out_stage + (size_t)count * (32 + 4)));
     // [shard staging][lens u32][roots][present]: the u32 lens stay aligned for any n
@@ -2040,9 +2086,21 @@ static int host_receive(rbc_ctx *c, int count, const uint8_t *shards, size_t sha
     uint32_t *ln = reinterpret_cast<uint32_t *>(i_sh + in_stage);
     uint8_t *i_rt = reinterpret_cast<uint8_t *>(ln + count), *i_pr = i_rt + (size_t)count * 32;
     // present mask first: the zero-copy gather reads it
-    memcpy(i_pr, present, (size_t)count * n);
+    if (dev_rows)
+        for (size_t r = 0; r < (size_t)count * n; ++r) i_pr[r] = dev_rows[r] != nullptr;
+    else
+        memcpy(i_pr, present, (size_t)count * n);
     RBC_HIP(hipMemcpyAsync(d_pres, i_pr, (size_t)count * n, hipMemcpyHostToDevice, st));
-    if (zc) {
+    if (dev_rows) {  // device to device: one wave per row, zero past S_i and for absent rows
+        uint64_t *tab = reinterpret_cast<uint64_t *>(i_sh);
+        for (size_t r = 0; r < (size_t)count * n; ++r) tab[r] = (uint64_t)(uintptr_t)dev_rows[r];
+        for (int i = 0; i < count; ++i) ln[i] = (uint32_t)shard_lens[i];
+        RBC_HIP(s.d_offs.ensure((size_t)count * n * 8));
+        RBC_HIP(hipMemcpyAsync(s.d_offs.p, tab, (size_t)count * n * 8, hipMemcpyHostToDevice, st));
+        RBC_HIP(hipMemcpyAsync(s.d_slens.p, ln, (size_t)count * 4, hipMemcpyHostToDevice, st));
+        RBC_HIP(rbc_launch_gather_ptrs(s.d_offs.as<uint64_t>(), s.d_slens.as<uint32_t>(), (uint32_t)n,
+                                       s.d_shards.as<uint8_t>(), (uint32_t)dpitch, (uint32_t)(count * n), st));
+    } else if (zc) {
         // only the received rows cross PCIe (N-f of N at the bench shape)
         for (int i = 0; i < count; ++i) ln[i] = (uint32_t)shard_lens[i];
         RBC_HIP(rbc_launch_gather_present(zc, shard_pitch, (uint32_t)Smax, d_pres, s.d_shards.as<uint8_t>(),

@@ -251,6 +251,9 @@ hipError_t rbc_launch_gather_present(const uint8_t *host, uint64_t hpitch, uint3
 hipError_t rbc_launch_gather_msgs(const uint8_t *host, const uint64_t *offs, const uint32_t *lens, uint32_t count,
                                   uint8_t *dev, hipStream_t st);
 // pinned host values (device array of their addresses) -> device value rows (zero-copy reads)
+// rows from device addresses (0 = absent), lens per instance of n rows
+hipError_t rbc_launch_gather_ptrs(const uint64_t *ptrs, const uint32_t *lens, uint32_t n, uint8_t *dev,
+                                  uint32_t dpitch, uint32_t rows, hipStream_t st);
 hipError_t rbc_launch_gather_values(const uint64_t *ptrs, const uint32_t *lens, uint32_t count, uint8_t *dev,
                                     uint64_t vpitch, hipStream_t st);
 hipError_t rbc_launch_count_mismatch(const uint8_t *a, uint64_t a_pitch, const uint8_t *b, uint64_t b_pitch,

@@ -1787,9 +1787,36 @@ __global__ __launch_bounds__(256) void gather_values_kernel(const uint64_t *ptrs
                      reinterpret_cast<uint4 *>(dev + (size_t)i * vpitch), (lens[i] + 15) / 16, lane);
 }
 
+// Interpolate over rows a validate left in device memory
+// (rbc_interpolate_batch_kept): row r of the [count][n] batch is read from
+// ptrs[r] (lens[r / n] bytes; 0 = an absent row, written as zeros) into
+// dev + r * dpitch, zero-padded to dpitch.  One wave per row, HBM to HBM.
+__global__ __launch_bounds__(256) void gather_ptrs_kernel(const uint64_t *ptrs, const uint32_t *lens, uint32_t n,
+                                                          uint8_t *dev, uint32_t dpitch, uint32_t rows) {
+    const uint32_t lane = threadIdx.x & 63u, waves = gridDim.x * (blockDim.x >> 6);
+    const uint32_t chunks = dpitch / 16;
+    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < rows; r += waves) {
+        uint4 *dst = reinterpret_cast<uint4 *>(dev + (size_t)r * dpitch);
+        const uint64_t src = ptrs[r];
+        if (!src) {
+            for (uint32_t c = lane; c < chunks; c += 64) dst[c] = make_uint4(0, 0, 0, 0);
+            continue;
+        }
+        row_gather16(reinterpret_cast<const uint8_t *>(src), lens[r / n], dst, chunks, lane);
+    }
+}
+
 // ============================================================================
 // launchers
 // ============================================================================
+hipError_t rbc_launch_gather_ptrs(const uint64_t *ptrs, const uint32_t *lens, uint32_t n, uint8_t *dev,
+                                  uint32_t dpitch, uint32_t rows, hipStream_t st) {
+    if (rows == 0) return hipSuccess;
+    if (dpitch % 16 || n == 0) return hipErrorInvalidValue;
+    const uint32_t blocks = std::min((rows + 3) / 4, 2048u);  // device rows: fill the chip, not a PCIe queue
+    hipLaunchKernelGGL(gather_ptrs_kernel, dim3(blocks), dim3(256), 0, st, ptrs, lens, n, dev, dpitch, rows);
+    return hipGetLastError();
+}
 hipError_t rbc_launch_gather_values(const uint64_t *ptrs, const uint32_t *lens, uint32_t count, uint8_t *dev,
                                     uint64_t vpitch, hipStream_t st) {
     if (count == 0) return hipSuccess;

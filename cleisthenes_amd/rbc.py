@@ -431,10 +431,12 @@ class Context:
 
     def validate_packed_submit(self, arena: np.ndarray, offs, lens, idx, branches: np.ndarray, roots: np.ndarray,
                                arena_bytes: Optional[int] = None, leaves: bool = False,
-                               out: Optional[dict] = None) -> "HostTicket":
+                               out: Optional[dict] = None, keep: Optional["DeviceBuffer"] = None) -> "HostTicket":
         """Asynchronous rbc_validate_packed_leaves; .wait() returns the verdicts
         (bool array) or, leaves=True, (verdicts, leaves [count][32]).  `out` may
-        hold preallocated (pinned) "ok" [count] and "leaves" [count][32] arrays."""
+        hold preallocated (pinned) "ok" [count] and "leaves" [count][32] arrays.
+        keep (a DeviceBuffer >= the arena): rbc_validate_packed_keep -- message i
+        then stays at keep.value + offs[i] for interpolate_kept_submit."""
         count = len(offs)
         arena = arena if (isinstance(arena, np.ndarray) and arena.dtype == np.uint8 and arena.flags.c_contiguous) \
             else np.ascontiguousarray(arena, dtype=np.uint8)
@@ -446,10 +448,15 @@ class Context:
         ok = out["ok"] if out else np.zeros(max(count, 1), dtype=np.uint8)
         lv = (out["leaves"] if out else np.zeros((max(count, 1), 32), dtype=np.uint8)) if leaves else None
         t = c_uint64(0)
-        check(lib.rbc_validate_packed_leaves(self._p, count, _ptr(arena),
-                                             arena.nbytes if arena_bytes is None else arena_bytes, _ptr(o), _ptr(ln),
-                                             _ptr(ix), _ptr(br), _ptr(rt), _ptr(ok),
-                                             _ptr(lv) if leaves else None, byref(t)), "rbc_validate_packed_leaves")
+        nb = arena.nbytes if arena_bytes is None else arena_bytes
+        if keep is not None:
+            check(lib.rbc_validate_packed_keep(self._p, count, _ptr(arena), nb, _ptr(o), _ptr(ln), _ptr(ix), _ptr(br),
+                                               _ptr(rt), _ptr(ok), _ptr(lv) if leaves else None, keep.ptr,
+                                               keep.nbytes, byref(t)), "rbc_validate_packed_keep")
+        else:
+            check(lib.rbc_validate_packed_leaves(self._p, count, _ptr(arena), nb, _ptr(o), _ptr(ln), _ptr(ix),
+                                                 _ptr(br), _ptr(rt), _ptr(ok), _ptr(lv) if leaves else None,
+                                                 byref(t)), "rbc_validate_packed_leaves")
 
         class _V(HostTicket):
             def wait(self_):
@@ -499,6 +506,34 @@ class Context:
                                                  byref(t)), "rbc_interpolate_batch_verified")
         out = {"values": values, "digests": digests, "status": status}
         return HostTicket(self, t.value, out, keep=(shards, present, roots, sl, lv))
+
+    def interpolate_kept_submit(self, rows: np.ndarray, shard_lens, roots: np.ndarray,
+                                leaves: Optional[np.ndarray] = None, values_out: Optional[np.ndarray] = None,
+                                digests_out: Optional[np.ndarray] = None,
+                                status_out: Optional[np.ndarray] = None) -> "HostTicket":
+        """Asynchronous rbc_interpolate_batch_kept: rows [count][n] uint64 device
+        addresses of the shards (0 = missing), e.g. keep.value + offs of a
+        validate_packed_submit(keep=...); leaves [count][n][32] as
+        interpolate_submit's.  .wait() returns values / digests / status."""
+        rows = np.ascontiguousarray(rows, dtype=np.uint64)
+        count, n = rows.shape
+        assert n == self.n
+        roots = np.ascontiguousarray(roots, dtype=np.uint8)
+        sl = (c_size_t * count)(*[int(x) for x in shard_lens])
+        vp = self.k * int(max(shard_lens))
+        values = values_out if values_out is not None else np.zeros((count, max(vp, 1)), dtype=np.uint8)
+        assert values.shape[0] == count and values.shape[1] >= vp and values.dtype == np.uint8
+        digests = np.zeros((count, 32), dtype=np.uint8) if digests_out is None else digests_out
+        status = np.zeros(count, dtype=np.int32) if status_out is None else status_out
+        lv = None if leaves is None else np.ascontiguousarray(leaves, dtype=np.uint8)
+        assert lv is None or lv.size == count * self.n * 32
+        t = c_uint64(0)
+        check(lib.rbc_interpolate_batch_kept(self._p, count, _ptr(rows), sl, _ptr(lv) if lv is not None else None,
+                                             _ptr(roots), _ptr(values), values.shape[1], _ptr(digests),
+                                             status.ctypes.data_as(_lib.i32p), byref(t)),
+              "rbc_interpolate_batch_kept")
+        out = {"values": values, "digests": digests, "status": status}
+        return HostTicket(self, t.value, out, keep=(rows, roots, sl, lv))
 
     def receive_batch(self, shards, shard_lens, present, branches, roots, **kw) -> dict:
         return self.receive_submit(shards, shard_lens, present, branches, roots, **kw).wait()
@@ -738,6 +773,14 @@ class Encoder:
         return bytes(out[:out_size])
 
 
+def _by_ref(x) -> np.ndarray:
+    """A contiguous uint8 ndarray as it is (the caller keeps it unchanged until
+    the request completes), anything else copied into one."""
+    if isinstance(x, np.ndarray) and x.dtype == np.uint8 and x.flags.c_contiguous and x.ndim == 1:
+        return x
+    return _bytes_array(x).copy()
+
+
 class Batcher:
     """Request coalescing (include/rbc_gpu.h rbc_batcher_*): single-instance
     shard / validate / interpolate submissions from any number of threads are
@@ -774,8 +817,10 @@ class Batcher:
 
     def submit_validate(self, root, branch, shard, index, leaf: bool = False) -> dict:
         """validateMessage through the lane; leaf=True also returns the shard's
-        SHA-256 leaf (rbc_batcher_validate_leaf) for submit_interpolate(leaves=)."""
-        r, b, s = _bytes_array(root).copy(), _bytes_array(branch).copy(), _bytes_array(shard).copy()
+        SHA-256 leaf (rbc_batcher_validate_leaf) for submit_interpolate(leaves=).
+        A contiguous uint8 ndarray shard is passed by reference (not copied):
+        with set_keep, interpolate finds it kept when handed the same array."""
+        r, b, s = _bytes_array(root).copy(), _bytes_array(branch).copy(), _by_ref(shard)
         h = {"kind": "validate", "r": r, "b": b, "s": s, "ok": c_int(0), "t": c_uint64(0),
              "leaf": np.zeros(32, np.uint8) if leaf else None}
         check(lib.rbc_batcher_validate_leaf(self._p, _ptr(r), _ptr(b) if len(b) else None, len(b),
@@ -789,7 +834,7 @@ class Batcher:
         present shards from submit_validate(leaf=True)) selects
         rbc_batcher_interpolate_verified: only regenerated rows are hashed."""
         n, k = self.ctx.n, self.ctx.k
-        arrs = [_bytes_array(x).copy() for x in shards]
+        arrs = [_by_ref(x) for x in shards]
         S = max(len(a) for a in arrs)
         lens = (c_size_t * n)(*[len(a) for a in arrs])
         ptrs = (c_void_p * n)(*[(a.ctypes.data if len(a) else None) for a in arrs])
@@ -822,6 +867,16 @@ class Batcher:
             return {"shards": [h["out"][j * S:(j + 1) * S].copy() for j in range(self.ctx.n)],
                     "root": bytes(h["root"]), "shard_len": S}
         return {"value": bytes(h["value"][: h["vlen"].value]), "digest": bytes(h["dig"])}
+
+    def set_keep(self, device_bytes: int) -> None:
+        """rbc_batcher_set_keep: validated shards stay in a device ring of
+        device_bytes for their instance's interpolate (before the first validate)."""
+        check(lib.rbc_batcher_set_keep(self._p, int(device_bytes)), "rbc_batcher_set_keep")
+
+    def keep_stats(self) -> dict:
+        v = [c_uint64(0) for _ in range(4)]
+        check(lib.rbc_batcher_keep_stats(self._p, *[byref(x) for x in v]), "rbc_batcher_keep_stats")
+        return dict(zip(("kept_interps", "host_interps", "kept_launches", "unkept_launches"), (x.value for x in v)))
 
     def set_validate(self, max_msgs: int, max_bytes: int) -> None:
         """The validate lane's arena size (rbc_batcher_set_validate; before the first validate)."""

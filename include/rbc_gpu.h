@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define RBC_ABI_VERSION 6
+#define RBC_ABI_VERSION 7
 
 /* ---- status codes ------------------------------------------------------- */
 #define RBC_OK 0
@@ -75,6 +75,7 @@ typedef struct rbc_ctx rbc_ctx;
 int rbc_ctx_create(int n, int f, int device, rbc_ctx **out);
 void rbc_ctx_destroy(rbc_ctx *ctx);
 int rbc_ctx_params(const rbc_ctx *ctx, int *k, int *p, int *depth);
+int rbc_ctx_device(const rbc_ctx *ctx, int *device); /* ABI 7: the HIP device the context runs on */
 /* klauspost buildMatrix(k, n) as used by this context: n*k bytes, row-major */
 int rbc_ctx_encode_matrix(const rbc_ctx *ctx, uint8_t *out);
 /* GF(2^8) codec behind encode / interpolate (same bytes either way):
@@ -315,6 +316,19 @@ int rbc_validate_packed_leaves(rbc_ctx *ctx, int count, const uint8_t *arena, si
                                const uint64_t *offs, const uint32_t *lens, const uint8_t *idx,
                                const uint8_t *branches, const uint8_t *roots, uint8_t *ok_out, uint8_t *leaves_out,
                                uint64_t *ticket);
+/* ABI 7: rbc_validate_packed_leaves whose messages stay on the device: the
+ * arena is moved into keep_dev (device memory, keep_bytes >= arena_bytes, e.g.
+ * rbc_dev_malloc) instead of a launch buffer, so message i's bytes are
+ * keep_dev[offs[i] .. offs[i] + lens[i]) once the ticket completes -- for an
+ * interpolate of the same shards straight from device memory
+ * (rbc_interpolate_batch_kept): the ECHO rows of the drop-in's
+ * validateMessage -> interpolate sequence (rbc/rbc.go:92-95, 86-90) then
+ * cross PCIe once.  The caller must not reuse keep_dev before the
+ * interpolates that read it have completed. */
+int rbc_validate_packed_keep(rbc_ctx *ctx, int count, const uint8_t *arena, size_t arena_bytes, const uint64_t *offs,
+                             const uint32_t *lens, const uint8_t *idx, const uint8_t *branches, const uint8_t *roots,
+                             uint8_t *ok_out, uint8_t *leaves_out, uint8_t *keep_dev, size_t keep_bytes,
+                             uint64_t *ticket);
 /* interpolate() for `count` instances: shards [count][n][shard_pitch] with
  * present [count][n] (0 = missing, the Go `len == 0`), shard_lens [count],
  * roots [count][32] -> values_out [count][value_pitch] (k*S_i bytes),
@@ -337,6 +351,15 @@ int rbc_interpolate_batch_verified(rbc_ctx *ctx, int count, const uint8_t *shard
                                    const size_t *shard_lens, const uint8_t *present, const uint8_t *leaves,
                                    const uint8_t *roots, uint8_t *values_out, size_t value_pitch,
                                    uint8_t *digests_out, int32_t *status_out, uint64_t *ticket);
+/* ABI 7: rbc_interpolate_batch_verified over rows that are already in device
+ * memory (rbc_validate_packed_keep): rows [count][n] holds the device address
+ * of shard j of instance i (NULL = missing), shard_lens[i] bytes each; leaves
+ * [count][n][32] their SHA-256 (as rbc_interpolate_batch_verified; NULL
+ * rehashes all N).  Outputs and statuses equal rbc_interpolate_batch_verified's
+ * over the same bytes. */
+int rbc_interpolate_batch_kept(rbc_ctx *ctx, int count, const uint8_t *const *rows, const size_t *shard_lens,
+                               const uint8_t *leaves, const uint8_t *roots, uint8_t *values_out, size_t value_pitch,
+                               uint8_t *digests_out, int32_t *status_out, uint64_t *ticket);
 /* ABI 6: the receiver's whole batch in one submission, for a batching host
  * that holds each instance's received ECHOs together (validateMessage of
  * every present row, rbc/rbc.go:92-95, then interpolate of the ones that
@@ -399,6 +422,24 @@ int rbc_batcher_set_validate(rbc_batcher *b, int max_msgs, size_t max_bytes);
 int rbc_batcher_validate_leaf(rbc_batcher *b, const uint8_t *root, const uint8_t *branch, size_t branch_len,
                               const uint8_t *shard, size_t shard_len, uint32_t index, int *ok_out, uint8_t *leaf_out,
                               uint64_t *ticket);
+/* ABI 7: keep validated shards on the device for their instance's
+ * interpolate.  With a ring of device_bytes (rbc_dev_malloc'ed on the
+ * context's device; 0 turns keeping off, the default) every validate launch
+ * moves its arena into the ring (rbc_validate_packed_keep) and indexes each
+ * shard that validated by (root, index) with the caller's shard pointer and
+ * length; rbc_batcher_interpolate(_verified) whose every present shard is
+ * indexed -- the SAME pointer and length that was validated -- reads the rows
+ * (and their leaves) on the device (rbc_interpolate_batch_kept), so the ECHO
+ * rows cross PCIe once, as the Go handlers' validateMessage -> interpolate
+ * sequence (rbc/rbc.go:92-95, 86-90) stays unchanged.  Any miss takes the
+ * host path; results are the same either way provided the caller does not
+ * modify a validated shard's bytes before its interpolate.  A launch whose
+ * ring region is still read by an interpolate in flight is not kept.  Before
+ * the first validate only. */
+int rbc_batcher_set_keep(rbc_batcher *b, size_t device_bytes);
+/* interpolates served from kept rows / from host memory, validate launches kept / not kept */
+int rbc_batcher_keep_stats(rbc_batcher *b, uint64_t *kept_interps, uint64_t *host_interps, uint64_t *kept_launches,
+                           uint64_t *unkept_launches);
 /* interpolate(): shards/lens are n entries (lens[j] == 0: missing) */
 int rbc_batcher_interpolate(rbc_batcher *b, const uint8_t *root, const uint8_t *const *shards, const size_t *lens,
                             uint8_t *value_out, size_t value_cap, size_t *value_len, uint8_t *digest_out,

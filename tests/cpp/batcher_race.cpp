@@ -98,6 +98,22 @@ int rbc_ctx_params(const rbc_ctx *c, int *k, int *p, int *depth) {
     return RBC_OK;
 }
 
+int rbc_ctx_device(const rbc_ctx *, int *device) {
+    *device = 0;
+    return RBC_OK;
+}
+
+// "device" memory of the stand-in: host memory the launch threads read
+int rbc_dev_malloc(int, size_t bytes, void **ptr) {
+    *ptr = malloc(bytes);
+    return *ptr ? RBC_OK : RBC_ERR_DEVICE;
+}
+
+int rbc_dev_free(void *ptr) {
+    free(ptr);
+    return RBC_OK;
+}
+
 int rbc_host_alloc(size_t bytes, void **ptr) {
     *ptr = malloc(bytes);
     return *ptr ? RBC_OK : RBC_ERR_DEVICE;
@@ -173,6 +189,60 @@ int rbc_validate_packed_leaves(rbc_ctx *c, int count, const uint8_t *arena, size
     };
     if (!ticket) return work();  // a NULL ticket: synchronous, as the real API
     *ticket = launch(c, work);
+    return RBC_OK;
+}
+
+// ABI 7: the arena moves into keep_dev (as the device copy would) and is
+// verified from there
+int rbc_validate_packed_keep(rbc_ctx *c, int count, const uint8_t *arena, size_t arena_bytes, const uint64_t *offs,
+                             const uint32_t *lens, const uint8_t *idx, const uint8_t *branches, const uint8_t *roots,
+                             uint8_t *ok_out, uint8_t *leaves_out, uint8_t *keep_dev, size_t keep_bytes,
+                             uint64_t *ticket) {
+    if (!keep_dev || keep_bytes < arena_bytes) return RBC_ERR_INVALID_ARG;
+    for (int i = 0; i < count; ++i)
+        if (offs[i] % 64 || !lens[i] || offs[i] + (lens[i] + 63) / 64 * 64 > arena_bytes || idx[i] >= c->n)
+            return RBC_ERR_INVALID_ARG;
+    const size_t bslot = (size_t)std::max(c->d, 1) * 32;
+    *ticket = launch(c, [=] {
+        memcpy(keep_dev, arena, arena_bytes);
+        for (int i = 0; i < count; ++i) {
+            ok_out[i] = rbcref_merkle_verify(c->n, keep_dev + offs[i], lens[i], idx[i], branches + i * bslot,
+                                             roots + 32 * i);
+            if (leaves_out) rbcref_sha256(keep_dev + offs[i], lens[i], leaves_out + 32 * (size_t)i);
+        }
+        return RBC_OK;
+    });
+    return RBC_OK;
+}
+
+// ABI 7: rows read from the kept "device" addresses at some point before completion
+int rbc_interpolate_batch_kept(rbc_ctx *c, int count, const uint8_t *const *rows, const size_t *shard_lens,
+                               const uint8_t *leaves, const uint8_t *roots, uint8_t *values_out, size_t value_pitch,
+                               uint8_t *digests_out, int32_t *status_out, uint64_t *ticket) {
+    for (int i = 0; i < count; ++i)
+        if ((size_t)c->k * shard_lens[i] > value_pitch) return RBC_ERR_INVALID_ARG;
+    std::vector<const uint8_t *> rp(rows, rows + (size_t)count * c->n);
+    std::vector<size_t> sl(shard_lens, shard_lens + count);
+    *ticket = launch(c, [=] {
+        for (int i = 0; i < count; ++i) {
+            const size_t S = sl[i];
+            std::vector<uint8_t> flat((size_t)c->n * S, 0), valid(c->n, 0);
+            for (int j = 0; j < c->n; ++j)
+                if (const uint8_t *r = rp[(size_t)i * c->n + j]) {
+                    memcpy(flat.data() + (size_t)j * S, r, S);
+                    valid[j] = 1;
+                }
+            status_out[i] =
+                leaves ? rbcref_interpolate_leaves(c->n, c->f, flat.data(), S, S, valid.data(),
+                                                   leaves + (size_t)i * c->n * 32, roots + 32 * i,
+                                                   values_out + (size_t)i * value_pitch,
+                                                   digests_out ? digests_out + 32 * i : nullptr)
+                       : rbcref_interpolate(c->n, c->f, flat.data(), S, S, valid.data(), roots + 32 * i,
+                                            values_out + (size_t)i * value_pitch,
+                                            digests_out ? digests_out + 32 * i : nullptr);
+        }
+        return RBC_OK;
+    });
     return RBC_OK;
 }
 
@@ -546,6 +616,88 @@ void destroy_outstanding(int n, int f, const std::vector<Commit> &pool, int T, i
     printf("n=%d f=%d destroy with %d requests outstanding: all drained\n", n, f, n_checked);
 }
 
+// ABI 7, rbc_batcher_set_keep: each client runs RBC instances of its own
+// (fresh values), validates every ECHO (some tampered) and interpolates the
+// ones that validated -- the Go handlers' sequence.  A keep ring of a few
+// arenas wraps many times, so launches are kept and not kept and regions are
+// recycled while other clients' interpolates pin theirs; every 4th
+// interpolate passes copies of the validated shards (another pointer: the host
+// path).  Every value and digest must equal the oracle's, and both paths must
+// have run.
+void kept_epoch(int n, int f, int T, int R, size_t ring) {
+    const int k = n - 2 * f, d = rbcref_tree_depth(n);
+    rbc_ctx ctx;
+    ctx.n = n;
+    ctx.f = f;
+    ctx.k = k;
+    ctx.d = d;
+    rbc_batcher *bt = nullptr;
+    if (rbc_batcher_create(&ctx, 4, 200, &bt) != RBC_OK || rbc_batcher_set_validate(bt, 9, 1 << 14) != RBC_OK ||
+        rbc_batcher_set_keep(bt, ring) != RBC_OK)
+        abort();
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            std::mt19937_64 rng(4242 + t);
+            for (int r = 0; r < R; ++r) {
+                std::vector<uint8_t> v(1 + rng() % 2500);
+                for (auto &c : v) c = (uint8_t)rng();
+                const Commit cm = commit(n, f, v);
+                std::vector<std::vector<uint8_t>> rows(n), brs(n);
+                std::vector<int> ok(n, -1);
+                std::vector<uint64_t> tk(n, 0);
+                const int bad = (int)(rng() % (2 * n)) - n;  // < 0: none tampered
+                for (int j = 0; j < n; ++j) {
+                    rows[j].assign(cm.shards.begin() + (size_t)j * cm.S, cm.shards.begin() + (size_t)(j + 1) * cm.S);
+                    if (j == bad) rows[j][rng() % cm.S] ^= 0x10;
+                    brs[j] = flat_branch(n, d, cm, (uint32_t)j);
+                    EXPECT(rbc_batcher_validate(bt, cm.root, brs[j].data(), brs[j].size(), rows[j].data(),
+                                                rows[j].size(), (uint32_t)j, &ok[j], &tk[j]) == RBC_OK, "kv");
+                }
+                std::vector<const uint8_t *> ptrs(n, nullptr);
+                std::vector<size_t> lens(n, 0);
+                std::vector<std::vector<uint8_t>> copies(n);
+                const bool copy = r % 4 == 3;
+                for (int j = 0; j < n; ++j) {
+                    EXPECT(rbc_batcher_wait(bt, tk[j]) == RBC_OK, "kv wait");
+                    EXPECT(ok[j] == (j != bad), "kept epoch verdict %d at %d", ok[j], j);
+                    if (ok[j] == 1) {
+                        copies[j] = rows[j];
+                        ptrs[j] = copy ? copies[j].data() : rows[j].data();
+                        lens[j] = cm.S;
+                    }
+                }
+                std::vector<uint8_t> value((size_t)k * cm.S), digest(32), want_v((size_t)k * cm.S), want_d(32);
+                std::vector<uint8_t> flat((size_t)n * cm.S, 0), valid(n, 0);
+                for (int j = 0; j < n; ++j)
+                    if (lens[j]) {
+                        memcpy(flat.data() + (size_t)j * cm.S, rows[j].data(), cm.S);
+                        valid[j] = 1;
+                    }
+                const int want = rbcref_interpolate(n, f, flat.data(), cm.S, cm.S, valid.data(), cm.root,
+                                                    want_v.data(), want_d.data());
+                size_t vlen = 0;
+                uint64_t ti = 0;
+                EXPECT(rbc_batcher_interpolate(bt, cm.root, ptrs.data(), lens.data(), value.data(), value.size(),
+                                               &vlen, digest.data(), &ti) == RBC_OK, "ki");
+                const int rc = rbc_batcher_wait(bt, ti);
+                EXPECT(rc == want, "kept interpolate status %d want %d", rc, want);
+                if (rc == RBC_OK)
+                    EXPECT(value == want_v && digest == want_d && !memcmp(value.data(), v.data(), v.size()),
+                           "kept interpolate result differs from the oracle");
+            }
+        });
+    for (auto &x : th) x.join();
+    uint64_t kept = 0, host = 0, kl = 0, ul = 0;
+    rbc_batcher_keep_stats(bt, &kept, &host, &kl, &ul);
+    rbc_batcher_destroy(bt);
+    EXPECT(kept > 0 && host > 0 && kl > 0, "keep paths: %llu kept, %llu host interpolates, %llu kept launches",
+           (unsigned long long)kept, (unsigned long long)host, (unsigned long long)kl);
+    printf("n=%d f=%d keep ring %zu B: %llu interpolates from kept rows, %llu from host memory; %llu launches kept, "
+           "%llu not\n", n, f, ring, (unsigned long long)kept, (unsigned long long)host, (unsigned long long)kl,
+           (unsigned long long)ul);
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
@@ -587,6 +739,8 @@ int main(int argc, char **argv) {
         }
         failed_launches(n, f, pool, std::min(T, 6), R);
         destroy_outstanding(n, f, pool, std::min(T, 6), std::max(R / 2, 8));
+        kept_epoch(n, f, std::min(T, 8), std::max(R / 4, 8), (size_t)48 << 10);
+        kept_epoch(n, f, std::min(T, 8), std::max(R / 4, 8), (size_t)6 << 10);  // arenas larger than the ring too
     }
     if (failures) {
         printf("FAILED %d\n", failures.load());

@@ -328,6 +328,16 @@ hipError_t rbc_launch_gather_msgs(const uint8_t *host, const uint64_t *offs, con
     }
     return hipSuccess;
 }
+hipError_t rbc_launch_gather_ptrs(const uint64_t *ptrs, const uint32_t *lens, uint32_t n, uint8_t *dev,
+                                  uint32_t dpitch, uint32_t rows, hipStream_t) {
+    for (uint32_t r = 0; r < rows; ++r) {  // whole rows: zeros past lens[r / n] and for absent rows
+        uint8_t *d = dev + (size_t)r * dpitch;
+        touch(d, dpitch);
+        memset(d, 0, dpitch);
+        if (ptrs[r]) memcpy(d, reinterpret_cast<const void *>(ptrs[r]), lens[r / n]);
+    }
+    return hipSuccess;
+}
 hipError_t rbc_launch_count_mismatch(const uint8_t *, uint64_t, const uint8_t *, uint64_t, uint64_t, uint64_t,
                                      uint32_t *counter, hipStream_t) {
     touch(counter, 4);

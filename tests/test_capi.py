@@ -22,7 +22,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_version_and_strerror():
     from cleisthenes_amd import _lib
-    assert _lib.lib.rbc_abi_version() == 6
+    assert _lib.lib.rbc_abi_version() == 7
     assert _lib.lib.rbc_strerror(-3) == b"too few shards given"
     assert _lib.lib.rbc_strerror(-8).startswith(b"interpolated merkle root")
     assert _lib.lib.rbc_strerror(12345) == b"unknown rbc status"

@@ -147,7 +147,8 @@ def test_batcher_epoch_all_three_kinds_with_reused_leaves(tmp_path):
     instances with a corrupted ECHO.  tools/batcher_bench checks every
     verdict, value, shard row and root itself, and that interpolate with the
     validate lane's leaves (only regenerated rows hashed) equals the full
-    rehash bit for bit; the sampled digests and roots are checked here against
+    rehash bit for bit, and so does the pass with the validated rows kept on
+    the device (ABI 7, rbc_batcher_set_keep); the sampled digests and roots are checked here against
     the C oracle."""
     import json
     import os
@@ -160,12 +161,15 @@ def test_batcher_epoch_all_three_kinds_with_reused_leaves(tmp_path):
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
     rows = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     ep = [x for x in rows if x["phase"] == "epoch"]
-    assert [x["interpolate"].split()[0] for x in ep] == ["verified", "full"]
+    assert [x["interpolate"].split()[0] for x in ep] == ["verified", "full", "kept"]
     for x in ep:
         assert x["instances"] == 1024 and x["echo_messages"] == 1024 * 86 and x["requests"] == 1024 * 88
         assert x["value_failures"] == 0 and x["shard_failures"] == 0 and x["client_failures"] == 0 and x["GBps"] > 0
     chk = rows[-1]
     assert chk["phase"] == "check" and chk["failures"] == 0 and chk["verified_equals_full"]
+    # ABI 7: with rbc_batcher_set_keep every interpolate of the kept pass read its rows on the device
+    keep = next(x for x in rows if x["phase"] == "keep")
+    assert keep["kept_interps"] >= 1024 and keep["kept_launches"] > 0, keep
     n, f, B = 128, 42, 1 << 20
     k = n - 2 * f
     raw = dump.read_bytes()

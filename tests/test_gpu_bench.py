@@ -162,6 +162,7 @@ def test_bench_host_fed_leg_on_every_rank(gpus):
     assert p["ok"] and p["ranks"] == gpus and len(p["per_rank_GBps"]) == gpus
     _host_fed_ok(p["rank0"], n, S)
     assert p["rank0"]["alone_GBps"]["validate+interpolate"] > 0
+    assert p["kept"]["ok"] and p["kept"]["aggregate_GBps"] > 0 and p["rank0"]["kept"]["checks"]["values_ok"]
     for r in d["ranks"]:
         assert r["host_fed"]["ok"] and r["host_fed"]["instances"] == 256 and r["host_fed"]["GBps"] > 0
     assert p["aggregate_GBps"] <= sum(p["per_rank_GBps"]) * 1.001

@@ -258,3 +258,136 @@ def test_shard_commit_many_short_pinned_values_gathered(gpu, n, f):
         assert not out["shards"][i, :, S:].any(), i  # the flat copy returns the zero pad
         assert bytes(got["roots"][i]) == root and np.array_equal(got["branches"][i], br), i
         assert np.array_equal(ref["shards"][i, :, :S], shards) and bytes(ref["roots"][i]) == root, i
+
+
+@pytest.mark.parametrize("n,f,B,pinned", [(128, 42, 44 * 600 + 7, True), (128, 42, 44 * 600 + 7, False),
+                                          (256, 85, 86 * 380, True), (37, 12, 13 * 70, True)])
+def test_validate_keep_then_interpolate_kept(gpu, n, f, B, pinned):
+    """ABI 7: rbc_validate_packed_keep leaves the ECHO rows in a device buffer
+    and rbc_interpolate_batch_kept interpolates from there (the rows cross
+    PCIe once on the drop-in's validate -> interpolate path).  Verdicts and
+    leaves equal rbc_validate_packed_leaves'; values / digests / statuses
+    equal the host-memory interpolate over the rows that validated (leaves
+    reused, and with leaves=None the full rehash), and the input values."""
+    count = 24
+    e = _epoch(n, f, count, B, seed=11 * n + B % 13)
+    ctx = gpu.Context(n, f)
+    k, S = e["k"], e["S"]
+    buf, pitch = _receive_buffer(gpu, e, n, pinned)
+    inst, pos, offs, lens, idx, br, roots = _messages(e, n, pitch)
+    keep = gpu.DeviceBuffer(buf.nbytes)
+    ok, lv = ctx.validate_packed_submit(buf, offs, lens, idx, br, roots, leaves=True, keep=keep).wait()
+    ok0, lv0 = ctx.validate_packed(buf, offs, lens, idx, br, roots, leaves=True)
+    assert np.array_equal(ok, ok0) and np.array_equal(lv[ok], lv0[ok])
+    valid = np.zeros((count, n), np.uint8)
+    valid[inst[ok], pos[ok]] = 1
+    rows = np.zeros((count, n), np.uint64)
+    rows[inst[ok], pos[ok]] = keep.value + offs[ok]
+    leaves = np.zeros((count, n, 32), np.uint8)
+    leaves[inst[ok], pos[ok]] = lv[ok]
+    got = ctx.interpolate_kept_submit(rows, [S] * count, e["roots"], leaves=leaves).wait()
+    rehash = ctx.interpolate_kept_submit(rows, [S] * count, e["roots"]).wait()
+    full = ctx.interpolate_batch(np.array(buf), [S] * count, valid, e["roots"])
+    assert (full["status"] == 0).all()
+    for r in (got, rehash):
+        assert np.array_equal(r["status"], full["status"])
+        assert np.array_equal(r["values"], full["values"]) and np.array_equal(r["digests"], full["digests"])
+    for i in range(count):
+        assert got["values"][i, :B].tobytes() == e["vals"][i].tobytes(), i
+
+
+def test_interpolate_kept_ragged_from_two_keep_buffers(gpu):
+    """Instances of two shard lengths, their rows kept by two validate
+    launches in two device buffers, interpolated in ONE kept batch: each
+    instance's value is k*S_i bytes, zero past it in the value row."""
+    n, f = 128, 42
+    ea = _epoch(n, f, 10, 44 * 500 + 9, seed=31)
+    eb = _epoch(n, f, 10, 44 * 333 + 1, seed=32)
+    ctx = gpu.Context(n, f)
+    k = ea["k"]
+    rows, lens, roots, leaves, want = [], [], [], [], []
+    keeps = []
+    for e in (ea, eb):
+        buf, pitch = _receive_buffer(gpu, e, n, pinned=True)
+        inst, pos, offs, ln, idx, br, rt = _messages(e, n, pitch)
+        keep = gpu.DeviceBuffer(buf.nbytes)
+        keeps.append(keep)
+        ok, lv = ctx.validate_packed_submit(buf, offs, ln, idx, br, rt, leaves=True, keep=keep).wait()
+        r = np.zeros((10, n), np.uint64)
+        r[inst[ok], pos[ok]] = keep.value + offs[ok]
+        l = np.zeros((10, n, 32), np.uint8)
+        l[inst[ok], pos[ok]] = lv[ok]
+        rows.append(r)
+        leaves.append(l)
+        lens += [e["S"]] * 10
+        roots.append(e["roots"])
+        want += [v.tobytes() for v in e["vals"]]
+    got = ctx.interpolate_kept_submit(np.concatenate(rows), lens, np.concatenate(roots),
+                                      leaves=np.concatenate(leaves)).wait()
+    assert (got["status"] == 0).all()
+    for i in range(20):
+        v = got["values"][i]
+        assert v[:len(want[i])].tobytes() == want[i], i
+        assert not v[k * lens[i]:].any(), i
+
+
+@pytest.mark.parametrize("ring_mib", [512, 3])
+def test_batcher_keep_validate_then_interpolate(gpu, ring_mib):
+    """ABI 7, rbc_batcher_set_keep: the unchanged handler sequence (validate
+    every ECHO, then interpolate the ones that validated, through the batcher
+    from many threads) with the shards kept on the device.  With a ring that
+    holds the epoch every interpolate reads kept rows; with a ring of a few
+    arenas launches go unkept and regions are recycled, and those interpolates
+    take the host path.  Every value and digest equals the oracle's, and an
+    interpolate handed copies of the shards (other pointers) takes the host
+    path with the same result."""
+    n, f, B, count = 128, 42, 44 * 900 + 3, 32
+    e = _epoch(n, f, count, B, seed=41 + ring_mib)
+    S = e["S"]
+    ctx = gpu.Context(n, f)
+    bt = gpu.Batcher(ctx, max_batch=8, max_wait_us=500)
+    bt.set_validate(4096, 1 << 20)  # 1 MiB arenas: a 3 MiB ring holds three
+    bt.set_keep(ring_mib << 20)
+    results, errors = [None] * count, []
+
+    def node(i):
+        try:
+            rows, hs = {}, []
+            for j in np.flatnonzero(e["present"][i]):
+                sh = e["shards"][i, j].copy()
+                if e["bad"][i] == j:
+                    sh[S // 2] ^= 0x40
+                rows[j] = sh
+                hs.append((j, bt.submit_validate(e["roots"][i].tobytes(), e["br"][i, j].tobytes(), sh, int(j))))
+            shards = [np.zeros(0, np.uint8)] * n
+            for j, h in hs:
+                ok = bt.wait(h)
+                assert ok == (e["bad"][i] != j)
+                if ok:
+                    shards[j] = rows[j]
+            r = bt.wait(bt.submit_interpolate(e["roots"][i].tobytes(), shards))
+            r2 = bt.wait(bt.submit_interpolate(e["roots"][i].tobytes(), [s.copy() for s in shards]))
+            results[i] = (r, r2, shards)
+        except Exception as x:  # noqa: BLE001
+            errors.append(repr(x))
+
+    th = [threading.Thread(target=node, args=(i,)) for i in range(count)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    st = bt.keep_stats()
+    bt.close()
+    assert not errors, errors[:3]
+    for i, (r, r2, shards) in enumerate(results):
+        assert r == r2 and r["value"][:B] == e["vals"][i].tobytes(), i
+        if i % 8 == 0:
+            valid = np.array([1 if len(s) else 0 for s in shards], np.uint8)
+            rows = np.stack([s if len(s) else np.zeros(S, np.uint8) for s in shards])
+            stc, val, dig = rbc_ref.interpolate(n, f, rows, valid, e["roots"][i].tobytes())
+            assert stc == 0 and val.tobytes() == r["value"] and dig == r["digest"]
+    assert st["host_interps"] >= count  # the copies
+    if ring_mib >= 512:
+        assert st["kept_interps"] == count and st["unkept_launches"] == 0, st
+    else:
+        assert st["kept_launches"] > 0, st

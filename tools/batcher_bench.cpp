@@ -291,7 +291,10 @@ int validate_sweep(int argc, char **argv) {
 // the oracle check in tests/test_gpu_batcher.py.
 // `kinds` (default svi) drops request kinds for a breakdown: s = shard, v =
 // validate, i = interpolate (with v: of the ECHOs that validated).
-//   tools/batcher_bench epoch [instances] [threads] [window] [max_wait_us] [dump|-] [kinds]
+// With keep_mib > 0 (default 6 GiB) a fourth timed pass (after its own warm-up)
+// runs the same plain calls through a batcher with rbc_batcher_set_keep: the
+// validated rows stay on the device and interpolate reads them there.
+//   tools/batcher_bench epoch [instances] [threads] [window] [max_wait_us] [dump|-] [kinds] [keep_mib]
 int epoch(int argc, char **argv) {
     const int n = 128, f = 42, k = n - 2 * f, d = 7, R = n - f;
     const size_t B = 1 << 20, S = (B + k - 1) / k;
@@ -301,6 +304,7 @@ int epoch(int argc, char **argv) {
     const int WAIT = argc > 4 ? atoi(argv[4]) : 200;
     const char *dump = argc > 5 && strcmp(argv[5], "-") ? argv[5] : nullptr;
     const char *kinds = argc > 6 ? argv[6] : "svi";
+    const size_t keep_mib = argc > 7 ? (size_t)atol(argv[7]) : 6144;  // the kept pass's device ring (0: no kept pass)
     const bool ks = strchr(kinds, 's') != nullptr, kv = strchr(kinds, 'v') != nullptr,
                ki = strchr(kinds, 'i') != nullptr;
     rbc_ctx *ctx;
@@ -349,19 +353,19 @@ int epoch(int argc, char **argv) {
     std::vector<size_t> slen(I);
     std::vector<int> ok((size_t)I * R);
     std::vector<uint8_t> leaf((size_t)I * n * 32);
-    std::vector<uint8_t> vout[2] = {std::vector<uint8_t>((size_t)I * k * S), std::vector<uint8_t>((size_t)I * k * S)};
-    std::vector<uint8_t> dig[2] = {std::vector<uint8_t>((size_t)I * 32), std::vector<uint8_t>((size_t)I * 32)};
+    const bool kept = ki && kv && keep_mib > 0;
+    std::vector<uint8_t> vout[3], dig[3];
+    for (int o = 0; o < 3; ++o) {
+        vout[o].resize(o < 2 || kept ? (size_t)I * k * S : 0);
+        dig[o].resize((size_t)I * 32);
+    }
     std::vector<size_t> vlen(I);
     int fails = 0;
-    double secs[2] = {0, 0};
-    uint64_t launches[2] = {0, 0}, reqs[2] = {0, 0};
-    // pass 0: warm-up (verified); pass 1: timed, leaves reused; pass 2: timed, full rehash.  One batcher
-    // for all passes: its pinned arenas and launch buffers are allocated in the warm-up, not timed
-    rbc_batcher *b;
-    CK(rbc_batcher_create(ctx, 64, WAIT, &b));
-    for (int pass = 0; pass < (ki && kv ? 3 : 2); ++pass) {
-        const bool verified = pass < 2 && kv;
-        const int o = pass == 2 ? 1 : 0;
+    double secs[3] = {0, 0, 0};
+    uint64_t launches[3] = {0, 0, 0}, reqs[3] = {0, 0, 0};
+    // One pass of the epoch through batcher b; pass 0 is a warm-up (not reported: the batcher's pinned
+    // arenas and launch buffers are allocated there), `o` the output set
+    auto run_pass = [&](rbc_batcher *b, int pass, bool verified, int o, const char *label) {
         uint64_t nb0 = 0, nr0 = 0;
         rbc_batcher_stats(b, &nb0, &nr0);
         std::atomic<int> next{0}, bad_count{0};
@@ -437,7 +441,7 @@ int epoch(int argc, char **argv) {
         launches[o] -= nb0;
         reqs[o] -= nr0;
         fails += bad_count.load();
-        if (pass == 0) continue;
+        if (pass == 0) return;
         secs[o] = dt;
         // checks: every value, every proposer shard row / root (the verdicts were checked by the clients)
         int vbad = 0, sbad = 0;
@@ -453,14 +457,33 @@ int epoch(int argc, char **argv) {
         printf("{\"phase\": \"epoch\", \"kinds\": \"%s\", \"interpolate\": \"%s\", \"instances\": %d, \"threads\": %d, \"window\": %d, "
                "\"echo_messages\": %d, \"max_wait_us\": %d, \"seconds\": %.4f, \"GBps\": %.3f, \"requests\": %llu, "
                "\"launches\": %llu, \"value_failures\": %d, \"shard_failures\": %d, \"client_failures\": %d}\n",
-               kinds, verified ? "verified (leaves reused)" : "full rehash", I, T, W, I * R, WAIT, dt,
+               kinds, label, I, T, W, I * R, WAIT, dt,
                (double)I * n * S / dt / 1e9, (unsigned long long)reqs[o], (unsigned long long)launches[o], vbad, sbad,
                bad_count.load());
         fflush(stdout);
-    }
+    };
+    // warm-up (verified), then timed with the leaves reused and with the full rehash: one batcher
+    rbc_batcher *b;
+    CK(rbc_batcher_create(ctx, 64, WAIT, &b));
+    for (int pass = 0; pass < (ki && kv ? 3 : 2); ++pass)
+        run_pass(b, pass, pass < 2 && kv, pass == 2 ? 1 : 0,
+                 pass < 2 && kv ? "verified (leaves reused)" : "full rehash");
     rbc_batcher_destroy(b);
-    // the leaf-reusing and the full-rehash interpolate agree bit for bit
-    const int same = !(ki && kv) || (vout[0] == vout[1] && dig[0] == dig[1]);
+    if (kept) {  // ABI 7: the same handler calls with the shards kept on the device (rbc_batcher_set_keep)
+        CK(rbc_batcher_create(ctx, 64, WAIT, &b));
+        CK(rbc_batcher_set_keep(b, keep_mib << 20));
+        run_pass(b, 0, false, 2, "kept");
+        run_pass(b, 1, false, 2, "kept (validated rows stay on the device)");
+        uint64_t kint = 0, hint = 0, kl = 0, ul = 0;
+        rbc_batcher_keep_stats(b, &kint, &hint, &kl, &ul);
+        printf("{\"phase\": \"keep\", \"ring_bytes\": %zu, \"kept_interps\": %llu, \"host_interps\": %llu, "
+               "\"kept_launches\": %llu, \"unkept_launches\": %llu}\n", keep_mib << 20, (unsigned long long)kint,
+               (unsigned long long)hint, (unsigned long long)kl, (unsigned long long)ul);
+        rbc_batcher_destroy(b);
+    }
+    // the leaf-reusing, the full-rehash and the kept interpolate agree bit for bit
+    const int same = !(ki && kv) || (vout[0] == vout[1] && dig[0] == dig[1] &&
+                                     (!kept || (vout[2] == vout[0] && dig[2] == dig[0])));
     fails += !same;
     if (dump) {  // sampled records for the oracle (tests only read this)
         FILE *fp = fopen(dump, "wb");
@@ -475,7 +498,8 @@ int epoch(int argc, char **argv) {
         fclose(fp);
     }
     rbc_ctx_destroy(ctx);
-    printf("{\"phase\": \"check\", \"failures\": %d, \"verified_equals_full\": %s, \"speedup\": %.3f}\n", fails,
-           same ? "true" : "false", secs[0] > 0 ? secs[1] / secs[0] : 0.0);
+    printf("{\"phase\": \"check\", \"failures\": %d, \"verified_equals_full\": %s, \"speedup\": %.3f, "
+           "\"kept_speedup\": %.3f}\n", fails, same ? "true" : "false", secs[0] > 0 ? secs[1] / secs[0] : 0.0,
+           secs[2] > 0 ? secs[0] / secs[2] : 0.0);
     return fails ? 1 : 0;
 }

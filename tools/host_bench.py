@@ -143,7 +143,11 @@ def epoch(ca, n, f, B, instances=1024, sub=128, ring=3, inflight=2, device=0, se
     run the leg together.  GB/s = instances x N x S committed shard bytes
     per second (the bench's unit); PCIe bytes are counted per direction.
     contexts=2: the proposer and the receiver side submit through contexts of
-    their own (own host slots, streams and lock), as a node may."""
+    their own (own host slots, streams and lock), as a node may.
+    A third timed run (ABI 7, "kept") makes the same drop-in calls with the
+    validated rows left on the device: rbc_validate_packed_keep into a device
+    buffer per slot, then rbc_interpolate_batch_kept from it -- the ECHO rows
+    cross PCIe once, as with the fused receive."""
     import time as _t
     ctx = ca.Context(n, f, device=device)
     pctx = ca.Context(n, f, device=device) if contexts == 2 else ctx  # the proposer side's
@@ -199,20 +203,24 @@ def epoch(ca, n, f, B, instances=1024, sub=128, ring=3, inflight=2, device=0, se
     vmask = [np.zeros((sub, n), np.uint8) for _ in range(inflight + 1)]
     roots_out = np.zeros((instances, 32), np.uint8)
     verdict_bad = [0]
+    keeps = [ca.DeviceBuffer(rx[0]["buf"].nbytes, device) for _ in range(inflight + 1)]
 
     def commit(b, slot):
         c = counts[b]
         o = {kk: v[:c] for kk, v in prop[slot].items()}
         return pctx.shard_commit_submit(list(vals[b % ring][:c]), out=o)
 
-    def validate(b, slot):
+    def validate(b, slot, keep=False):
+        """keep: the rows stay in keeps[slot] (free again: the interpolate that read them, of sub-batch
+        b - inflight - 1, was waited before this submission)"""
         R = rx[b % ring]
         m = int(np.searchsorted(R["inst"], counts[b]))
         return ctx.validate_packed_submit(R["buf"], R["offs"][:m], R["lens"][:m], R["idx"][:m], R["br"][:m],
                                           R["mroots"][:m], leaves=True,
-                                          out={"ok": vres[slot]["ok"], "leaves": vres[slot]["leaves"]})
+                                          out={"ok": vres[slot]["ok"], "leaves": vres[slot]["leaves"]},
+                                          keep=keeps[slot] if keep else None)
 
-    def interpolate(b, slot, ok, leaves):
+    def interpolate(b, slot, ok, leaves, kept=False):
         R, c = rx[b % ring], counts[b]
         m = len(ok)
         if not np.array_equal(ok, R["want"][:m]):
@@ -223,6 +231,11 @@ def epoch(ca, n, f, B, instances=1024, sub=128, ring=3, inflight=2, device=0, se
         lv = lvs[slot][:c]
         lv[iv, pv] = leaves[ok]
         lo = b * sub
+        if kept:  # the valid rows where the validate left them on the device
+            rows = np.zeros((c, n), np.uint64)
+            rows[iv, pv] = keeps[slot].value + R["offs"][:m][ok]
+            return ctx.interpolate_kept_submit(rows, [S] * c, R["roots"][:c], leaves=lv, values_out=vout[lo:lo + c],
+                                               digests_out=digests[lo:lo + c], status_out=status[lo:lo + c])
         return ctx.interpolate_submit(R["buf"][:c], [S] * c, valid, R["roots"][:c], values_out=vout[lo:lo + c],
                                       leaves=lv, digests_out=digests[lo:lo + c], status_out=status[lo:lo + c])
 
@@ -243,15 +256,15 @@ def epoch(ca, n, f, B, instances=1024, sub=128, ring=3, inflight=2, device=0, se
                 if "c" in kinds:
                     live["c"].append((b, commit(b, b % (inflight + 1))))
                 if "v" in kinds:
-                    live["v"].append((b, validate(b, b % (inflight + 1))))
+                    live["v"].append((b, validate(b, b % (inflight + 1), keep="k" in kinds)))
                 if "r" in kinds:
                     live["r"].append((b, receive(b, b % (inflight + 1))))
             # the receive side: interpolate a sub-batch once its validate is back
             while live["v"] and (len(live["v"]) > inflight - 1 or b == nsub):
                 bv, tv = live["v"].pop(0)
                 ok, leaves = tv.wait()
-                if "i" in kinds:
-                    live["i"].append((bv, interpolate(bv, bv % (inflight + 1), ok, leaves)))
+                if "i" in kinds or "k" in kinds:
+                    live["i"].append((bv, interpolate(bv, bv % (inflight + 1), ok, leaves, kept="k" in kinds)))
                 if b < nsub:
                     break
             for kd in ("c", "i", "r"):
@@ -292,6 +305,7 @@ def epoch(ca, n, f, B, instances=1024, sub=128, ring=3, inflight=2, device=0, se
 
     el, checks, ok = timed("cvi")  # the drop-in's calls: shard_commit || validate -> interpolate
     el_f, checks_f, ok_f = timed("cr")  # shard_commit || the fused receive
+    el_k, checks_k, ok_k = timed("cvk")  # the drop-in's calls, the validated rows kept on the device
     shard_bytes = instances * n * S
     echo = sum(int((rx[b % ring]["inst"] < counts[b]).sum()) for b in range(nsub))
     h2d = instances * B + 2 * echo * S  # values, ECHO rows for validate, the valid ECHO rows for interpolate
@@ -300,16 +314,20 @@ def epoch(ca, n, f, B, instances=1024, sub=128, ring=3, inflight=2, device=0, se
     out = {"GBps": round(shard_bytes / el / 1e9, 3), "seconds": round(el, 4), "instances": instances,
            "sub_batch": sub, "inflight": inflight, "echo_messages": echo,
            "pcie_GBps": {"h2d": round(h2d / el / 1e9, 2), "d2h": round(d2h / el / 1e9, 2)},
-           "checks": checks, "ok": ok and ok_f,
+           "checks": checks, "ok": ok and ok_f and ok_k,
            "timed_windows_ns": marks,
            "fused": {"GBps": round(shard_bytes / el_f / 1e9, 3), "seconds": round(el_f, 4), "checks": checks_f,
                      "ok": ok_f, "pcie_GBps": {"h2d": round(h2d_f / el_f / 1e9, 2), "d2h": round(d2h / el_f / 1e9, 2)},
                      "path": "rbc_shard_commit || rbc_receive_batch (ECHO rows cross PCIe once, verified on the "
-                             "device, interpolate reusing the leaves)"}}
+                             "device, interpolate reusing the leaves)"},
+           "kept": {"GBps": round(shard_bytes / el_k / 1e9, 3), "seconds": round(el_k, 4), "checks": checks_k,
+                    "ok": ok_k, "pcie_GBps": {"h2d": round(h2d_f / el_k / 1e9, 2), "d2h": round(d2h / el_k / 1e9, 2)},
+                    "path": "rbc_shard_commit || rbc_validate_packed_keep -> rbc_interpolate_batch_kept (the drop-in's "
+                            "calls; the validated ECHO rows stay on the device, crossing PCIe once)"}}
     if phases:  # each side alone over the same epoch: which one binds
         alone = {}
         for name, kinds in (("shard_commit", "c"), ("validate", "v"), ("validate+interpolate", "vi"),
-                            ("receive_fused", "r")):
+                            ("receive_fused", "r"), ("validate+interpolate_kept", "vk")):
             alone[name] = round(shard_bytes / run(kinds) / 1e9, 3)
         out["alone_GBps"] = alone
     out["contexts"] = contexts
