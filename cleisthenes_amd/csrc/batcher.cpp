@@ -335,7 +335,16 @@ struct rbc_batcher {
     void v_finish_run();
 
     void run();
-    std::vector<std::unique_ptr<PinnedSet>> pool;  // worker thread only
+    std::mutex pool_mu;
+    std::vector<std::unique_ptr<PinnedSet>> pool;  // under pool_mu (worker takes, completer returns)
+    // the coalescer's launches in flight, completed in order by their own
+    // thread: the copies out of batch t overlap the copies into batch t+1
+    std::mutex cmu;
+    std::condition_variable c_cv, c_space;
+    std::deque<std::unique_ptr<struct Pending>> cq;
+    bool c_stop = false;
+    std::thread completer;
+    void c_run();
 
     KeepStore keep;                     // rbc_batcher_set_keep
     std::atomic<bool> keep_on{false};
@@ -398,11 +407,14 @@ std::unique_ptr<Pending> rbc_batcher::submit(Kind kind, std::vector<Req> &&batch
     const int count = (int)P->reqs.size();
     P->st.assign(count, RBC_OK);
     std::vector<Req> &b = P->reqs;
-    if (pool.empty()) {
-        P->pin = std::make_unique<PinnedSet>();
-    } else {
-        P->pin = std::move(pool.back());
-        pool.pop_back();
+    {
+        std::lock_guard<std::mutex> lk(pool_mu);
+        if (pool.empty()) {
+            P->pin = std::make_unique<PinnedSet>();
+        } else {
+            P->pin = std::move(pool.back());
+            pool.pop_back();
+        }
     }
     if (kind == K_SHARD) {
         std::vector<const uint8_t *> vals(count);
@@ -521,7 +533,10 @@ void rbc_batcher::finish(Pending &P) {
         for (const Req &r : b)
             for (uint64_t g : r.kgens) keep.release(g);
     }
-    if (P.pin) pool.push_back(std::move(P.pin));  // the launch is complete: its buffers are free
+    if (P.pin) {  // the launch is complete: its buffers are free
+        std::lock_guard<std::mutex> lk(pool_mu);
+        pool.push_back(std::move(P.pin));
+    }
     {  // count the launch before any of its requests reads as done: a client
        // that saw its last request complete then sees it in rbc_batcher_stats
         std::lock_guard<std::mutex> lk(mu);
@@ -539,11 +554,11 @@ void rbc_batcher::finish(Pending &P) {
         if (touched >> sh & 1) shard[sh].cv.notify_all();
 }
 
-// Worker: coalesce, submit asynchronously, and complete launches in order.
-// Up to `depth` launches are in flight, so the host-side staging of batch
-// t+1 overlaps the GPU work (and copies) of batch t.
+// Worker: coalesce and submit asynchronously; the completer thread (c_run)
+// completes launches in order.  Up to depth_max launches are in flight (the
+// context has as many host slots), so the host-side staging of batch t+1
+// overlaps the GPU work of batch t and the copies out of batch t-1.
 void rbc_batcher::run() {
-    std::deque<std::unique_ptr<Pending>> inflight;
     // launches in flight: 4 (41 vs 27 GB/s of shard + commit through the
     // coalescer at 2); the context has as many host slots
     constexpr size_t depth_max = 4;
@@ -560,14 +575,7 @@ void rbc_batcher::run() {
             earliest = std::min(earliest, due);
         }
         if (pick < 0) {
-            if (!inflight.empty()) {  // nothing new is due: complete what runs
-                lk.unlock();
-                finish(*inflight.front());
-                inflight.pop_front();
-                lk.lock();
-                continue;
-            }
-            if (stop) return;
+            if (stop) break;  // every queue drained
             cv_work.wait_until(lk, earliest);
             continue;
         }
@@ -587,12 +595,39 @@ void rbc_batcher::run() {
         std::vector<Req> batch;
         batch.reserve(taken.size());
         for (auto &r : taken) batch.push_back(std::move(r));
-        inflight.push_back(submit((Kind)pick, std::move(batch)));
-        if (inflight.size() >= depth_max) {
-            finish(*inflight.front());
-            inflight.pop_front();
+        {  // a free launch slot first: a submission never waits inside the context for one
+            std::unique_lock<std::mutex> cl(cmu);
+            c_space.wait(cl, [&] { return cq.size() < depth_max; });
         }
+        auto P = submit((Kind)pick, std::move(batch));
+        {
+            std::lock_guard<std::mutex> cl(cmu);
+            cq.push_back(std::move(P));
+        }
+        c_cv.notify_one();
         lk.lock();
+    }
+    lk.unlock();
+    {
+        std::lock_guard<std::mutex> cl(cmu);
+        c_stop = true;  // the completer drains cq and exits
+    }
+    c_cv.notify_one();
+}
+
+// Completer: the oldest launch's rbc_wait and copies out, in submission order
+// (it stays at the head of cq, counted as in flight, until it is done).
+void rbc_batcher::c_run() {
+    std::unique_lock<std::mutex> cl(cmu);
+    for (;;) {
+        c_cv.wait(cl, [&] { return !cq.empty() || c_stop; });
+        if (cq.empty()) return;
+        Pending *P = cq.front().get();
+        cl.unlock();
+        finish(*P);
+        cl.lock();
+        cq.pop_front();
+        c_space.notify_all();
     }
 }
 
@@ -901,6 +936,7 @@ int rbc_batcher_create(rbc_ctx *ctx, int max_batch, int max_wait_us, rbc_batcher
     b->bslot = std::max(d, 1) * 32;
     for (auto &x : b->vb) x = std::make_unique<VBuf>();
     b->worker = std::thread([b] { b->run(); });
+    b->completer = std::thread([b] { b->c_run(); });
     b->v_worker = std::thread([b] { b->v_run(); });
     b->v_completer = std::thread([b] { b->v_finish_run(); });
     *out = b;
@@ -962,6 +998,7 @@ void rbc_batcher_destroy(rbc_batcher *b) {
     }
     b->cv_work.notify_all();
     if (b->worker.joinable()) b->worker.join();
+    if (b->completer.joinable()) b->completer.join();  // the worker's last launches completed
     {
         std::lock_guard<std::mutex> lk(b->vmu);
         b->v_stop = true;  // the lane drains too
