@@ -593,7 +593,7 @@ def host_fed_aggregate(per, n, S):
 
 
 BATCHER_LEVELS = (1024, 8192, 32768, 88064)  # outstanding validates; 88,064 = one C2 epoch (1,024 x 86 ECHOs)
-EPOCH_WINDOW = 8  # instances each of the 16 client threads keeps in flight in the batcher's epoch
+EPOCH_WINDOW = 64  # instances each of the 16 client threads keeps in flight: all 1,024 at once, one goroutine per instance (8: 15-19 GB/s and noisy, profiles/r06z)
 
 
 def batcher_sweep(cpu):

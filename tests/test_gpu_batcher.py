@@ -157,7 +157,7 @@ def test_batcher_epoch_all_three_kinds_with_reused_leaves(tmp_path):
     exe = os.path.join(root, "tools", "batcher_bench")
     assert os.path.exists(exe), "build() makes tools/batcher_bench"
     dump = tmp_path / "epoch.bin"
-    r = subprocess.run([exe, "epoch", "1024", "16", "8", "200", str(dump)], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([exe, "epoch", "1024", "16", "64", "200", str(dump)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
     rows = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     ep = [x for x in rows if x["phase"] == "epoch"]
