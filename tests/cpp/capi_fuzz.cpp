@@ -176,13 +176,54 @@ static void fuzz_validate_packed(Geo &g) {
     std::vector<uint8_t> ok(count + 1), leaves((size_t)count * 32 + 1);
     uint64_t t = 0;
     const bool async = coin(50);
-    const int rc = rbc_validate_packed_leaves(g.ctx, count, arena, arena_bytes, offs.data(), lens.data(), idx.data(),
-                                              br.data(), roots.data(), ok.data(), coin(50) ? leaves.data() : nullptr,
-                                              async ? &t : nullptr);
-    if (count > 0 && bad) EXPECT(rc == RBC_ERR_INVALID_ARG);
+    // ABI 7: a third of the calls move the arena into a device buffer of the caller's (sometimes too small)
+    void *keep = nullptr;
+    const size_t keep_bytes = coin(85) ? arena_bytes + rnd(3) * 64 : rnd(arena_bytes);
+    if (coin(33)) EXPECT(rbc_dev_malloc(0, keep_bytes + 1, &keep) == RBC_OK);
+    const int rc = keep ? rbc_validate_packed_keep(g.ctx, count, arena, arena_bytes, offs.data(), lens.data(),
+                                                   idx.data(), br.data(), roots.data(), ok.data(),
+                                                   coin(50) ? leaves.data() : nullptr, (uint8_t *)keep, keep_bytes,
+                                                   async ? &t : nullptr)
+                        : rbc_validate_packed_leaves(g.ctx, count, arena, arena_bytes, offs.data(), lens.data(),
+                                                     idx.data(), br.data(), roots.data(), ok.data(),
+                                                     coin(50) ? leaves.data() : nullptr, async ? &t : nullptr);
+    if (count > 0 && (bad || (keep && keep_bytes < arena_bytes))) EXPECT(rc == RBC_ERR_INVALID_ARG);
     else EXPECT(rc == RBC_OK);
     if (rc == RBC_OK && async && t) EXPECT(rbc_wait(g.ctx, t) == RBC_OK);
+    if (keep) rbc_dev_free(keep);
     if (pinned) rbc_host_free(arena);
+}
+
+// ABI 7, rbc_interpolate_batch_kept: rows by device address (NULL = absent)
+// inside one device buffer, ragged lengths, value pitches too small now and
+// then, with and without leaves.
+static void fuzz_interpolate_kept(Geo &g) {
+    const int count = (int)rnd(5);
+    std::vector<size_t> sl(count + 1);
+    size_t Smax = 1;
+    for (int i = 0; i < count; ++i) Smax = std::max(Smax, sl[i] = 1 + rnd(300));
+    const size_t dev_bytes = 64 + (size_t)g.n * Smax;
+    void *dev = nullptr;
+    EXPECT(rbc_dev_malloc(0, dev_bytes, &dev) == RBC_OK);
+    std::vector<uint8_t> fill = bytes(dev_bytes);
+    EXPECT(rbc_memcpy_h2d(dev, fill.data(), dev_bytes) == RBC_OK);
+    std::vector<const uint8_t *> rows((size_t)count * g.n + 1, nullptr);
+    for (int i = 0; i < count; ++i)
+        for (int j = 0; j < g.n; ++j)
+            if (coin(70)) rows[(size_t)i * g.n + j] = (const uint8_t *)dev + rnd(dev_bytes - sl[i] + 1);
+    std::vector<uint8_t> roots = bytes((size_t)count * 32 + 1), leaves = bytes((size_t)count * g.n * 32 + 1);
+    const size_t vpitch = coin(85) ? (size_t)g.k * Smax + rnd(40) : rnd((size_t)g.k * Smax);
+    std::vector<uint8_t> values((size_t)count * vpitch + 1), digests((size_t)count * 32 + 1);
+    std::vector<int32_t> status(count + 1);
+    uint64_t t = 0;
+    const bool async = coin(50);
+    const int rc = rbc_interpolate_batch_kept(g.ctx, count, rows.data(), sl.data(), coin(50) ? leaves.data() : nullptr,
+                                              roots.data(), values.data(), vpitch, coin(30) ? nullptr : digests.data(),
+                                              status.data(), async ? &t : nullptr);
+    if (count > 0 && vpitch < (size_t)g.k * Smax) EXPECT(rc == RBC_ERR_INVALID_ARG);
+    else EXPECT(rc == RBC_OK);
+    if (rc == RBC_OK && async && t) EXPECT(rbc_wait(g.ctx, t) == RBC_OK);
+    rbc_dev_free(dev);
 }
 
 static void fuzz_single_calls(Geo &g) {
@@ -390,7 +431,7 @@ int main(int argc, char **argv) {
                 fuzz_rs(encs[e], kp[e].first, kp[e].second);
                 break;
             }
-            case 5: coin(50) ? fuzz_acs() : fuzz_validate_packed(g); break;
+            case 5: coin(50) ? fuzz_acs() : coin(50) ? fuzz_validate_packed(g) : fuzz_interpolate_kept(g); break;
             default: fuzz_receive_step(g); break;
         }
         EXPECT(rbc_strerror((int)rnd(40) - 30) != nullptr);
