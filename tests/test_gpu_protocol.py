@@ -23,11 +23,13 @@ class Net:
     """Nodes[(proposer, i)] for the given proposers; `tamper(p, src, dst, msg)`
     may rewrite or drop (None) any message in flight."""
 
-    def __init__(self, ca, n, f, proposers, tamper=None, max_batch=1024, max_wait_us=5000):
+    def __init__(self, ca, n, f, proposers, tamper=None, max_batch=1024, max_wait_us=5000, keep=0):
         from cleisthenes_amd import protocol
         self.protocol = protocol
         self.ctx = ca.Context(n, f)
         self.bt = ca.Batcher(self.ctx, max_batch=max_batch, max_wait_us=max_wait_us)
+        if keep:  # ABI 7: validated ECHO rows stay on the device for the interpolates
+            self.bt.set_keep(keep)
         self.n, self.f = n, f
         self.nodes = {(p, i): protocol.Node(self.bt, n, f, i, p) for p in proposers for i in range(n)}
         self.tamper = tamper
@@ -94,10 +96,13 @@ def test_honest_network_delivers(ca, n, f, B):
         net.close()
 
 
-def test_all_proposers_concurrently_share_launches(ca):
-    """An ACS round: N proposers x N nodes = 256 instances, one batcher."""
+@pytest.mark.parametrize("keep", [0, 64 << 20])
+def test_all_proposers_concurrently_share_launches(ca, keep):
+    """An ACS round: N proposers x N nodes = 256 instances, one batcher; with
+    keep, the batcher keeps validated ECHO rows on the device (ABI 7) and the
+    round must deliver the same values."""
     n, f = 16, 5
-    net = Net(ca, n, f, proposers=list(range(n)))
+    net = Net(ca, n, f, proposers=list(range(n)), keep=keep)
     try:
         vals = {p: rand(4096 + 17 * p, 100 + p) for p in range(n)}
         for p in range(n):
