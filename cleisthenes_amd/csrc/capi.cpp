@@ -1937,7 +1937,7 @@ static int validate_packed(rbc_ctx *c, int count, const uint8_t *arena, size_t a
     RBC_HIP(hipMemcpyAsync(s.d_slens.p, lens, (size_t)count * 4, hipMemcpyHostToDevice, st));
     if (zc)
         RBC_HIP(rbc_launch_gather_msgs(zc, s.d_offs.as<uint64_t>(), s.d_slens.as<uint32_t>(), (uint32_t)count,
-                                       d_arena, st));
+                                       d_arena, (uint32_t)std::min<size_t>(named / count, 0xffffffffu), st));
     else
         RBC_HIP(hipMemcpyAsync(d_arena, arena, arena_bytes, hipMemcpyHostToDevice, st));
     RBC_HIP(hipMemcpyAsync(s.d_idx.p, idx, (size_t)count, hipMemcpyHostToDevice, st));

@@ -249,7 +249,7 @@ hipError_t rbc_launch_gather_present(const uint8_t *host, uint64_t hpitch, uint3
 // the messages of a pinned validate arena -> the same offsets of a device arena
 // (zero-copy reads of bytes [offs[i], offs[i] + lens[i]) only; the rest untouched)
 hipError_t rbc_launch_gather_msgs(const uint8_t *host, const uint64_t *offs, const uint32_t *lens, uint32_t count,
-                                  uint8_t *dev, hipStream_t st);
+                                  uint8_t *dev, uint32_t avg_len, hipStream_t st);
 // pinned host values (device array of their addresses) -> device value rows (zero-copy reads)
 // rows from device addresses (0 = absent), lens per instance of n rows
 hipError_t rbc_launch_gather_ptrs(const uint64_t *ptrs, const uint32_t *lens, uint32_t n, uint8_t *dev,

@@ -1809,6 +1809,19 @@ __global__ __launch_bounds__(256) void gather_ptrs_kernel(const uint64_t *ptrs, 
 // ============================================================================
 // launchers
 // ============================================================================
+// Waves in flight for a zero-copy gather of rows of about S bytes: each wave
+// moves one row per round trip over PCIe, so 256 waves keep the read queue
+// full for long rows (C2: 23.8 KB); short rows (C4: 763 B) need more waves for
+// the same bytes in flight.
+#ifndef RBC_GATHER_SHORT_ROWS
+#define RBC_GATHER_SHORT_ROWS 0
+#endif
+static uint32_t gather_blocks(uint32_t rows, uint32_t S) {
+    uint32_t cap = 64;
+    if (RBC_GATHER_SHORT_ROWS && S < 4096) cap = 64 * std::min<uint32_t>(16u, (4096u + S - 1) / std::max(S, 1u));
+    return std::min((rows + 3) / 4, cap);
+}
+
 hipError_t rbc_launch_gather_ptrs(const uint64_t *ptrs, const uint32_t *lens, uint32_t n, uint8_t *dev,
                                   uint32_t dpitch, uint32_t rows, hipStream_t st) {
     if (rows == 0) return hipSuccess;
@@ -1826,9 +1839,9 @@ hipError_t rbc_launch_gather_values(const uint64_t *ptrs, const uint32_t *lens, 
     return hipGetLastError();
 }
 hipError_t rbc_launch_gather_msgs(const uint8_t *host, const uint64_t *offs, const uint32_t *lens, uint32_t count,
-                                  uint8_t *dev, hipStream_t st) {
+                                  uint8_t *dev, uint32_t avg_len, hipStream_t st) {
     if (count == 0) return hipSuccess;
-    const uint32_t blocks = std::min((count + 3) / 4, 64u);  // as gather_present: 256 messages' reads in flight
+    const uint32_t blocks = gather_blocks(count, avg_len);  // as gather_present
     hipLaunchKernelGGL(gather_msgs_kernel, dim3(blocks), dim3(256), 0, st, host, offs, lens, count, dev);
     return hipGetLastError();
 }
@@ -1863,7 +1876,7 @@ hipError_t rbc_launch_gather_present(const uint8_t *host, uint64_t hpitch, uint3
                                      uint8_t *dev, uint32_t dpitch, uint32_t rows, hipStream_t st) {
     if (rows == 0) return hipSuccess;
     if (dpitch % 16 || S > dpitch) return hipErrorInvalidValue;
-    const uint32_t blocks = std::min((rows + 3) / 4, 64u);  // 256 rows' reads in flight, one wave each
+    const uint32_t blocks = gather_blocks(rows, S);  // one wave per row
     hipLaunchKernelGGL(gather_present_kernel, dim3(blocks), dim3(256), 0, st, host, hpitch, S, present, dev, dpitch,
                        rows);
     return hipGetLastError();

@@ -321,7 +321,7 @@ hipError_t rbc_launch_gather_values(const uint64_t *ptrs, const uint32_t *lens, 
     return hipSuccess;
 }
 hipError_t rbc_launch_gather_msgs(const uint8_t *host, const uint64_t *offs, const uint32_t *lens, uint32_t count,
-                                  uint8_t *dev, hipStream_t) {
+                                  uint8_t *dev, uint32_t, hipStream_t) {
     for (uint32_t m = 0; m < count; ++m) {  // the kernel stores whole 16-B chunks up to round_up(len, 16)
         touch(dev + offs[m], (lens[m] + 15) / 16 * 16);
         memcpy(dev + offs[m], host + offs[m], lens[m]);
