@@ -130,7 +130,7 @@ struct Ws {
 // buffers at completion (rbc_wait / rbc_poll / slot reuse).
 struct Slot {
     DevBuf d_values, d_shards, d_leaves, d_roots, d_branches, d_valid, d_status, d_digests, d_lens, d_slens, d_idx,
-        d_offs, d_present;
+        d_offs, d_present, d_pack;
     DevBuf h_in{nullptr, 0, true}, h_out{nullptr, 0, true};
     Ws ws;
     hipStream_t stream = nullptr;
@@ -153,7 +153,7 @@ struct Slot {
     int d2h_rc = 0;
     void release() {
         for (DevBuf *b : {&d_values, &d_shards, &d_leaves, &d_roots, &d_branches, &d_valid, &d_status, &d_digests,
-                          &d_lens, &d_slens, &d_idx, &d_offs, &d_present, &h_in, &h_out})
+                          &d_lens, &d_slens, &d_idx, &d_offs, &d_present, &d_pack, &h_in, &h_out})
             b->release();
         ws.release();
         if (stream) (void)hipStreamDestroy(stream);
@@ -2150,12 +2150,21 @@ static int host_receive(rbc_ctx *c, int count, const uint8_t *shards, size_t sha
     if (rc) return rc;
     uint8_t *o_val = s.h_out.as<uint8_t>(), *o_dig = o_val + out_stage;
     int32_t *o_st = reinterpret_cast<int32_t *>(o_dig + (size_t)count * 32);
-    void *d_val = s.d_values.p, *d_dig = s.d_digests.p, *d_st = s.d_status.p, *d_vd = s.d_valid.p;
+    // pinned values at another pitch: the rows repacked to it on the device, then ONE copy
+    // (a pitched D2H runs as one DMA per row: 2,048 of them per C4 sub-batch, ~11 us each)
+    const uint64_t packed = (uint64_t)(count - 1) * value_pitch + (uint64_t)k * Smax;
+    const bool pack = out_direct && value_pitch != vpitch && (uint64_t)count * value_pitch < 0xffffffffULL;
+    if (pack) {
+        RBC_HIP(s.d_pack.ensure((size_t)count * value_pitch));
+        RBC_HIP(rbc_launch_pack_rows(s.d_values.as<uint8_t>(), (uint32_t)vpitch, s.d_pack.as<uint8_t>(),
+                                     (uint32_t)value_pitch, (uint32_t)(k * Smax), (uint32_t)count, st));
+    }
+    void *d_val = pack ? s.d_pack.p : s.d_values.p, *d_dig = s.d_digests.p, *d_st = s.d_status.p,
+         *d_vd = s.d_valid.p;
     auto d2h = [=](hipStream_t cs) -> int {
         if (valid_out) RBC_HIP(hipMemcpyAsync(valid_out, d_vd, (size_t)count * n, hipMemcpyDeviceToHost, cs));
-        if (out_direct && value_pitch == vpitch)  // one contiguous DMA (a 2-D copy runs as a blit kernel)
-            RBC_HIP(hipMemcpyAsync(values_out, d_val, (size_t)(count - 1) * vpitch + (size_t)k * Smax,
-                                   hipMemcpyDeviceToHost, cs));
+        if (out_direct && (value_pitch == vpitch || pack))  // one contiguous DMA
+            RBC_HIP(hipMemcpyAsync(values_out, d_val, (size_t)packed, hipMemcpyDeviceToHost, cs));
         else if (out_direct)
             RBC_HIP(hipMemcpy2DAsync(values_out, value_pitch, d_val, vpitch, (size_t)k * Smax, (size_t)count,
                                      hipMemcpyDeviceToHost, cs));

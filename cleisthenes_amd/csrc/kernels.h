@@ -251,6 +251,9 @@ hipError_t rbc_launch_gather_present(const uint8_t *host, uint64_t hpitch, uint3
 hipError_t rbc_launch_gather_msgs(const uint8_t *host, const uint64_t *offs, const uint32_t *lens, uint32_t count,
                                   uint8_t *dev, uint32_t avg_len, hipStream_t st);
 // pinned host values (device array of their addresses) -> device value rows (zero-copy reads)
+// rows [0, width) of src (src_pitch) into dst at dst_pitch, zeros to dst_pitch
+hipError_t rbc_launch_pack_rows(const uint8_t *src, uint32_t src_pitch, uint8_t *dst, uint32_t dst_pitch,
+                                uint32_t width, uint32_t rows, hipStream_t st);
 // rows from device addresses (0 = absent), lens per instance of n rows
 hipError_t rbc_launch_gather_ptrs(const uint64_t *ptrs, const uint32_t *lens, uint32_t n, uint8_t *dev,
                                   uint32_t dpitch, uint32_t rows, hipStream_t st);

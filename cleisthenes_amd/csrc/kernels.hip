@@ -1812,14 +1812,44 @@ __global__ __launch_bounds__(256) void gather_ptrs_kernel(const uint64_t *ptrs, 
 // Waves in flight for a zero-copy gather of rows of about S bytes: each wave
 // moves one row per round trip over PCIe, so 256 waves keep the read queue
 // full for long rows (C2: 23.8 KB); short rows (C4: 763 B) need more waves for
-// the same bytes in flight.
-#ifndef RBC_GATHER_SHORT_ROWS
-#define RBC_GATHER_SHORT_ROWS 0
-#endif
+// the same bytes in flight (C4 host-fed validate 30 -> 54 GB/s, fused receive
+// 13 -> 16, profiles/r06ac/).
 static uint32_t gather_blocks(uint32_t rows, uint32_t S) {
-    uint32_t cap = 64;
-    if (RBC_GATHER_SHORT_ROWS && S < 4096) cap = 64 * std::min<uint32_t>(16u, (4096u + S - 1) / std::max(S, 1u));
+    const uint32_t cap = S < 4096 ? 64 * std::min<uint32_t>(16u, (4096u + S - 1) / std::max(S, 1u)) : 64u;
     return std::min((rows + 3) / 4, cap);
+}
+
+// Values into the caller's row pitch on the device (host batch API): dst row
+// r = src row r [0, width), zeros up to dst_pitch; one thread per dst dword,
+// byte loads (dst rows need not be aligned).
+__global__ __launch_bounds__(256) void pack_rows_kernel(const uint8_t *src, uint32_t src_pitch, uint8_t *dst,
+                                                        uint32_t dst_pitch, uint32_t width, uint32_t total) {
+    for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < (total + 3) / 4; w += gridDim.x * blockDim.x) {
+        uint32_t v = 0;
+        for (uint32_t b = 0; b < 4; ++b) {
+            const uint32_t o = 4 * w + b;
+            if (o >= total) break;
+            const uint32_t r = o / dst_pitch, c = o - r * dst_pitch;
+            if (c < width) v |= (uint32_t)src[(size_t)r * src_pitch + c] << (8 * b);
+        }
+        if (4 * w + 4 <= total) {
+            reinterpret_cast<uint32_t *>(dst)[w] = v;
+        } else {
+            for (uint32_t b = 0; 4 * w + b < total; ++b) dst[4 * w + b] = (uint8_t)(v >> (8 * b));
+        }
+    }
+}
+
+hipError_t rbc_launch_pack_rows(const uint8_t *src, uint32_t src_pitch, uint8_t *dst, uint32_t dst_pitch,
+                                uint32_t width, uint32_t rows, hipStream_t st) {
+    const uint64_t total = (uint64_t)dst_pitch * rows;
+    if (rows == 0 || total == 0) return hipSuccess;
+    if (total >= 0xffffffffULL || width > dst_pitch || width > src_pitch || ((uintptr_t)dst % 4))
+        return hipErrorInvalidValue;
+    const uint32_t words = (uint32_t)((total + 3) / 4);
+    hipLaunchKernelGGL(pack_rows_kernel, dim3(std::min<uint32_t>((words + 255) / 256, 8192u)), dim3(256), 0, st, src,
+                       src_pitch, dst, dst_pitch, width, (uint32_t)total);
+    return hipGetLastError();
 }
 
 hipError_t rbc_launch_gather_ptrs(const uint64_t *ptrs, const uint32_t *lens, uint32_t n, uint8_t *dev,

@@ -332,7 +332,9 @@ int rbc_validate_packed_keep(rbc_ctx *ctx, int count, const uint8_t *arena, size
 /* interpolate() for `count` instances: shards [count][n][shard_pitch] with
  * present [count][n] (0 = missing, the Go `len == 0`), shard_lens [count],
  * roots [count][32] -> values_out [count][value_pitch] (k*S_i bytes),
- * digests_out [count][32] (nullable), status_out [count]. */
+ * digests_out [count][32] (nullable), status_out [count].  Pinned values_out
+ * comes back in one copy: every row but the last whole, bytes [k*S_i,
+ * value_pitch) as zero. */
 int rbc_interpolate_batch(rbc_ctx *ctx, int count, const uint8_t *shards, size_t shard_pitch,
                           const size_t *shard_lens, const uint8_t *present, const uint8_t *roots,
                           uint8_t *values_out, size_t value_pitch, uint8_t *digests_out, int32_t *status_out,

@@ -328,6 +328,15 @@ hipError_t rbc_launch_gather_msgs(const uint8_t *host, const uint64_t *offs, con
     }
     return hipSuccess;
 }
+hipError_t rbc_launch_pack_rows(const uint8_t *src, uint32_t src_pitch, uint8_t *dst, uint32_t dst_pitch,
+                                uint32_t width, uint32_t rows, hipStream_t) {
+    for (uint32_t r = 0; r < rows; ++r) {  // whole dst rows: zeros past width
+        touch(dst + (size_t)r * dst_pitch, dst_pitch);
+        memset(dst + (size_t)r * dst_pitch, 0, dst_pitch);
+        memcpy(dst + (size_t)r * dst_pitch, src + (size_t)r * src_pitch, width);
+    }
+    return hipSuccess;
+}
 hipError_t rbc_launch_gather_ptrs(const uint64_t *ptrs, const uint32_t *lens, uint32_t n, uint8_t *dev,
                                   uint32_t dpitch, uint32_t rows, hipStream_t) {
     for (uint32_t r = 0; r < rows; ++r) {  // whole rows: zeros past lens[r / n] and for absent rows

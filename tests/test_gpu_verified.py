@@ -391,3 +391,39 @@ def test_batcher_keep_validate_then_interpolate(gpu, ring_mib):
         assert st["kept_interps"] == count and st["unkept_launches"] == 0, st
     else:
         assert st["kept_launches"] > 0, st
+
+
+def test_interpolate_pinned_values_at_an_odd_pitch(gpu):
+    """Pinned values_out at a pitch the device rows do not use (k*Smax + 5,
+    not a multiple of 16): the rows are repacked on the device and come back
+    in one copy.  Ragged instances (two shard lengths): every row holds its
+    value then zeros up to the pitch (the last row up to k*S_i), equal to the
+    pageable (staged) result."""
+    n, f = 128, 42
+    ea = _epoch(n, f, 9, 44 * 400 + 3, seed=51)
+    eb = _epoch(n, f, 9, 44 * 257 + 11, seed=52)
+    ctx = gpu.Context(n, f)
+    k = ea["k"]
+    Sa, Sb = ea["S"], eb["S"]
+    Smax = max(Sa, Sb)
+    pitch = (Smax + 63) // 64 * 64
+    count = 18
+    shards = np.zeros((count, n, pitch), np.uint8)
+    shards[:9, :, :Sa] = ea["shards"]
+    shards[9:, :, :Sb] = eb["shards"]
+    present = np.concatenate([ea["present"], eb["present"]])
+    roots = np.concatenate([ea["roots"], eb["roots"]])
+    lens = [Sa] * 9 + [Sb] * 9
+    vp = k * Smax + 5
+    v_pin = gpu.pinned_empty((count, vp))
+    v_pin[:] = 0xA5
+    got = ctx.interpolate_submit(shards, lens, present, roots, values_out=v_pin).wait()
+    ref = ctx.interpolate_batch(shards, lens, present, roots)
+    assert (got["status"] == 0).all() and np.array_equal(got["digests"], ref["digests"])
+    vals = [v.tobytes() for v in ea["vals"]] + [v.tobytes() for v in eb["vals"]]
+    for i in range(count):
+        kS = k * lens[i]
+        assert v_pin[i, :len(vals[i])].tobytes() == vals[i], i
+        assert np.array_equal(v_pin[i, :kS], ref["values"][i, :kS]), i
+        end = vp if i < count - 1 else k * Smax
+        assert not v_pin[i, kS:end].any(), i
