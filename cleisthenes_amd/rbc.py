@@ -489,7 +489,7 @@ class Context:
         vp = self.k * Smax
         if values_out is not None:
             values = values_out
-            assert values.shape == (count, max(vp, 1)) and values.dtype == np.uint8
+            assert values.shape[0] == count and values.shape[1] >= max(vp, 1) and values.dtype == np.uint8
         else:
             values = np.zeros((count, max(vp, 1)), dtype=np.uint8)
         digests = np.zeros((count, 32), dtype=np.uint8) if digests_out is None else digests_out
