@@ -311,16 +311,16 @@ def epoch(ca, n, f, B, instances=1024, sub=128, ring=3, inflight=2, device=0, se
     h2d = instances * B + 2 * echo * S  # values, ECHO rows for validate, the valid ECHO rows for interpolate
     d2h = shard_bytes + instances * n * d * 32 + instances * k * S
     h2d_f = instances * B + echo * S  # the fused receive moves the ECHO rows once
-    out = {"GBps": round(shard_bytes / el / 1e9, 3), "seconds": round(el, 4), "instances": instances,
+    out = {"GBps": round(shard_bytes / el / 1e9, 3), "seconds": round(el, 6), "instances": instances,
            "sub_batch": sub, "inflight": inflight, "echo_messages": echo,
            "pcie_GBps": {"h2d": round(h2d / el / 1e9, 2), "d2h": round(d2h / el / 1e9, 2)},
            "checks": checks, "ok": ok and ok_f and ok_k,
            "timed_windows_ns": marks,
-           "fused": {"GBps": round(shard_bytes / el_f / 1e9, 3), "seconds": round(el_f, 4), "checks": checks_f,
+           "fused": {"GBps": round(shard_bytes / el_f / 1e9, 3), "seconds": round(el_f, 6), "checks": checks_f,
                      "ok": ok_f, "pcie_GBps": {"h2d": round(h2d_f / el_f / 1e9, 2), "d2h": round(d2h / el_f / 1e9, 2)},
                      "path": "rbc_shard_commit || rbc_receive_batch (ECHO rows cross PCIe once, verified on the "
                              "device, interpolate reusing the leaves)"},
-           "kept": {"GBps": round(shard_bytes / el_k / 1e9, 3), "seconds": round(el_k, 4), "checks": checks_k,
+           "kept": {"GBps": round(shard_bytes / el_k / 1e9, 3), "seconds": round(el_k, 6), "checks": checks_k,
                     "ok": ok_k, "pcie_GBps": {"h2d": round(h2d_f / el_k / 1e9, 2), "d2h": round(d2h / el_k / 1e9, 2)},
                     "path": "rbc_shard_commit || rbc_validate_packed_keep -> rbc_interpolate_batch_kept (the drop-in's "
                             "calls; the validated ECHO rows stay on the device, crossing PCIe once)"}}
