@@ -578,6 +578,14 @@ def run(args, world, rank, local_rank, wd, out):
     return 0
 
 
+def _run_key(name):
+    """Profile file names carry their run, r<round><letters>: runs of a round
+    are lettered a..z, then aa, ab, ... -- so r06ae is newer than r06h."""
+    import re
+    m = re.search(r"_r(\d+)([a-z]*)", name)
+    return (int(m.group(1)), len(m.group(2)), m.group(2), name) if m else (-1, 0, "", name)
+
+
 def host_fed_aggregate(per, n, S):
     """The ranks' host-fed epochs (tools/host_bench.epoch results, rank
     order) -> the job's figure: every rank's committed shard bytes over the
@@ -742,7 +750,7 @@ def report(args, ctx, I, n, k, d, S, present_h, corrupt_h, stage_ms, iso, elapse
     want_form = "joined" if args.join else "row view"
     cands = []
     for cand in sorted((x for x in os.listdir(os.path.join(ROOT, "profiles")) if x.startswith("pmc_traffic_r")),
-                       reverse=True):
+                       key=_run_key, reverse=True):
         try:
             c = json.load(open(os.path.join(ROOT, "profiles", cand)))
         except (OSError, ValueError):
@@ -758,7 +766,7 @@ def report(args, ctx, I, n, k, d, S, present_h, corrupt_h, stage_ms, iso, elapse
     # the loaded clock per kernel, each kernel alone (serial schedule; tools/clock_summary.py)
     clk, clk_path = {}, None
     for cand in sorted((x for x in os.listdir(os.path.join(ROOT, "profiles")) if x.startswith("valu_clock_r")),
-                       reverse=True):
+                       key=_run_key, reverse=True):
         try:
             c = json.load(open(os.path.join(ROOT, "profiles", cand)))
         except (OSError, ValueError):
