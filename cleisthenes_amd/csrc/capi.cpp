@@ -1500,6 +1500,23 @@ static bool host_pinned(const void *p, size_t bytes) {
     return true;
 }
 
+// [p, p + bytes) readable by a kernel: device memory, or pinned host memory
+// mapped at the same address (both ends checked: one attribute query each)
+static bool device_readable(const void *p, size_t bytes) {
+    if (!p) return false;
+    for (const void *q : {p, (const void *)((const uint8_t *)p + (bytes ? bytes - 1 : 0))}) {
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        if (a.type == hipMemoryTypeDevice) continue;
+        if (a.type == hipMemoryTypeHost && a.devicePointer == q) continue;
+        return false;
+    }
+    return true;
+}
+
 // The device address of pinned caller memory when it is the host address itself
 // (hipHostMalloc / rbc_host_alloc under unified addressing), else NULL: a
 // kernel may then read it directly over PCIe.
@@ -1889,7 +1906,8 @@ int rbc_validate_packed_keep(rbc_ctx *c, int count, const uint8_t *arena, size_t
                              const uint32_t *lens, const uint8_t *idx, const uint8_t *branches, const uint8_t *roots,
                              uint8_t *ok_out, uint8_t *leaves_out, uint8_t *keep_dev, size_t keep_bytes,
                              uint64_t *ticket) {
-    if (count > 0 && (!keep_dev || keep_bytes < arena_bytes)) return RBC_ERR_INVALID_ARG;
+    if (count > 0 && (!keep_dev || keep_bytes < arena_bytes || !device_readable(keep_dev, arena_bytes)))
+        return RBC_ERR_INVALID_ARG;
     return validate_packed(c, count, arena, arena_bytes, offs, lens, idx, branches, roots, ok_out, leaves_out,
                            keep_dev, keep_bytes, ticket);
 }
@@ -2003,7 +2021,17 @@ int rbc_interpolate_batch_verified(rbc_ctx *c, int count, const uint8_t *shards,
 int rbc_interpolate_batch_kept(rbc_ctx *c, int count, const uint8_t *const *rows, const size_t *shard_lens,
                                const uint8_t *leaves, const uint8_t *roots, uint8_t *values_out, size_t value_pitch,
                                uint8_t *digests_out, int32_t *status_out, uint64_t *ticket) {
-    if (count > 0 && !rows) return RBC_ERR_INVALID_ARG;
+    if (!c || (count > 0 && (!rows || !shard_lens))) return RBC_ERR_INVALID_ARG;
+    // every instance's first and last row must be memory a kernel can read (a pageable host
+    // address would fault the gather): one attribute query at each end
+    for (int i = 0; i < count; ++i) {
+        const uint8_t *const *r = rows + (size_t)i * c->n;
+        int lo = 0, hi = c->n - 1;
+        while (lo < c->n && !r[lo]) ++lo;
+        while (hi >= 0 && !r[hi]) --hi;
+        if (lo <= hi && (!device_readable(r[lo], shard_lens[i]) || !device_readable(r[hi], shard_lens[i])))
+            return RBC_ERR_INVALID_ARG;
+    }
     return host_receive(c, count, nullptr, 0, shard_lens, nullptr, leaves, nullptr, roots, nullptr, values_out,
                         value_pitch, digests_out, status_out, ticket, rows);
 }

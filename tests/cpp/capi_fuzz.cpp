@@ -217,10 +217,22 @@ static void fuzz_interpolate_kept(Geo &g) {
     std::vector<int32_t> status(count + 1);
     uint64_t t = 0;
     const bool async = coin(50);
+    // now and then one row in pageable host memory: refused before anything is launched
+    std::vector<uint8_t> pageable_row = bytes(320);
+    bool stray = false;
+    if (count > 0 && coin(15)) {
+        const int i = (int)rnd(count);
+        int j = 0;
+        while (j < g.n && !rows[(size_t)i * g.n + j]) ++j;
+        if (j < g.n) {
+            rows[(size_t)i * g.n + j] = pageable_row.data();
+            stray = true;
+        }
+    }
     const int rc = rbc_interpolate_batch_kept(g.ctx, count, rows.data(), sl.data(), coin(50) ? leaves.data() : nullptr,
                                               roots.data(), values.data(), vpitch, coin(30) ? nullptr : digests.data(),
                                               status.data(), async ? &t : nullptr);
-    if (count > 0 && vpitch < (size_t)g.k * Smax) EXPECT(rc == RBC_ERR_INVALID_ARG);
+    if (count > 0 && (vpitch < (size_t)g.k * Smax || stray)) EXPECT(rc == RBC_ERR_INVALID_ARG);
     else EXPECT(rc == RBC_OK);
     if (rc == RBC_OK && async && t) EXPECT(rbc_wait(g.ctx, t) == RBC_OK);
     rbc_dev_free(dev);

@@ -27,6 +27,7 @@
 namespace {
 std::mutex mu;
 std::map<const char *, size_t> pinned;  // hipHostMalloc'd ranges
+std::map<const char *, size_t> devmem;  // hipMalloc'd ranges (reported as device memory)
 struct Dummy {
     int x = 0;
 };
@@ -69,9 +70,16 @@ hipError_t hipDeviceGetStreamPriorityRange(int *least, int *greatest) {
 }
 hipError_t hipMalloc(void **p, size_t bytes) {
     *p = calloc(1, bytes ? bytes : 1);
-    return *p ? hipSuccess : hipErrorOutOfMemory;
+    if (!*p) return hipErrorOutOfMemory;
+    std::lock_guard<std::mutex> lk(mu);
+    devmem[(const char *)*p] = bytes ? bytes : 1;
+    return hipSuccess;
 }
 hipError_t hipFree(void *p) {
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        devmem.erase((const char *)p);
+    }
     free(p);
     return hipSuccess;
 }
@@ -92,15 +100,25 @@ hipError_t hipHostFree(void *p) {
 }
 hipError_t hipPointerGetAttributes(hipPointerAttribute_t *a, const void *p) {
     std::lock_guard<std::mutex> lk(mu);
-    auto it = pinned.upper_bound((const char *)p);
-    if (it == pinned.begin()) return hipErrorInvalidValue;
-    --it;
-    if ((const char *)p >= it->first + it->second) return hipErrorInvalidValue;
+    auto in = [p](std::map<const char *, size_t> &m) {
+        auto it = m.upper_bound((const char *)p);
+        if (it == m.begin()) return false;
+        --it;
+        return (const char *)p < it->first + it->second;
+    };
     memset(a, 0, sizeof *a);
-    a->type = hipMemoryTypeHost;
-    a->devicePointer = const_cast<void *>(p);
-    a->hostPointer = const_cast<void *>(p);
-    return hipSuccess;
+    if (in(pinned)) {
+        a->type = hipMemoryTypeHost;
+        a->devicePointer = const_cast<void *>(p);
+        a->hostPointer = const_cast<void *>(p);
+        return hipSuccess;
+    }
+    if (in(devmem)) {  // hipMalloc'd "device" memory
+        a->type = hipMemoryTypeDevice;
+        a->devicePointer = const_cast<void *>(p);
+        return hipSuccess;
+    }
+    return hipErrorInvalidValue;
 }
 hipError_t hipMemcpy(void *d, const void *s, size_t n, hipMemcpyKind) {
     if (n) memcpy(d, s, n);
