@@ -7,4 +7,8 @@ R=$(pwd)
 python -c "import json; d=json.load(open('$O/host_c4_prof.json')); print('drop-in', d['GBps'], 'kept', d['kept']['GBps'], 'fused', d['fused']['GBps'], d['alone_GBps'])"
 head -12 $O/prof/run_kernel_stats.csv | cut -c1-200
 head -6 $O/prof/run_memory_copy_stats.csv
+
+T="python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu"
+timeout -k 10 600 $T tests/test_gpu_verified.py tests/test_gpu_batcher.py tests/test_gpu_protocol.py > $O/tests.log 2>&1 || { echo TESTFAIL; tail -40 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
 echo ok
