@@ -286,3 +286,14 @@ def test_value_form_defaults_to_the_joined_value():
     assert bench.parse_args([]).join is True
     assert bench.parse_args(["--row-view"]).join is False
     assert bench.parse_args(["--no-joined-leg"]).no_second_form is True
+
+
+def test_profile_files_are_taken_newest_run_first():
+    """The bench takes PMC traffic and clock files from the newest run of a
+    round: runs are lettered a..z, then aa, ab, ... (r06ae after r06h)."""
+    import bench
+    names = ["pmc_traffic_r06h_c2.json", "pmc_traffic_r06ae_c2.json", "pmc_traffic_r05b_c2.json",
+             "pmc_traffic_r06z_c2.json", "pmc_traffic_r06_c2.json", "pmc_traffic_r10a_c2.json"]
+    got = sorted(names, key=bench._run_key, reverse=True)
+    assert got == ["pmc_traffic_r10a_c2.json", "pmc_traffic_r06ae_c2.json", "pmc_traffic_r06z_c2.json",
+                   "pmc_traffic_r06h_c2.json", "pmc_traffic_r06_c2.json", "pmc_traffic_r05b_c2.json"]
