@@ -469,6 +469,9 @@ int epoch(int argc, char **argv) {
     for (int pass = 0; pass < (only_kept ? 0 : ki && kv ? 3 : 2); ++pass)
         run_pass(b, pass, pass < 2 && kv, pass == 2 ? 1 : 0,
                  pass < 2 && kv ? "verified (leaves reused)" : "full rehash");
+    if (getenv("RBC_EPOCH_ORDER_CHECK") && ki && kv && !only_kept)  // the two forms again, the other way round
+        for (int pass = 1; pass <= 2; ++pass)
+            run_pass(b, pass, pass == 2, pass == 2 ? 0 : 1, pass == 2 ? "verified (leaves reused), second" : "full rehash, second");
     rbc_batcher_destroy(b);
     if (kept) {  // ABI 7: the same handler calls with the shards kept on the device (rbc_batcher_set_keep)
         CK(rbc_batcher_create(ctx, 64, WAIT, &b));
