@@ -291,7 +291,7 @@ int validate_sweep(int argc, char **argv) {
 // the oracle check in tests/test_gpu_batcher.py.
 // `kinds` (default svi) drops request kinds for a breakdown: s = shard, v =
 // validate, i = interpolate (with v: of the ECHOs that validated).
-// With keep_mib > 0 (default 6 GiB) a fourth timed pass (after its own warm-up)
+// With keep_mib > 0 (default 8 GiB) a fourth timed pass (after its own warm-up)
 // runs the same plain calls through a batcher with rbc_batcher_set_keep: the
 // validated rows stay on the device and interpolate reads them there.
 //   tools/batcher_bench epoch [instances] [threads] [window] [max_wait_us] [dump|-] [kinds] [keep_mib]
@@ -304,7 +304,7 @@ int epoch(int argc, char **argv) {
     const int WAIT = argc > 4 ? atoi(argv[4]) : 200;
     const char *dump = argc > 5 && strcmp(argv[5], "-") ? argv[5] : nullptr;
     const char *kinds = argc > 6 ? argv[6] : "svi";
-    const size_t keep_mib = argc > 7 ? (size_t)atol(argv[7]) : 6144;  // the kept pass's device ring (0: no kept pass)
+    const size_t keep_mib = argc > 7 ? (size_t)atol(argv[7]) : 8192;  // the kept passes' device ring (0: none): three epochs
     const bool ks = strchr(kinds, 's') != nullptr, kv = strchr(kinds, 'v') != nullptr,
                ki = strchr(kinds, 'i') != nullptr;
     rbc_ctx *ctx;
