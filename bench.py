@@ -468,7 +468,7 @@ def run(args, world, rank, local_rank, wd, out):
                 "ms_per_step": round(el * 1000.0 / steps_j, 4),
                 "decoded_ok": int((res["status"] == 0).sum()), "values_ok": res["mism"] == 0,
                 "stage_ms": {kk: round(v, 4) for kk, v in sm.items()},
-                "value_form": "joined (k*S contiguous bytes per instance, assembled by the FFT re-encode)" if join2
+                "value_form": "joined (k*S contiguous bytes per instance, assembled on the device)" if join2
                 else "row view (the k data rows of the shard set, no join)",
                 "note": "secondary run after the guard, same pipelined schedule; `value` is the "
                         + ("row view" if join2 else "joined form")}
@@ -600,6 +600,7 @@ def host_fed_aggregate(per, n, S):
             "ok": all(x["ok"] for x in per), "rank0": per[0]}
 
 
+FUSED_JOIN_MIN_S = 2048  # csrc/capi.cpp kFusedJoinMinS: the FFT decode joins rows of at least this many bytes
 BATCHER_LEVELS = (1024, 8192, 32768, 88064)  # outstanding validates; 88,064 = one C2 epoch (1,024 x 86 ECHOs)
 EPOCH_WINDOW = 64  # instances each of the 16 client threads keeps in flight: all 1,024 at once, one goroutine per instance (8: 15-19 GB/s and noisy, profiles/r06z)
 
@@ -743,9 +744,11 @@ def report(args, ctx, I, n, k, d, S, present_h, corrupt_h, stage_ms, iso, elapse
     else:
         kern["sha_rows_kernel<verify>"] = ("verify", R * (S + 32 * d + 32 + 1) + I * 32, R * (bps + 2 * d))
     if pipe:
-        # + the joined value the FFT re-encode writes from the data rows it loads (k*S per instance)
+        # + the joined value the FFT re-encode writes from the data rows it loads (k*S per instance), for
+        # rows of >= FUSED_JOIN_MIN_S bytes; shorter rows are joined by join_kernel on the aux stream
         kern["decode: prepare + gf_regen_kernel + rs_fft_kernel<decode>"] = (
-            "decode", decode_bytes(n, k, S, present_h, corrupt_h) + (I * k * S if args.join else 0), 0)
+            "decode", decode_bytes(n, k, S, present_h, corrupt_h) + (I * k * S if args.join and S >= FUSED_JOIN_MIN_S
+                                                                     else 0), 0)
     pm, pmc_path = {}, None
     want_form = "joined" if args.join else "row view"
     cands = []

@@ -479,10 +479,12 @@ int ensure_ws(rbc_ctx *c, Ws &w, int count) {
 // re-encode from the data rows it loads (no separate join pass) where that
 // applies -- the FFT codec, uniform S, a value row at most 256 B longer than
 // k*S; *joined tells the caller whether it happened
-// build-time A/B: 0 = the value join always as its own kernel (on the aux stream in the receive step)
-#ifndef RBC_FUSED_JOIN
-#define RBC_FUSED_JOIN 1
-#endif
+// The FFT decode joins the value itself only for rows of at least this many
+// bytes.  Short rows (C4: 763 B, 86 unaligned row stores per lane in the
+// 256-VGPR decode) join faster as join_kernel on the receive step's aux
+// stream, beside the recheck: C4 349 -> 361 GB/s, while C1 / C2 lose 4 % that
+// way (profiles/r06am/).
+constexpr uint32_t kFusedJoinMinS = 2048;
 int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shards, uint32_t shard_pitch,
                      const uint32_t *shard_lens, uint32_t uniform_shard_len, const uint8_t *valid,
                      int32_t *status, int compare = 0, uint32_t *zeroed_counter = nullptr,
@@ -576,7 +578,8 @@ int stage_regenerate(rbc_ctx *c, Ws &w, hipStream_t st, int count, uint8_t *shar
         // tile 0's lanes zero the value's tail, 4 B each, and only the lanes
         // with a column inside the row pitch run (rs_fft.hip): the tail must
         // fit min(256, shard_pitch) bytes, else the separate join zero-fills it
-        if (RBC_FUSED_JOIN && values_out && joined && !shard_lens && value_pitch >= (uint64_t)c->k * uniform_shard_len &&
+        if (values_out && joined && !shard_lens && uniform_shard_len >= kFusedJoinMinS &&
+            value_pitch >= (uint64_t)c->k * uniform_shard_len &&
             value_pitch - (uint64_t)c->k * uniform_shard_len <= std::min<uint64_t>(256, shard_pitch)) {
             a.join = values_out;
             a.join_pitch = value_pitch;

@@ -1929,7 +1929,9 @@ def test_fused_join_zeroes_the_whole_padded_value_tail(gpu, n, f, B, tail):
     join is then not used and the separate join zero-fills it.  Every byte of
     every value row (data, then zero tail) is checked, the buffer having been
     filled with garbage first.  Rows of S bytes with S mod 4 != 0 start off a
-    dword boundary in the value, so neighbouring rows share a dword."""
+    dword boundary in the value, so neighbouring rows share a dword.  Rows
+    shorter than kFusedJoinMinS (capi.cpp) take join_kernel instead: both
+    forms are checked here."""
     I = 32
     pl = Pipeline(gpu, n, f, B, I, seed=B + tail, corrupt_frac=0.2)
     k, S = pl.k, pl.S
